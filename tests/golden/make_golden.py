@@ -1,0 +1,424 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Runs only where /root/reference exists (the build container).  It imports the
+reference's own modules from /root/reference/src -- ``binning``,
+``average_spectrum_clustering`` and ``most_similar_representative`` -- with the
+import stand-ins under tests/golden/stubs (pyteomics / pyopenms are absent
+offline; see the stub docstrings), feeds them deterministic inputs and writes
+inputs + reference outputs as data (compressed .npz without pickles, JSON, MGF).
+No reference source is copied: only values it computed.
+
+    python tests/golden/make_golden.py            # regenerate everything
+
+Fixtures:
+  bin_mean_<set>.npz        combine_bin_mean() per cluster (binning.py:170-231)
+  bin_mean_cli_in.mgf/out   binning.py main() end to end (binning.py:250-302)
+  gap_average_<set>.npz     average_spectrum() per cluster (average_spectrum_clustering.py:26-103)
+  precursor_helpers.npz     lower_median_mass & co (average_spectrum_clustering.py:106-148)
+  medoid_<set>.npz          most_similar_representative.main() reps (most_similar_representative.py:22-115)
+  pairwise_sum.npz          numpy pairwise summation (the reduction pandas .sum() runs)
+"""
+from __future__ import annotations
+
+import contextlib
+import io
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_SRC = "/root/reference/src"
+STUBS = os.path.join(HERE, "stubs")
+
+sys.path.insert(0, REPO)
+from specpride_amd.csr import SpectraCSR  # noqa: E402
+from specpride_amd.mgf import write_csr_mgf  # noqa: E402
+from specpride_amd.synthetic import make_clusters_np  # noqa: E402
+
+STATUS_OK, STATUS_MIXED_CHARGE, STATUS_NO_GAP, STATUS_EMPTY = 0, 1, 2, 3
+
+
+def _import_reference():
+    sys.path.insert(0, STUBS)
+    sys.path.insert(0, REF_SRC)
+    import binning  # noqa: F401
+    import average_spectrum_clustering  # noqa: F401
+    import most_similar_representative  # noqa: F401
+    return binning, average_spectrum_clustering, most_similar_representative
+
+
+def _csr_arrays(csr: SpectraCSR, prefix=""):
+    return {prefix + "cluster_off": csr.cluster_off, prefix + "spec_off": csr.spec_off,
+            prefix + "mz": csr.mz, prefix + "inten": csr.inten, prefix + "prec_mz": csr.prec_mz,
+            prefix + "charge": csr.charge, prefix + "rt": csr.rt}
+
+
+def _concat(parts, dtype=np.float64):
+    return np.concatenate(parts).astype(dtype) if parts else np.zeros(0, dtype)
+
+
+# ----------------------------------------------------------------- inputs
+EXAMPLE_PEAKS = [  # file_formats.md:10-52 (the only in-repo spectrum: cluster-1, 43 peaks)
+    (1.5, 8.84), (5.8, 0.75), (8.285, 1.34), (17.4, 0.32), (97.999, 1.1), (132.017, 445.98),
+    (158.996, 235.36), (169.955, 4235.4), (175.045, 518.94), (185.063, 336.05), (209.069, 186.72),
+    (260.189, 1255.96), (268.922, 159.25), (277.729, 3557.77), (286.234, 510.24), (334.264, 3129.8),
+    (339.303, 328.09), (346.855, 400.5), (350.224, 199.13), (383.827, 5392.89), (402.894, 272.86),
+    (411.354, 1636.43), (417.31, 2169.19), (420.341, 446.95), (491.367, 214.35), (519.401, 325.75),
+    (521.779, 35.4), (537.578, 32.16), (554.307, 1514.12), (592.429, 35.01), (600.643, 1.7),
+    (627.992, 6.41), (647.458, 2.33), (667.572, 61.7), (677.451, 3.69), (713.578, 0.65),
+    (761.149, 0.54), (795.495, 0.72), (808.411, 0.68), (839.005, 1.06), (850.931, 1.57),
+    (869.944, 0.86), (879.392, 0.61)]
+
+
+def _spec(mz, it, prec=500.0, z=2, rt=100.0):
+    return {"m/z array": list(map(float, mz)), "intensity array": list(map(float, it)),
+            "precursor mz": float(prec), "precursor charge": int(z), "rt": float(rt)}
+
+
+def bin_mean_edge_clusters(rng):
+    ex_mz, ex_int = zip(*EXAMPLE_PEAKS)
+    cl = []
+    cl.append([_spec(ex_mz, ex_int, 318.185, 2)])                          # single example spectrum
+    cl.append([_spec(ex_mz, ex_int, 318.185, 2),                           # example + jittered copies
+               _spec(np.array(ex_mz) + 0.004, np.array(ex_int) * 1.5, 318.19, 2),
+               _spec(np.array(ex_mz) - 0.011, np.array(ex_int) * 0.5, 318.18, 2)])
+    cl.append([_spec([150.001, 150.005, 150.011], [10, 20, 40], 400, 3),  # A.1 item 8: last wins
+               _spec([150.003], [1], 401, 3)])
+    cl.append([_spec([100.0, 99.99999, 1999.99999, 2000.0, 150.0], [1, 2, 3, 4, 5], 600, 2),  # range edges
+               _spec([100.0, 1999.99999, 2000.00001], [7, 8, 9], 600.5, 2)])
+    for n in (3, 4, 5, 7, 8, 9):                                           # quorum boundaries
+        base = np.sort(rng.uniform(100, 2000, 30))
+        sp = []
+        for k in range(n):
+            take = rng.random(30) < (0.3 + 0.7 * (k / max(1, n - 1)))
+            sp.append(_spec(np.round(base[take] + rng.normal(0, 0.004, take.sum()), 5),
+                            np.round(rng.lognormal(4, 1, take.sum()), 2), 700 + k * 0.01, 2))
+        cl.append(sp)
+    # unsorted spectra with non-adjacent duplicates in one bin (last in FILE order wins)
+    cl.append([_spec([300.011, 500.0, 300.001, 250.0, 300.013], [1, 2, 3, 4, 5], 500, 2),
+               _spec([500.001, 300.005, 250.015, 300.019], [10, 20, 30, 40], 500, 2),
+               _spec([300.0, 300.002, 499.999], [6, 7, 8], 500, 2)])
+    # an empty spectrum inside a cluster, and identical spectra
+    cl.append([_spec([], [], 420, 2), _spec([200.0, 300.0], [1, 2], 421, 2), _spec([200.0, 300.0], [1, 2], 422, 2)])
+    cl.append([_spec([123.456, 456.789], [3.0, 4.0], 333, 3)] * 4)
+    # large intensities (f32 accumulation rounding visible) and tiny ones
+    cl.append([_spec([1000.00001, 1500.5], [1.23456789e9, 3.3e-7], 900, 2),
+               _spec([1000.00002, 1500.50001], [9.87654321e8, 1.1e-7], 900, 2)])
+    return cl
+
+
+def csr_to_peaklists(csr: SpectraCSR):
+    out = []
+    for c in range(csr.n_clusters):
+        pl = []
+        for s in range(csr.cluster_off[c], csr.cluster_off[c + 1]):
+            mz, it = csr.spectrum(s)
+            pl.append({"m/z array": [float(x) for x in mz], "intensity array": [float(x) for x in it],
+                       "precursor mz": float(csr.prec_mz[s]), "precursor charge": int(csr.charge[s]),
+                       "rt": float(csr.rt[s])})
+        out.append(pl)
+    return out
+
+
+def peaklists_to_csr(clusters):
+    return SpectraCSR.from_clusters(clusters, rt_key="rt")
+
+
+# ---------------------------------------------------------------- bin-mean
+def gen_bin_mean(binning):
+    rsc = binning.RepresentativeSpectrumCreator(verbose=0)
+    rng = np.random.default_rng(101)
+    sets = {
+        "edge": (bin_mean_edge_clusters(rng), dict()),
+        "synthetic": (csr_to_peaklists(make_clusters_np(32, seed=7)), dict()),
+        "params_b": (csr_to_peaklists(make_clusters_np(16, seed=8, max_size=20)),
+                     dict(minimum=150, maximum=1500, binsize=0.05, apply_peak_quorum=False)),
+        "params_c": (csr_to_peaklists(make_clusters_np(12, seed=9, max_size=12)),
+                     dict(minimum=0, maximum=3000, binsize=0.01, apply_peak_quorum=True)),
+    }
+    mixed = [[_spec([200.0], [1.0], 400, 2), _spec([200.0], [1.0], 400, 3)],
+             [_spec([210.0, 220.0], [1.0, 2.0], 410, 2), _spec([210.0], [1.0], 410, 2)]]
+    sets["mixed_charge"] = (mixed, dict())
+    for name, (clusters, kw) in sets.items():
+        out_mz, out_int, out_off, prec, charge, status = [], [], [0], [], [], []
+        for pl in clusters:
+            try:
+                r = rsc.combine_bin_mean(pl, **kw)
+            except AssertionError:
+                status.append(STATUS_MIXED_CHARGE)
+                out_off.append(out_off[-1])
+                prec.append(np.nan)
+                charge.append(0)
+                continue
+            status.append(STATUS_OK)
+            assert r["mzs"].dtype == np.float64 and r["intensities"].dtype == np.float64
+            out_mz.append(r["mzs"])
+            out_int.append(r["intensities"])
+            out_off.append(out_off[-1] + len(r["mzs"]))
+            prec.append(float(r["precursor_mz"]))
+            charge.append(int(r["precursor_charge"]))
+        csr = peaklists_to_csr(clusters)
+        params = dict(minimum=100, maximum=2000, binsize=0.02, apply_peak_quorum=True)
+        params.update(kw)
+        np.savez_compressed(os.path.join(HERE, f"bin_mean_{name}.npz"), **_csr_arrays(csr),
+                            out_off=np.array(out_off, np.int64), out_mz=_concat(out_mz),
+                            out_int=_concat(out_int), out_prec=np.array(prec), out_charge=np.array(charge, np.int32),
+                            status=np.array(status, np.int32),
+                            params=np.array([params["minimum"], params["maximum"], params["binsize"],
+                                             float(params["apply_peak_quorum"])], np.float64))
+        print(f"bin_mean_{name}: {len(clusters)} clusters, {out_off[-1]} output peaks")
+
+
+def gen_bin_mean_cli():
+    csr = make_clusters_np(20, seed=11, n_template=40)
+    ex_mz, ex_int = zip(*EXAMPLE_PEAKS)
+    extra = SpectraCSR.from_clusters([[_spec(ex_mz, ex_int, 318.185, 2), _spec(ex_mz, ex_int, 318.185, 2)]],
+                                     cluster_ids=["cluster-ex"], rt_key="rt")
+    in_path = os.path.join(HERE, "bin_mean_cli_in.mgf")
+    out_path = os.path.join(HERE, "bin_mean_cli_out.mgf")
+    with open(in_path, "w") as fh:
+        write_csr_mgf(csr, fh)
+        # a second run of cluster-3 after the others (binning.py merges by id: A.4)
+        extra_titles = [f"cluster-ex;mzspec:PXD004732:ex.raw:scan:{k}" for k in range(2)]
+        write_csr_mgf(extra, fh, titles=extra_titles, sequences=["VLHPLEGAVVIIFK/2", ""])
+        late = csr.select([3])
+        write_csr_mgf(late, fh, titles=[f"cluster-3;mzspec:PXDSYN:synthetic:scan:late{k}"
+                                        for k in range(late.n_spectra)])
+    env = dict(os.environ, PYTHONPATH=STUBS)
+    with tempfile.TemporaryDirectory() as td:
+        r = subprocess.run([sys.executable, os.path.join(REF_SRC, "binning.py"), "--mgf_file", in_path,
+                            "--out", os.path.join(td, "out.mgf")], env=env, cwd=td, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr)
+        with open(os.path.join(td, "out.mgf")) as src, open(out_path, "w") as dst:
+            dst.write(src.read())
+        r2 = subprocess.run([sys.executable, os.path.join(REF_SRC, "binning.py")], env=env, cwd=td,
+                            capture_output=True, text=True)
+    with open(os.path.join(HERE, "bin_mean_cli.json"), "w") as fh:
+        json.dump({"stdout": r.stdout, "no_args_returncode": r2.returncode, "no_args_stdout": r2.stdout}, fh, indent=1)
+    print("bin_mean_cli: ok", os.path.getsize(in_path), os.path.getsize(out_path))
+
+
+# ------------------------------------------------------------- gap-average
+def gap_edge_clusters(rng):
+    S = lambda mz, it: {"m/z array": np.array(mz, float), "intensity array": np.array(it, float)}  # noqa: E731
+    cl = []
+    cl.append([S([500.0, 100.0, 300.0], [5.0, 1.0, 0.001])])                       # n=1 passthrough (unsorted)
+    cl.append([S([100.0, 100.001], [1, 2]), S([100.002], [3])])                     # one group -> IndexError
+    cl.append([S([100.0, 200.0], [1, 2]), S([100.001, 200.001], [3, 4])])           # two groups
+    cl.append([S([100.0, 200.0, 300.0], [1, 2, 3]), S([100.001, 200.001, 300.001], [1, 2, 3])])  # merge quirk
+    cl.append([S([100, 150, 200, 250, 300, 350], [1, 2, 3, 4, 5, 6]),
+               S([100.005, 200.005, 300.005], [1, 1, 1]), S([150.002, 350.001], [9, 9])])     # min_fraction drops
+    cl.append([S([100.0, 300.0], [1, 1]), S([200.0, 400.0], [1, 1]), S([500.0], [1])])        # merged tail survives
+    cl.append([S([100.0], [1]), S([200.0], [1]), S([300.0], [1]), S([400.0], [1]), S([500.0], [1])])  # all dropped -> ValueError
+    cl.append([S([100.0, 200.0, 300.0, 400.0], [1000.0, 1.0, 0.999, 500.0]),
+               S([100.0, 200.0, 300.0, 400.0], [1000.0, 1.0, 1.001, 500.0])])  # dyn-range: 2000/1000 = 2.0 boundary
+    cl.append([S([], []), S([], [])])                                               # no peaks -> IndexError
+    cl.append([S([], [])])                                                          # n=1 empty -> ValueError
+    cl.append([S([100.0, 100.0, 100.0, 200.0], [1, 2, 3, 4]), S([100.0, 200.0], [5, 6])])  # mz ties
+    cl.append([S([100.00, 100.01, 100.02, 100.035], [1, 2, 3, 4]), S([100.005, 100.03], [5, 6])])  # gaps ~ acc
+    big = rng.uniform(100, 2000, 40)
+    cl.append([S(np.round(np.sort(big + rng.normal(0, 0.002, 40)), 5), np.round(rng.lognormal(5, 1.5, 40), 2))
+               for _ in range(6)])
+    return cl
+
+
+def _pyteo_spectra(csr: SpectraCSR):
+    out = []
+    for c in range(csr.n_clusters):
+        sp = []
+        for s in range(csr.cluster_off[c], csr.cluster_off[c + 1]):
+            mz, it = csr.spectrum(s)
+            sp.append({"m/z array": mz.copy(), "intensity array": it.copy(),
+                       "params": {"title": f"cluster-{c};scan:{s}", "pepmass": (float(csr.prec_mz[s]), None),
+                                  "charge": [int(csr.charge[s])], "rtinseconds": float(csr.rt[s])}})
+        out.append(sp)
+    return out
+
+
+def gen_gap_average(asc):
+    rng = np.random.default_rng(202)
+    sets = {
+        "edge": (gap_edge_clusters(rng), dict()),
+        "synthetic": (_pyteo_spectra(make_clusters_np(32, seed=17)), dict()),
+        "params_b": (_pyteo_spectra(make_clusters_np(16, seed=18, max_size=20)),
+                     dict(mz_accuracy=0.02, dyn_range=100, min_fraction=0.3)),
+        "params_c": (_pyteo_spectra(make_clusters_np(12, seed=19, max_size=30)),
+                     dict(mz_accuracy=0.005, dyn_range=10000, min_fraction=0.75)),
+    }
+    for name, (clusters, kw) in sets.items():
+        out_mz, out_int, out_off, status = [], [], [0], []
+        for sp in clusters:
+            try:
+                r = asc.average_spectrum(sp, "t", **kw)
+            except IndexError:
+                status.append(STATUS_NO_GAP)
+                out_off.append(out_off[-1])
+                continue
+            except ValueError:
+                status.append(STATUS_EMPTY)
+                out_off.append(out_off[-1])
+                continue
+            status.append(STATUS_OK)
+            out_mz.append(np.asarray(r["m/z array"], np.float64))
+            out_int.append(np.asarray(r["intensity array"], np.float64))
+            out_off.append(out_off[-1] + len(r["m/z array"]))
+        csr = SpectraCSR.from_clusters(clusters)
+        p = dict(mz_accuracy=asc.DIFF_THRESH, dyn_range=asc.DYN_RANGE, min_fraction=asc.MIN_FRACTION)
+        p.update(kw)
+        np.savez_compressed(os.path.join(HERE, f"gap_average_{name}.npz"), **_csr_arrays(csr),
+                            out_off=np.array(out_off, np.int64), out_mz=_concat(out_mz), out_int=_concat(out_int),
+                            status=np.array(status, np.int32),
+                            params=np.array([p["mz_accuracy"], p["dyn_range"], p["min_fraction"]], np.float64))
+        print(f"gap_average_{name}: {len(clusters)} clusters, {out_off[-1]} output peaks, status {status[:12]}")
+
+
+def gen_precursor_helpers(asc):
+    csr = make_clusters_np(40, seed=23, max_size=9, n_template=5)
+    csr.charge[csr.cluster_off[5]] = 3 if csr.charge[csr.cluster_off[5]] == 2 else 2  # one mixed-charge cluster
+    clusters = _pyteo_spectra(csr)
+    res = {k: [] for k in ("lm_mz", "lm_z", "lm_rt", "na_mz", "na_z", "na_status", "ne_mz", "ne_z", "med_rt")}
+    for sp in clusters:
+        m, z = asc.lower_median_mass(sp)
+        res["lm_mz"].append(m)
+        res["lm_z"].append(z)
+        res["lm_rt"].append(asc.lower_median_mass_rt(sp))
+        try:
+            m, z = asc.naive_average_mass_and_charge(sp)
+            res["na_mz"].append(m)
+            res["na_z"].append(z)
+            res["na_status"].append(0)
+        except ValueError:
+            res["na_mz"].append(np.nan)
+            res["na_z"].append(0)
+            res["na_status"].append(1)
+        m, z = asc.neutral_average_mass_and_charge(sp)
+        res["ne_mz"].append(m)
+        res["ne_z"].append(z)
+        res["med_rt"].append(float(asc.median_rt(sp)))
+    np.savez_compressed(os.path.join(HERE, "precursor_helpers.npz"), **_csr_arrays(csr),
+                        **{k: np.array(v) for k, v in res.items()}, H=np.array(asc.H))
+    print("precursor_helpers: ok")
+
+
+# ------------------------------------------------------------------ medoid
+def medoid_cases():
+    sizes = [1, 2, 3, 9, 17, 130, 300, 5, 4, 33, 64, 65, 7, 8, 129]
+    csr = make_clusters_np(len(sizes), seed=31, sizes=np.array(sizes), n_template=60)
+    clusters = [[(m.copy(), i.copy()) for (m, i) in csr.cluster(c)] for c in range(csr.n_clusters)]
+    prec = [[float(csr.prec_mz[s]) for s in range(csr.cluster_off[c], csr.cluster_off[c + 1])]
+            for c in range(csr.n_clusters)]
+    # identical spectra (ties -> lowest index) and a spectrum with two peaks in one 0.1 bin
+    base_mz = np.array([200.01, 300.02, 400.03, 500.04])
+    clusters.append([(base_mz.copy(), np.ones(4)) for _ in range(5)])
+    prec.append([500.0] * 5)
+    clusters.append([(np.array([200.01, 200.05, 300.0]), np.ones(3)), (np.array([200.03, 300.0]), np.ones(2)),
+                     (np.array([200.09, 300.02, 300.07, 450.0]), np.ones(4)), (np.array([450.0]), np.ones(1))])
+    prec.append([500.0] * 4)
+    big = make_clusters_np(1, seed=32, sizes=np.array([1000]), n_template=30)
+    clusters.append([(m.copy(), i.copy()) for (m, i) in big.cluster(0)])
+    prec.append([float(x) for x in big.prec_mz])
+    return clusters, prec
+
+
+def _write_medoid_mgf(path, order):
+    """order: list of (cluster_name, mz, inten, prec, scan)."""
+    with open(path, "w") as fh:
+        for name, mz, it, p, scan in order:
+            fh.write(f"BEGIN IONS\nTITLE={name};mzspec:PXDSYN:synthetic:scan:{scan}\nPEPMASS={p!r}\nCHARGE=2+\n")
+            fh.write("".join(f"{float(a)!r} {float(b)!r}\n" for a, b in zip(mz, it)))
+            fh.write("END IONS\n\n")
+
+
+def _run_medoid_main(msr, in_path):
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "out.txt")
+        with contextlib.redirect_stdout(io.StringIO()):
+            msr.main(["-i", in_path, "-o", out])
+        with open(out) as fh:
+            rows = [ln.rstrip("\n").split("\t") for ln in fh if ln.strip()]
+    return [(int(i), t) for i, t in rows]
+
+
+def gen_medoid(msr):
+    clusters, prec = medoid_cases()
+    order, scan = [], 0
+    for c, (sp, pr) in enumerate(zip(clusters, prec)):
+        for (mz, it), p in zip(sp, pr):
+            order.append((f"cluster-{c}", mz, it, p, scan))
+            scan += 1
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "in.mgf")
+        _write_medoid_mgf(path, order)
+        reps = _run_medoid_main(msr, path)
+    csr = SpectraCSR.from_clusters([[{"m/z array": m, "intensity array": i} for (m, i) in sp] for sp in clusters])
+    np.savez_compressed(os.path.join(HERE, "medoid_main.npz"), **_csr_arrays(csr),
+                        rep_index=np.array([r[0] for r in reps], np.int64))
+    print("medoid_main:", [r[0] for r in reps])
+
+    # non-contiguous cluster order (A.4): A A B A C C B D -> first runs only
+    rng = np.random.default_rng(33)
+    names = ["A", "A", "B", "A", "C", "C", "B", "D", "D", "D", "A"]
+    order = []
+    for k, nm in enumerate(names):
+        mz = np.round(np.sort(rng.uniform(100, 600, 12)), 3)
+        order.append((nm, mz, np.ones(12), 400.0 + k, k))
+    for k in (1, 3):  # make some members similar so the choice is non-trivial
+        order[k] = (order[k][0], order[0][1].copy(), np.ones(12), order[k][3], k)
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "in.mgf")
+        _write_medoid_mgf(path, order)
+        reps = _run_medoid_main(msr, path)
+        with open(path) as fh:
+            mgf_text = fh.read()
+    with open(os.path.join(HERE, "medoid_noncontiguous.mgf"), "w") as fh:
+        fh.write(mgf_text)
+    with open(os.path.join(HERE, "medoid_noncontiguous.json"), "w") as fh:
+        json.dump({"names": names, "rep_index": [r[0] for r in reps], "titles": [r[1] for r in reps]}, fh, indent=1)
+    print("medoid_noncontiguous:", reps)
+
+
+def gen_pairwise():
+    """numpy/pandas pairwise-summation tree (what `.iloc[i,:].sum()` evaluates,
+    most_similar_representative.py:98-100): random vectors with zeros kept in
+    place, several lengths crossing the n<8 / n<=128 / recursive-split regimes."""
+    import pandas as pd
+
+    rng = np.random.default_rng(44)
+    lens = [1, 2, 5, 7, 8, 9, 15, 16, 17, 31, 64, 127, 128, 129, 130, 200, 255, 256, 257, 300, 1000, 1031, 4097]
+    vals, offs, sums_np, sums_pd = [], [0], [], []
+    for n in lens:
+        v = rng.random(n) * (10.0 ** rng.uniform(-3, 3, n))
+        v[rng.random(n) < 0.3] = 0.0
+        vals.append(v)
+        offs.append(offs[-1] + n)
+        sums_np.append(np.add.reduce(v))
+        m = np.zeros((n, n))
+        m[0, :] = v
+        sums_pd.append(pd.DataFrame(m).iloc[0, :].sum())
+    assert all(a == b for a, b in zip(sums_np, sums_pd))
+    np.savez_compressed(os.path.join(HERE, "pairwise_sum.npz"), off=np.array(offs, np.int64),
+                        vals=np.concatenate(vals), sums=np.array(sums_np))
+    print("pairwise_sum: ok")
+
+
+def main():
+    if not os.path.isdir(REF_SRC):
+        raise SystemExit("reference not present; fixtures are committed under tests/golden/")
+    binning, asc, msr = _import_reference()
+    gen_bin_mean(binning)
+    gen_bin_mean_cli()
+    gen_gap_average(asc)
+    gen_precursor_helpers(asc)
+    gen_pairwise()
+    gen_medoid(msr)
+
+
+if __name__ == "__main__":
+    main()
