@@ -1,0 +1,146 @@
+/*
+ * specpride.h -- C-ABI of the MI355X consensus/representative-spectrum engine
+ * (libspecpride_hip.so, built from specpride_amd/csrc for gfx950).
+ *
+ * The reference (timosachsenberg/specpride) has no FFI: its hot path is three
+ * Python functions.  Each entry point below replaces one of them for a whole
+ * batch of clusters at once; the Python shims in specpride_amd/ keep the
+ * reference's own names and call these through ctypes.
+ *
+ *   spx_bin_mean     <- src/binning.py:170-231  RepresentativeSpectrumCreator.combine_bin_mean
+ *                       (called per cluster from binning.py:291-297)
+ *   spx_gap_average  <- src/average_spectrum_clustering.py:26-103  average_spectrum
+ *                       + precursor helpers :106-148 (called from :151-165)
+ *   spx_medoid       <- src/most_similar_representative.py:13-19 distance() and the
+ *                       per-cluster medoid loop :60-111
+ *   spx_compact_peaks   (packing helper for the shims' output writers)
+ *
+ * Conventions
+ *   - Every array pointer inside spx_csr / outputs is a DEVICE pointer (HBM),
+ *     owned by the caller.  The library owns nothing but the workspace contents
+ *     while a call runs; size the workspace with the *_workspace_size queries.
+ *   - Work is enqueued on `stream` (a hipStream_t, passed as void*; NULL = the
+ *     default stream) and is asynchronous.  Entry points are reentrant (no
+ *     global mutable state) and never allocate or synchronise, so they can be
+ *     captured into a hipGraph.  The caller selects the device.
+ *   - Return value: SPX_SUCCESS or a negative spx_error.  Per-cluster outcomes
+ *     are reported in `status[c]` (spx_status) -- the shims raise the
+ *     reference's exception type for the first failing cluster in order.
+ *   - Peak outputs use the cluster's INPUT peak range as capacity: cluster c
+ *     writes count[c] peaks at out->mz/inten[spec_off[cluster_off[c]] + k], so
+ *     the out arrays have n_peaks entries and no planning pass is needed.
+ */
+#ifndef SPECPRIDE_H_
+#define SPECPRIDE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPX_ABI_VERSION 1
+
+typedef enum spx_error {
+  SPX_SUCCESS = 0,
+  SPX_EINVAL = -1,   /* bad argument (null pointer, inconsistent sizes) */
+  SPX_EHIP = -2,     /* a HIP launch/runtime call failed */
+  SPX_ENOSPACE = -3  /* workspace smaller than the matching *_workspace_size */
+} spx_error;
+
+typedef enum spx_status {
+  SPX_OK = 0,
+  SPX_MIXED_CHARGE = 1, /* binning.py:205-206 AssertionError / :131 ValueError   */
+  SPX_NO_GAP = 2,       /* average_spectrum_clustering.py:69 IndexError          */
+  SPX_EMPTY = 3,        /* average_spectrum_clustering.py:95 ValueError (max())  */
+  SPX_NON_FINITE = 4,   /* NaN/inf m/z or intensity in a gap-average cluster     */
+  SPX_UNRESOLVED = 100  /* outside the engine's limits            */
+} spx_status;
+
+/* Cluster-segmented CSR batch (device pointers).  Clusters are [cluster_off[c],
+ * cluster_off[c+1]) in spectra; spectra are [spec_off[s], spec_off[s+1]) in peaks;
+ * peaks in file order (not re-sorted).  rt may be NULL except for spx_gap_average. */
+typedef struct spx_csr {
+  int64_t n_clusters, n_spectra, n_peaks;
+  const int64_t *cluster_off; /* [n_clusters + 1] */
+  const int64_t *spec_off;    /* [n_spectra + 1]  */
+  const double *mz;           /* [n_peaks] */
+  const double *inten;        /* [n_peaks] */
+  const double *prec_mz;      /* [n_spectra] */
+  const int32_t *charge;      /* [n_spectra] */
+  const double *rt;           /* [n_spectra] or NULL */
+} spx_csr;
+
+/* Host-side facts about the batch that size the workspace (any upper bound works). */
+typedef struct spx_batch_info {
+  int64_t max_cluster_peaks;   /* max over clusters of its peak count */
+  int64_t max_cluster_spectra; /* max over clusters of its spectrum count */
+  double max_mz_span;          /* max over clusters of (max m/z - min m/z); 0 = 5000 Da */
+} spx_batch_info;
+
+typedef struct spx_peaks_out {
+  double *mz;     /* [n_peaks] capacity, see "Peak outputs" above */
+  double *inten;  /* [n_peaks] */
+  int64_t *count; /* [n_clusters] peaks written per cluster */
+} spx_peaks_out;
+
+/* ---- bin-mean: RepresentativeSpectrumCreator.combine_bin_mean(peaklists,
+ *      minimum=100, maximum=2000, binsize=0.02, apply_peak_quorum=True) ---- */
+typedef struct spx_bin_params {
+  double minimum, maximum, binsize;
+  int32_t apply_peak_quorum;
+} spx_bin_params;
+
+size_t spx_bin_mean_workspace_size(const spx_csr *csr, const spx_bin_params *params,
+                                   const spx_batch_info *info);
+/* prec_out[c] = np.mean(precursor m/z), charge_out[c] = charge of the cluster. */
+int spx_bin_mean(const spx_csr *csr, const spx_bin_params *params, const spx_batch_info *info,
+                 spx_peaks_out *out, double *prec_out, int32_t *charge_out, int32_t *status,
+                 void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---- gap-average: average_spectrum(spectra, title, pepmass, rtinseconds, charge,
+ *      mz_accuracy=0.01, dyn_range=1000, min_fraction=0.5) + precursor helpers ---- */
+typedef enum spx_pepmass_mode { SPX_PEPMASS_LOWER_MEDIAN = 0, SPX_PEPMASS_NAIVE_AVERAGE = 1,
+                                SPX_PEPMASS_NEUTRAL_AVERAGE = 2 } spx_pepmass_mode;
+typedef enum spx_rt_mode { SPX_RT_MEDIAN = 0, SPX_RT_MASS_LOWER_MEDIAN = 1 } spx_rt_mode;
+
+typedef struct spx_gap_params {
+  double mz_accuracy, dyn_range, min_fraction;
+  double proton;        /* pyteomics nist_mass['H+'][0][0] = 1.00727646677 */
+  int32_t pepmass_mode; /* spx_pepmass_mode */
+  int32_t rt_mode;      /* spx_rt_mode */
+} spx_gap_params;
+
+size_t spx_gap_average_workspace_size(const spx_csr *csr, const spx_gap_params *params,
+                                      const spx_batch_info *info);
+int spx_gap_average(const spx_csr *csr, const spx_gap_params *params, const spx_batch_info *info,
+                    spx_peaks_out *out, double *pepmass_out, int32_t *charge_out, double *rt_out,
+                    int32_t *status, void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---- medoid: most_similar_representative.py distance(s1, s2, 'xcorr') with
+ *      XQuestScores().xCorrelationPrescore(s1, s2, 0.1) + argmin of summed distance ---- */
+typedef struct spx_medoid_params {
+  double tolerance; /* 0.1 at most_similar_representative.py:15 */
+} spx_medoid_params;
+
+/* Needs the HOST copies of the offsets: the large-cluster arena is sized from them. */
+size_t spx_medoid_workspace_size(const int64_t *host_cluster_off, const int64_t *host_spec_off,
+                                 int64_t n_clusters);
+/* rep[c] = global index of the chosen spectrum (-1 empty cluster, <= -2 unresolved);
+ * totals (nullable) [n_spectra] = the reference's total_dist per spectrum. */
+int spx_medoid(const spx_csr *csr, const spx_medoid_params *params, int64_t *rep, double *totals,
+               void *workspace, size_t workspace_bytes, void *stream);
+
+/* Pack the per-cluster outputs densely: dst[out_off[c] + k] = src[spec_off[cluster_off[c]] + k]
+ * for k < count[c]; out_off is the exclusive prefix sum of count (device array [C+1]). */
+int spx_compact_peaks(const spx_csr *csr, const spx_peaks_out *src, const int64_t *out_off,
+                      double *dst_mz, double *dst_inten, void *stream);
+
+int spx_abi_version(void);
+const char *spx_last_error(void); /* thread-local text of the last failure */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPECPRIDE_H_ */

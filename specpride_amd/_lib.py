@@ -1,0 +1,119 @@
+"""ctypes binding of libspecpride_hip.so (the C-ABI in include/specpride.h).
+
+The library is built in-tree (``specpride_amd/lib/libspecpride_hip.so``) by
+:func:`build` / ``__graft_entry__.build()``.  There is no fallback: if the
+library is missing or fails to load, :func:`lib` raises -- the product path
+never silently degrades to a CPU implementation.
+
+torch is imported before the library is loaded so that both share the one HIP
+runtime (libamdhip64.so.7) that torch already mapped.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_DIR = os.path.join(HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libspecpride_hip.so")
+CSRC = os.path.join(HERE, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("SPX_OFFLOAD_ARCH", "gfx950")
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+             f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+
+_p = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_dbl = ctypes.c_double
+_sz = ctypes.c_size_t
+
+
+class SpxCsr(ctypes.Structure):
+    _fields_ = [("n_clusters", _i64), ("n_spectra", _i64), ("n_peaks", _i64),
+                ("cluster_off", _p), ("spec_off", _p), ("mz", _p), ("inten", _p),
+                ("prec_mz", _p), ("charge", _p), ("rt", _p)]
+
+
+class SpxBatchInfo(ctypes.Structure):
+    _fields_ = [("max_cluster_peaks", _i64), ("max_cluster_spectra", _i64), ("max_mz_span", _dbl)]
+
+
+class SpxPeaksOut(ctypes.Structure):
+    _fields_ = [("mz", _p), ("inten", _p), ("count", _p)]
+
+
+class SpxBinParams(ctypes.Structure):
+    _fields_ = [("minimum", _dbl), ("maximum", _dbl), ("binsize", _dbl), ("apply_peak_quorum", _i32)]
+
+
+class SpxGapParams(ctypes.Structure):
+    _fields_ = [("mz_accuracy", _dbl), ("dyn_range", _dbl), ("min_fraction", _dbl), ("proton", _dbl),
+                ("pepmass_mode", _i32), ("rt_mode", _i32)]
+
+
+class SpxMedoidParams(ctypes.Structure):
+    _fields_ = [("tolerance", _dbl)]
+
+
+# every symbol include/specpride.h declares (checked by tests/test_abi.py)
+EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_gap_average_workspace_size", "spx_gap_average",
+            "spx_medoid_workspace_size", "spx_medoid", "spx_compact_peaks", "spx_abi_version", "spx_last_error"]
+
+SPX_ABI_VERSION = 1
+_lib = None
+
+
+def sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp")))
+
+
+def build(force: bool = False) -> str:
+    """Compile the HIP engine for gfx950 into specpride_amd/lib (cross-compiles without a GPU)."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    newest = max(os.path.getmtime(f) for f in sources() + [os.path.join(REPO, "include", "specpride.h")])
+    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= newest:
+        return LIB_PATH
+    tmp = LIB_PATH + ".tmp"
+    cmd = [HIPCC, *HIP_FLAGS, "-o", tmp, os.path.join(CSRC, "spx_api.hip")]
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def lib():
+    """Load (once) and return the engine library; raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- share torch's HIP runtime (see module docstring)
+
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"specpride HIP engine not built: {LIB_PATH} is missing "
+                           "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.spx_abi_version.restype = ctypes.c_int
+    L.spx_last_error.restype = ctypes.c_char_p
+    L.spx_bin_mean_workspace_size.restype = _sz
+    L.spx_bin_mean_workspace_size.argtypes = [_p, _p, _p]
+    L.spx_bin_mean.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]
+    L.spx_gap_average_workspace_size.restype = _sz
+    L.spx_gap_average_workspace_size.argtypes = [_p, _p, _p]
+    L.spx_gap_average.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]
+    L.spx_medoid_workspace_size.restype = _sz
+    L.spx_medoid_workspace_size.argtypes = [_p, _p, _i64]
+    L.spx_medoid.argtypes = [_p, _p, _p, _p, _p, _sz, _p]
+    L.spx_compact_peaks.argtypes = [_p, _p, _p, _p, _p, _p]
+    if L.spx_abi_version() != SPX_ABI_VERSION:
+        raise RuntimeError(f"libspecpride_hip ABI {L.spx_abi_version()} != {SPX_ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().spx_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,277 @@
+// Segmented bin-mean consensus (reference: src/binning.py:170-231, combine_bin_mean;
+// exact semantics restated in SURVEY.md Appendix A.1 and oracle/np_oracle.py).
+//
+// One 256-thread workgroup (4 waves) per cluster.  The reference's dense
+// 95,001-bin float32 histogram does not fit LDS, so the cluster is processed
+// as a sparse, *ordered* histogram:
+//
+//   phase 1  (all peaks in parallel)  mark every occupied bin in an LDS bitmap
+//            (1 bit per bin, 95,001 bins = 11.9 KB; ds_or_b64)
+//   phase 2  exclusive popcount prefix per 64-bit word -> each occupied bin gets a
+//            compact slot id in ASCENDING bin order (D slots, D << #bins)
+//   phase 3  spectra in file order, peaks of one spectrum in parallel: the last
+//            peak of the spectrum in each bin (numpy fancy-index "+=" keeps the
+//            last, binning.py:197-199) updates its slot:
+//               cnt += 1;  I = f32(f64(I) + inten);  M = f32(f64(M) + mz)
+//            Spectrum order is the reference's float32 accumulation order, so the
+//            result is bit-exact; a barrier separates consecutive spectra.
+//            "Last in bin" is a neighbour compare for m/z-sorted spectra (the
+//            MGF norm); an unsorted spectrum (voted block-wide) takes an
+//            owner-tag path (LDS atomicMax of the peak position per slot).
+//   phase 4  slots with cnt >= int(0.25 n)+1 and a non-NaN mean are written in
+//            slot (= bin) order: mz = f64(M)/cnt, int = f64(I)/cnt.
+//
+// Bins are trunc(fl((mz - min)/binsize)) computed exactly (spx_device.hpp).
+// Clusters that do not fit the LDS budget (bins, distinct bins, > 128 spectra)
+// are appended to a deferred list and finished by bin_mean_global_kernel, the
+// same body with its state in a per-workgroup global scratch slice.
+//
+// HBM traffic per cluster: mz + inten once from HBM (16 B/peak; phase 3 re-reads
+// the m/z that phase 1 pulled into L2/MALL), 16 B per output peak, offsets.
+#include "spx_device.hpp"
+
+namespace spx {
+
+struct BinMeanParams {
+  double minimum, maximum, binsize, inv_binsize;
+  int32_t apply_quorum;
+  int32_t n_words;  // ceil(n_bins / 64)
+};
+
+template <class PrefixT>
+struct BinMeanState {
+  unsigned long long* bitmap;
+  PrefixT* wprefix;
+  uint32_t* cnt;
+  float* acc_i;
+  float* acc_m;
+  uint32_t* owner;
+  int dcap;
+  int nmax;  // clusters with more spectra are deferred (leaf-only pairwise mean)
+};
+
+constexpr int BM_BLOCK = 256;
+constexpr int BM_WMAX = 1536;  // 98,304 bins
+constexpr int BM_DCAP = 1536;  // distinct occupied bins per cluster
+constexpr int BM_NMAX = 128;
+
+struct BinMeanSmem {
+  unsigned long long bitmap[BM_WMAX];
+  uint16_t wprefix[BM_WMAX];
+  uint32_t cnt[BM_DCAP];
+  float acc_i[BM_DCAP];
+  float acc_m[BM_DCAP];
+  uint32_t owner[BM_DCAP];
+  int tmp[BM_BLOCK / kWave + 1];
+  int flag;
+};
+
+struct PeakLane {
+  double m, it, mn;  // m/z, intensity, m/z of the next peak in the spectrum
+  bool active, has_next;
+};
+
+__device__ __forceinline__ bool in_range(double m, const BinMeanParams& P) {
+  return m >= P.minimum && m < P.maximum;
+}
+
+__device__ __forceinline__ int64_t bin_of(double m, const BinMeanParams& P) {
+  return trunc_div_exact(m - P.minimum, P.binsize, P.inv_binsize);
+}
+
+__device__ __forceinline__ PeakLane load_lane(const CsrView& v, int64_t k, int64_t e) {
+  PeakLane L;
+  L.active = k < e;
+  L.has_next = k + 1 < e;
+  L.m = L.active ? v.mz[k] : 0.0;
+  L.it = L.active ? v.inten[k] : 0.0;
+  L.mn = L.has_next ? v.mz[k + 1] : 0.0;
+  return L;
+}
+
+template <class PrefixT>
+__device__ __forceinline__ void accumulate(const BinMeanState<PrefixT>& S, int slot, double m, double it) {
+  S.cnt[slot] += 1u;
+  S.acc_i[slot] = (float)((double)S.acc_i[slot] + it);
+  S.acc_m[slot] = (float)((double)S.acc_m[slot] + m);
+}
+
+// Processes one spectrum chunk lane on the sorted path.
+template <class PrefixT>
+__device__ __forceinline__ void sorted_lane(const BinMeanState<PrefixT>& S, const BinMeanParams& P,
+                                            const PeakLane& L) {
+  if (!L.active || !in_range(L.m, P)) return;
+  const int64_t b = bin_of(L.m, P);
+  if (L.has_next && in_range(L.mn, P) && bin_of(L.mn, P) == b) return;  // a later peak owns the bin
+  accumulate(S, bitmap_rank(S.bitmap, S.wprefix, b), L.m, L.it);
+}
+
+template <bool kSmall, class PrefixT>
+__device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const BinMeanState<PrefixT>& S,
+                                 int64_t c, const PeaksOut& out, double* prec_out, int32_t* charge_out,
+                                 int* tmp, int* flag) {
+  const int tid = threadIdx.x;
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1], n = s1 - s0;
+  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
+  if (n == 0) {
+    if (tid == 0) { out.count[c] = 0; prec_out[c] = __longlong_as_double(0x7ff8000000000000ll); charge_out[c] = 0; }
+    return kEmpty;
+  }
+  if (n > S.nmax || P.n_words > (kSmall ? BM_WMAX : 0x7fffffff)) return kDeferred;
+
+  // charge check (binning.py:205-206) -- nothing is emitted for a mixed cluster
+  const int32_t z0 = v.charge[s0];
+  int mixed = 0;
+  for (int64_t s = s0 + 1 + tid; s < s1; s += BM_BLOCK) mixed |= v.charge[s] != z0;
+  for (int w = tid; w < P.n_words; w += BM_BLOCK) S.bitmap[w] = 0ull;
+  if (__syncthreads_or(mixed)) {
+    if (tid == 0) { out.count[c] = 0; prec_out[c] = __longlong_as_double(0x7ff8000000000000ll); charge_out[c] = 0; }
+    return kMixedCharge;
+  }
+
+  // phase 1: occupied-bin bitmap
+  for (int64_t k = p0 + tid; k < p1; k += BM_BLOCK) {
+    const double m = v.mz[k];
+    if (in_range(m, P)) {
+      const int64_t b = bin_of(m, P);
+      atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
+    }
+  }
+  __syncthreads();
+
+  // phase 2: compact slot ids in bin order
+  const int D = bitmap_prefix<BM_BLOCK>(S.bitmap, S.wprefix, P.n_words, tmp);
+  if (D > S.dcap) return kDeferred;
+  for (int d = tid; d < D; d += BM_BLOCK) {
+    S.cnt[d] = 0u;
+    S.acc_i[d] = 0.0f;
+    S.acc_m[d] = 0.0f;
+  }
+  if (tid == 0) *flag = 0;  // owner tags not yet initialised
+  __syncthreads();
+
+  // phase 3: ordered accumulation, one spectrum at a time
+  for (int64_t s = s0; s < s1; ++s) {
+    const int64_t a = v.spec_off[s], e = v.spec_off[s + 1];
+    if (e - a <= BM_BLOCK) {
+      const PeakLane L = load_lane(v, a + tid, e);
+      const int unsorted = L.active && L.has_next && !(L.m <= L.mn);
+      if (!__syncthreads_or(unsorted)) {
+        sorted_lane(S, P, L);
+        continue;
+      }
+    } else {
+      int unsorted = 0;
+      for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
+        const PeakLane L = load_lane(v, k, e);
+        unsorted |= L.active && L.has_next && !(L.m <= L.mn);
+      }
+      if (!__syncthreads_or(unsorted)) {
+        for (int64_t k = a + tid; k < e; k += BM_BLOCK) sorted_lane(S, P, load_lane(v, k, e));
+        continue;
+      }
+    }
+    // unsorted spectrum: the highest file position per slot wins (tags grow
+    // monotonically through the cluster, so stale tags never win)
+    if (*flag == 0) {
+      for (int d = tid; d < D; d += BM_BLOCK) S.owner[d] = 0u;
+      __syncthreads();
+      if (tid == 0) *flag = 1;
+    }
+    for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
+      const double m = v.mz[k];
+      if (in_range(m, P)) atomicMax(&S.owner[bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P))], (uint32_t)(k - p0 + 1));
+    }
+    __syncthreads();
+    for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
+      const double m = v.mz[k];
+      if (!in_range(m, P)) continue;
+      const int slot = bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P));
+      if (S.owner[slot] == (uint32_t)(k - p0 + 1)) accumulate(S, slot, m, v.inten[k]);
+    }
+  }
+  __syncthreads();
+
+  // phase 4: quorum filter and ordered output (binning.py:181-183, 209-222)
+  const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
+  const int per = (D + BM_BLOCK - 1) / BM_BLOCK;
+  const int d0 = tid * per;
+  int mine = 0;
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d < D && S.cnt[d] >= quorum && !isnan((double)S.acc_i[d] / (double)S.cnt[d])) ++mine;
+  }
+  int total;
+  int o = block_exclusive_scan<BM_BLOCK>(mine, tmp, total);
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d < D && S.cnt[d] >= quorum) {
+      const double cn = (double)S.cnt[d];
+      const double mi = (double)S.acc_i[d] / cn;
+      if (isnan(mi)) continue;
+      out.inten[p0 + o] = mi;
+      out.mz[p0 + o] = S.acc_m[d] == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)S.acc_m[d] / cn;
+      ++o;
+    }
+  }
+  if (tid == 0) {
+    out.count[c] = total;
+    charge_out[c] = z0;
+    // np.mean of the precursor list (binning.py:224): pairwise sum / n
+    const double* pr = v.prec_mz + s0;
+    const double sum = kSmall ? pw_sum_small([&](int64_t j) { return pr[j]; }, n)
+                              : pw_sum([&](int64_t j) { return pr[j]; }, n);
+    prec_out[c] = sum / (double)n;
+  }
+  return kOk;
+}
+
+__global__ __launch_bounds__(BM_BLOCK) void bin_mean_lds_kernel(CsrView v, BinMeanParams P, PeaksOut out,
+                                                                double* prec_out, int32_t* charge_out,
+                                                                int32_t* status, int32_t* deferred,
+                                                                int32_t* n_deferred) {
+  __shared__ BinMeanSmem L;
+  const int64_t c = blockIdx.x;
+  BinMeanState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, L.owner, BM_DCAP, BM_NMAX};
+  const int32_t st = bin_mean_body<true>(v, P, S, c, out, prec_out, charge_out, L.tmp, &L.flag);
+  if (threadIdx.x == 0) {
+    status[c] = st;
+    if (st == kDeferred) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+  }
+}
+
+// Deferred clusters: same body, state in global scratch (slice per workgroup).
+__global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, BinMeanParams P, PeaksOut out,
+                                                                   double* prec_out, int32_t* charge_out,
+                                                                   int32_t* status, const int32_t* deferred,
+                                                                   const int32_t* n_deferred, char* scratch,
+                                                                   int64_t slice_bytes, int dcap) {
+  __shared__ int tmp[BM_BLOCK / kWave + 1];
+  __shared__ int flag;
+  char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
+  const int64_t nw = P.n_words;
+  BinMeanState<uint32_t> S;
+  S.bitmap = reinterpret_cast<unsigned long long*>(base);
+  S.wprefix = reinterpret_cast<uint32_t*>(base + nw * 8);
+  S.cnt = reinterpret_cast<uint32_t*>(base + nw * 12);
+  S.acc_i = reinterpret_cast<float*>(base + nw * 12 + (int64_t)dcap * 4);
+  S.acc_m = reinterpret_cast<float*>(base + nw * 12 + (int64_t)dcap * 8);
+  S.owner = reinterpret_cast<uint32_t*>(base + nw * 12 + (int64_t)dcap * 12);
+  S.dcap = dcap;
+  S.nmax = 0x7fffffff;
+  const int32_t nd = *n_deferred;
+  for (int32_t i = blockIdx.x; i < nd; i += gridDim.x) {
+    const int64_t c = deferred[i];
+    const int32_t st = bin_mean_body<false>(v, P, S, c, out, prec_out, charge_out, tmp, &flag);
+    if (threadIdx.x == 0) status[c] = st;
+    __syncthreads();
+  }
+}
+
+// bytes of one fallback slice
+__host__ int64_t bin_mean_slice_bytes(int32_t n_words, int64_t dcap) {
+  int64_t b = (int64_t)n_words * 12 + dcap * 16;
+  return (b + 255) & ~int64_t(255);
+}
+
+}  // namespace spx

@@ -1,0 +1,419 @@
+// Gap-average consensus (reference: src/average_spectrum_clustering.py:26-103,
+// average_spectrum; precursor helpers :106-148; semantics in SURVEY.md A.2 and
+// oracle/np_oracle.py gap_average_cluster).
+//
+// The reference pools the cluster's peaks, argsorts them by m/z, splits where
+// the sorted gap is >= mz_accuracy, keeps groups holding >= min_fraction*n
+// peaks (the last two true groups merged: the ind_list[1:-1] loop, :79) and
+// averages them through cumulative-sum differences, then applies a dynamic
+// range filter.  A full segmented sort is not needed to reproduce that
+// exactly: with buckets k = floor(mz / mz_accuracy),
+//   * two consecutive sorted peaks in one bucket differ by < mz_accuracy unless
+//     the bucket's own span reaches mz_accuracy (checked per bucket; such a
+//     cluster is deferred, never approximated);
+//   * the sorted gap between two consecutive occupied buckets is exactly
+//     fl(min(next) - max(prev)) -- the same f64 subtraction np.diff performs.
+// So group boundaries and group counts are exact (integer/bit-exact), and only
+// the group sums differ from the reference's cumsum differences by rounding
+// (within 1e-12 relative; the parity bar is 1e-5).  The sums are accumulated
+// as 64-bit fixed point (scale 2^e per cluster from max|value| * #peaks), so
+// LDS integer atomics make them order-independent and run-to-run deterministic.
+//
+//   1  block reduce: min/max m/z, max |intensity|, finiteness
+//   2  bucket bitmap (ds_or_b64) -> exclusive popcount prefix -> slot ids
+//   3  per peak: slot count, min and max m/z (u64 order keys, ds_min/max_u64)
+//   4  per slot: in-bucket span check, gap flags, block scan -> group ids
+//   5  per peak: fixed-point m/z and intensity sums per emitted group
+//   6  per group: min_fraction filter, values, dynamic-range filter, ordered write
+//
+// n == 1 passes the spectrum through (original order) with only the dynamic
+// range filter (:88-98).  Precursor m/z / charge / RT per cluster follow the
+// CLI's --pepmass / --rt choices (:106-148, :190-195).
+#include "spx_device.hpp"
+
+namespace spx {
+
+struct GapParams {
+  double mz_accuracy, dyn_range, min_fraction, proton;
+  double bucket_w, inv_bucket_w;  // mz_accuracy (LDS path) or mz_accuracy/2 (global path)
+  int32_t pepmass_mode;  // 0 lower_median, 1 naive_average, 2 neutral_average
+  int32_t rt_mode;       // 0 median, 1 mass_lower_median
+};
+
+enum : int32_t { kNonFinite = 4 };
+
+constexpr int GA_BLOCK = 256;
+constexpr int GA_WMAX = 3584;  // 229,376 buckets (2,293 Da at 0.01)
+constexpr int GA_DCAP = 1536;  // occupied buckets per cluster
+
+template <class PrefixT>
+struct GapState {
+  unsigned long long* bitmap;
+  PrefixT* wprefix;
+  uint32_t* cnt;        // per slot count, later its emitted group id
+  uint32_t* gcnt;       // per emitted group count
+  uint64_t* kmin;       // per slot min m/z key, later group fixed-point m/z sum
+  uint64_t* kmax;       // per slot max m/z key, later group fixed-point intensity sum
+  int wcap, dcap;
+};
+
+struct GapSmem {
+  unsigned long long bitmap[GA_WMAX];
+  uint16_t wprefix[GA_WMAX];
+  uint32_t cnt[GA_DCAP];
+  uint32_t gcnt[GA_DCAP];
+  uint64_t kmin[GA_DCAP];
+  uint64_t kmax[GA_DCAP];
+  int tmp[GA_BLOCK / kWave + 1];
+  double red[GA_BLOCK / kWave * 3];
+};
+
+__device__ __forceinline__ double nan_d() { return __longlong_as_double(0x7ff8000000000000ll); }
+
+// ------------------------------------------------------ precursor summary
+struct PrecSummary {
+  double pepmass, rt;
+  int32_t charge, status;
+};
+
+// numpy-compatible "less" for argsort/median ranks: NaN sorts last.
+__device__ __forceinline__ bool lt_nan_last(double a, double b) { return a < b || (!isnan(a) && isnan(b)); }
+
+// Run by one whole wave.  Ranks are stable (ties by index), which is what
+// numpy's argsort returns for n <= 16 and for tie-free input.
+__device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n, const GapParams& P) {
+  PrecSummary R;
+  const int lane = lane_id();
+  const double H = P.proton;
+  auto mass = [&](int64_t i) {
+    const double z = (double)v.charge[s0 + i];
+    return v.prec_mz[s0 + i] * z - z * H;  // (m*c - c*H), no contraction
+  };
+  // lower-median index of the neutral masses: rank == (n-1)//2
+  const int64_t want = (n - 1) / 2;
+  int64_t lm = -1;
+  for (int64_t i0 = 0; i0 < n; i0 += kWave) {
+    const int64_t i = i0 + lane;
+    int64_t rank = -1;
+    if (i < n) {
+      const double mi = mass(i);
+      rank = 0;
+      for (int64_t j = 0; j < n; ++j) {
+        const double mj = mass(j);
+        rank += lt_nan_last(mj, mi) || (!lt_nan_last(mi, mj) && j < i);
+      }
+    }
+    const unsigned long long hit = __ballot(rank == want);
+    if (hit && lm < 0) lm = i0 + __ffsll((long long)hit) - 1;
+  }
+  // median RT (np.median): middle element(s) of the sorted values
+  double rt_lo = 0.0, rt_hi = 0.0;
+  const int64_t k_lo = (n - 1) / 2, k_hi = n / 2;
+  if (P.rt_mode == 0) {
+    for (int64_t i0 = 0; i0 < n; i0 += kWave) {
+      const int64_t i = i0 + lane;
+      int64_t rank = -1;
+      double ri = 0.0;
+      if (i < n) {
+        ri = v.rt[s0 + i];
+        rank = 0;
+        for (int64_t j = 0; j < n; ++j) {
+          const double rj = v.rt[s0 + j];
+          rank += lt_nan_last(rj, ri) || (!lt_nan_last(ri, rj) && j < i);
+        }
+      }
+      const unsigned long long h1 = __ballot(rank == k_lo), h2 = __ballot(rank == k_hi);
+      if (h1) rt_lo = __shfl(ri, __ffsll((long long)h1) - 1, kWave);
+      if (h2) rt_hi = __shfl(ri, __ffsll((long long)h2) - 1, kWave);
+    }
+  }
+  R.status = kOk;
+  if (P.pepmass_mode == 0) {
+    const int32_t z = v.charge[s0 + lm];
+    R.pepmass = (mass(lm) + (double)z * H) / (double)z;
+    R.charge = z;
+  } else if (P.pepmass_mode == 1) {
+    double s = 0.0;
+    int mixed = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      s += v.prec_mz[s0 + i];
+      mixed |= v.charge[s0 + i] != v.charge[s0];
+    }
+    R.pepmass = s / (double)n;
+    R.charge = v.charge[s0];
+    if (mixed) R.status = kMixedCharge;
+  } else {
+    double sm = 0.0;
+    int64_t sz = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      sm += mass(i);
+      sz += v.charge[s0 + i];
+    }
+    const int32_t z = (int32_t)rint((double)sz / (double)n);
+    R.pepmass = (sm / (double)n + (double)z * H) / (double)z;
+    R.charge = z;
+  }
+  if (P.rt_mode == 1) {
+    R.rt = v.rt[s0 + lm];
+  } else {
+    R.rt = (n & 1) ? rt_lo : (0.0 + rt_lo + rt_hi) / 2.0;
+    if (isnan(rt_lo) || isnan(rt_hi)) R.rt = nan_d();
+  }
+  return R;
+}
+
+// --------------------------------------------------------------- the body
+template <class PrefixT>
+__device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState<PrefixT>& S, int64_t c,
+                            const PeaksOut& out, int* tmp, double* red) {
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1], n = s1 - s0;
+  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1], N = p1 - p0;
+  if (n == 0) return kNoGap;
+
+  // 1: extrema and finiteness
+  double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
+  int bad = 0;
+  for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
+    const double m = v.mz[k], it = v.inten[k];
+    bad |= !isfinite(m) || !isfinite(it);
+    lo = fmin(lo, m);
+    hi = fmax(hi, m);
+    imax = fmax(imax, fabs(it));
+  }
+  if (__syncthreads_or(bad)) return kNonFinite;
+
+  if (n == 1) {
+    // passthrough + dynamic-range filter on the raw spectrum (:88-98)
+    double mx = -__longlong_as_double(0x7ff0000000000000ll);
+    for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) mx = fmax(mx, v.inten[k]);
+    mx = wave_max(mx);
+    if (lane == 0) red[wid] = mx;
+    __syncthreads();
+    mx = red[0];
+    for (int w = 1; w < GA_BLOCK / kWave; ++w) mx = fmax(mx, red[w]);
+    __syncthreads();
+    if (N == 0) return kEmpty;
+    const double thr = mx / P.dyn_range;
+    int64_t base = 0;
+    for (int64_t k0 = p0; k0 < p1; k0 += GA_BLOCK) {
+      const int64_t k = k0 + tid;
+      const int keep = k < p1 && v.inten[k] >= thr;
+      int tot;
+      const int o = block_exclusive_scan<GA_BLOCK>(keep, tmp, tot);
+      if (keep) {
+        out.mz[p0 + base + o] = v.mz[k];
+        out.inten[p0 + base + o] = v.inten[k];
+      }
+      base += tot;
+    }
+    if (tid == 0) out.count[c] = base;
+    return kOk;
+  }
+  if (N < 2) return kNoGap;  // np.diff of < 2 values is empty -> ind_list[0] IndexError
+
+  lo = wave_min_d(lo);
+  hi = -wave_min_d(-hi);
+  imax = -wave_min_d(-imax);
+  if (lane == 0) { red[wid] = lo; red[4 + wid] = hi; red[8 + wid] = imax; }
+  __syncthreads();
+  for (int w = 0; w < GA_BLOCK / kWave; ++w) {
+    lo = fmin(lo, red[w]);
+    hi = fmax(hi, red[4 + w]);
+    imax = fmax(imax, red[8 + w]);
+  }
+  const int64_t kb = floor_div_exact(lo, P.bucket_w, P.inv_bucket_w);
+  const int64_t ke = floor_div_exact(hi, P.bucket_w, P.inv_bucket_w);
+  const int64_t nw = (ke - kb) / 64 + 1;
+  if (nw > S.wcap) return kDeferred;
+
+  // 2: occupied buckets
+  for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
+  __syncthreads();
+  for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
+    const int64_t b = floor_div_exact(v.mz[k], P.bucket_w, P.inv_bucket_w) - kb;
+    atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
+  }
+  __syncthreads();
+  const int D = bitmap_prefix<GA_BLOCK>(S.bitmap, S.wprefix, (int)nw, tmp);
+  if (D > S.dcap) return kDeferred;
+  for (int d = tid; d < D; d += GA_BLOCK) {
+    S.cnt[d] = 0u;
+    S.gcnt[d] = 0u;
+    S.kmin[d] = ~0ull;
+    S.kmax[d] = 0ull;
+  }
+  __syncthreads();
+
+  // 3: per-slot count and m/z extent
+  for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
+    const double m = v.mz[k];
+    const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
+    const uint64_t key = f64_order_key(m);
+    atomicAdd(&S.cnt[slot], 1u);
+    atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)key);
+    atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)key);
+  }
+  __syncthreads();
+
+  // 4: gaps between consecutive occupied buckets -> emitted group per slot
+  const int per = (D + GA_BLOCK - 1) / GA_BLOCK;
+  const int d0 = tid * per;
+  int my_gaps = 0, split = 0;
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d >= D) break;
+    const double mn = f64_from_order_key(S.kmin[d]), mx = f64_from_order_key(S.kmax[d]);
+    split |= (mx - mn) >= P.mz_accuracy;  // a gap could hide inside the bucket
+    if (d + 1 < D) my_gaps += (f64_from_order_key(S.kmin[d + 1]) - mx) >= P.mz_accuracy;
+  }
+  if (__syncthreads_or(split)) return kDeferred;
+  int m_gaps;
+  int g = block_exclusive_scan<GA_BLOCK>(my_gaps, tmp, m_gaps);
+  if (m_gaps == 0) return kNoGap;
+  const int E = m_gaps >= 2 ? m_gaps : 2;
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d >= D) break;
+    const int eg = m_gaps >= 2 ? min(g, m_gaps - 1) : g;
+    atomicAdd(&S.gcnt[eg], S.cnt[d]);
+    const bool gap_after = d + 1 < D &&
+        (f64_from_order_key(S.kmin[d + 1]) - f64_from_order_key(S.kmax[d])) >= P.mz_accuracy;
+    S.cnt[d] = (uint32_t)eg;
+    g += gap_after;
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
+  __syncthreads();
+
+  // 5: fixed-point group sums (exact integer adds: order-independent)
+  int ex_m, ex_i;
+  frexp(fmax(fabs(lo), fabs(hi)) * (double)N, &ex_m);
+  frexp(imax * (double)N, &ex_i);
+  const int sc_m = 61 - ex_m, sc_i = 61 - ex_i;
+  for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
+    const double m = v.mz[k], it = v.inten[k];
+    const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
+    const uint32_t eg = S.cnt[slot];
+    atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), (unsigned long long)__double2ll_rn(ldexp(m, sc_m)));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[eg]), (unsigned long long)__double2ll_rn(ldexp(it, sc_i)));
+  }
+  __syncthreads();
+
+  // 6: min_fraction filter, dynamic range, ordered output
+  const double min_len = P.min_fraction * (double)n;
+  const int gper = (E + GA_BLOCK - 1) / GA_BLOCK;
+  const int e0 = tid * gper;
+  double gmax = -__longlong_as_double(0x7ff0000000000000ll);
+  int any = 0;
+  for (int j = 0; j < gper; ++j) {
+    const int e = e0 + j;
+    if (e < E && (double)S.gcnt[e] >= min_len) {
+      gmax = fmax(gmax, ldexp((double)(int64_t)S.kmax[e], -sc_i) / (double)n);
+      any = 1;
+    }
+  }
+  gmax = wave_max(gmax);
+  if (lane == 0) red[wid] = gmax;
+  if (!__syncthreads_or(any)) return kEmpty;
+  for (int w = 0; w < GA_BLOCK / kWave; ++w) gmax = fmax(gmax, red[w]);
+  const double thr = gmax / P.dyn_range;
+  int mine = 0;
+  for (int j = 0; j < gper; ++j) {
+    const int e = e0 + j;
+    if (e < E && (double)S.gcnt[e] >= min_len && ldexp((double)(int64_t)S.kmax[e], -sc_i) / (double)n >= thr) ++mine;
+  }
+  int total;
+  int o = block_exclusive_scan<GA_BLOCK>(mine, tmp, total);
+  for (int j = 0; j < gper; ++j) {
+    const int e = e0 + j;
+    if (e >= E || (double)S.gcnt[e] < min_len) continue;
+    const double iv = ldexp((double)(int64_t)S.kmax[e], -sc_i) / (double)n;
+    if (!(iv >= thr)) continue;
+    out.mz[p0 + o] = ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e];
+    out.inten[p0 + o] = iv;
+    ++o;
+  }
+  if (tid == 0) out.count[c] = total;
+  return kOk;
+}
+
+template <class PrefixT>
+__device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P, int64_t c, int32_t st,
+                                           const PeaksOut& out, double* prec_out, int32_t* charge_out,
+                                           double* rt_out, int32_t* status) {
+  const int64_t s0 = v.cluster_off[c], n = v.cluster_off[c + 1] - s0;
+  if (st == kDeferred) return;
+  if (wave_id() == 0) {
+    PrecSummary R{nan_d(), nan_d(), 0, kOk};
+    if (n > 0) R = precursor_summary(v, s0, n, P);
+    if (lane_id() == 0) {
+      // the reference computes the precursor first (:161-163): its error wins
+      const int32_t fin = R.status != kOk ? R.status : st;
+      prec_out[c] = R.pepmass;
+      charge_out[c] = R.charge;
+      rt_out[c] = R.rt;
+      status[c] = fin;
+      if (fin != kOk) out.count[c] = 0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(GA_BLOCK) void gap_average_lds_kernel(CsrView v, GapParams P, PeaksOut out,
+                                                                   double* prec_out, int32_t* charge_out,
+                                                                   double* rt_out, int32_t* status,
+                                                                   int32_t* deferred, int32_t* n_deferred) {
+  __shared__ GapSmem L;
+  const int64_t c = blockIdx.x;
+  GapState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.gcnt, L.kmin, L.kmax, GA_WMAX, GA_DCAP};
+  const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red);
+  if (st == kDeferred) {
+    if (threadIdx.x == 0) {
+      status[c] = kDeferred;
+      deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    }
+    return;
+  }
+  gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status);
+}
+
+__global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v, GapParams P, PeaksOut out,
+                                                                      double* prec_out, int32_t* charge_out,
+                                                                      double* rt_out, int32_t* status,
+                                                                      const int32_t* deferred,
+                                                                      const int32_t* n_deferred, char* scratch,
+                                                                      int64_t slice_bytes, int wcap, int dcap,
+                                                                      int32_t* unresolved) {
+  __shared__ int tmp[GA_BLOCK / kWave + 1];
+  __shared__ double red[GA_BLOCK / kWave * 3];
+  char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
+  GapState<uint32_t> S;
+  S.bitmap = reinterpret_cast<unsigned long long*>(base);
+  S.wprefix = reinterpret_cast<uint32_t*>(base + (int64_t)wcap * 8);
+  S.cnt = reinterpret_cast<uint32_t*>(base + (int64_t)wcap * 12);
+  S.gcnt = reinterpret_cast<uint32_t*>(base + (int64_t)wcap * 12 + (int64_t)dcap * 4);
+  S.kmin = reinterpret_cast<uint64_t*>(base + (int64_t)wcap * 12 + (int64_t)dcap * 8);
+  S.kmax = reinterpret_cast<uint64_t*>(base + (int64_t)wcap * 12 + (int64_t)dcap * 16);
+  S.wcap = wcap;
+  S.dcap = dcap;
+  const int32_t nd = *n_deferred;
+  for (int32_t i = blockIdx.x; i < nd; i += gridDim.x) {
+    const int64_t c = deferred[i];
+    int32_t st = gap_body(v, P, S, c, out, tmp, red);
+    if (st == kDeferred) {
+      // bucket range beyond the scratch, or a bucket spanning >= mz_accuracy:
+      // reported, never approximated (the host re-runs it through the sort path)
+      if (threadIdx.x == 0) { status[c] = kDeferred; atomicAdd(unresolved, 1); }
+    } else {
+      gap_finish<uint32_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status);
+    }
+    __syncthreads();
+  }
+}
+
+__host__ int64_t gap_slice_bytes(int wcap, int dcap) {
+  int64_t b = (int64_t)wcap * 12 + (int64_t)dcap * 24;
+  return (b + 255) & ~int64_t(255);
+}
+
+}  // namespace spx

@@ -1,0 +1,271 @@
+// C-ABI of libspecpride_hip.so (include/specpride.h): argument checks,
+// workspace carving and kernel launches.  One translation unit (the kernel
+// sources are included) so the whole engine is a single gfx950 code object.
+//
+// Every entry point only enqueues work on the caller's stream: no allocation,
+// no synchronisation (hipGraph-capturable), no global mutable state except the
+// thread-local error text.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/specpride.h"
+#include "bin_mean.hip"
+#include "gap_average.hip"
+#include "medoid.hip"
+
+namespace {
+
+thread_local char g_err[256] = "";
+
+int fail(int code, const char* msg) {
+  std::snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    std::snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return SPX_EHIP;
+  }
+  return SPX_SUCCESS;
+}
+
+spx::CsrView view(const spx_csr* c) {
+  return spx::CsrView{c->n_clusters, c->n_spectra, c->n_peaks, c->cluster_off, c->spec_off,
+                      c->mz,         c->inten,     c->prec_mz, c->charge,      c->rt};
+}
+
+bool csr_ok(const spx_csr* c) {
+  return c && c->n_clusters >= 0 && c->n_spectra >= 0 && c->n_peaks >= 0 && c->cluster_off && c->spec_off &&
+         (c->n_peaks == 0 || (c->mz && c->inten)) && (c->n_spectra == 0 || (c->prec_mz && c->charge));
+}
+
+size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
+// carving helper: takes `bytes` (256-aligned) from the workspace
+struct Carver {
+  char* base;
+  size_t used, cap;
+  template <class T>
+  T* take(size_t count) {
+    T* p = reinterpret_cast<T*>(base + used);
+    used += align256(count * sizeof(T));
+    return p;
+  }
+};
+
+constexpr int kFallbackBlocks = 64;
+
+int64_t fallback_grid(int64_t C) { return std::max<int64_t>(1, std::min<int64_t>(C, kFallbackBlocks)); }
+
+int32_t bin_words(const spx_bin_params* p) {
+  const double nb = std::trunc((p->maximum - p->minimum) / p->binsize) + 1.0;  // binning.py:172
+  return (int32_t)((nb + 63.0) / 64.0);
+}
+
+int gap_wcap(const spx_gap_params* p, const spx_batch_info* info) {
+  const double span = (info && info->max_mz_span > 0) ? info->max_mz_span : 5000.0;
+  return (int)std::ceil((span / (p->mz_accuracy * 0.5) + 3.0) / 64.0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int spx_abi_version(void) { return SPX_ABI_VERSION; }
+const char* spx_last_error(void) { return g_err; }
+
+// ------------------------------------------------------------------ bin-mean
+size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info) {
+  if (!csr || !params || !info) return 0;
+  const int64_t C = csr->n_clusters;
+  const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
+  return align256(sizeof(int32_t)) + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
+         (size_t)fallback_grid(C) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
+}
+
+int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info, spx_peaks_out* out,
+                 double* prec_out, int32_t* charge_out, int32_t* status, void* workspace, size_t workspace_bytes,
+                 void* stream) {
+  if (!csr_ok(csr) || !params || !info || !out || !out->count || !prec_out || !charge_out || !status)
+    return fail(SPX_EINVAL, "spx_bin_mean: null argument");
+  if (!(params->binsize > 0) || !(params->maximum > params->minimum))
+    return fail(SPX_EINVAL, "spx_bin_mean: need binsize > 0 and maximum > minimum");
+  if (csr->n_peaks && (!out->mz || !out->inten)) return fail(SPX_EINVAL, "spx_bin_mean: null output arrays");
+  const size_t need = spx_bin_mean_workspace_size(csr, params, info);
+  if (!workspace || workspace_bytes < need) return fail(SPX_ENOSPACE, "spx_bin_mean: workspace too small");
+  const int64_t C = csr->n_clusters;
+  if (C == 0) return SPX_SUCCESS;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
+  int32_t* n_def = w.take<int32_t>(1);
+  int32_t* def = w.take<int32_t>((size_t)C);
+  char* scratch = w.base + w.used;
+
+  spx::BinMeanParams P;
+  P.minimum = params->minimum;
+  P.maximum = params->maximum;
+  P.binsize = params->binsize;
+  P.inv_binsize = 1.0 / params->binsize;
+  P.apply_quorum = params->apply_peak_quorum ? 1 : 0;
+  P.n_words = bin_words(params);
+  spx::PeaksOut O{out->mz, out->inten, out->count};
+  const spx::CsrView V = view(csr);
+  const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
+
+  if (hipMemsetAsync(n_def, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
+  hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                     charge_out, status, def, n_def);
+  if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)fallback_grid(C)), dim3(spx::BM_BLOCK), 0, s, V, P,
+                     O, prec_out, charge_out, status, def, n_def, scratch,
+                     spx::bin_mean_slice_bytes(P.n_words, dcap), (int)std::min<int64_t>(dcap, INT32_MAX));
+  return check_launch("bin_mean_global_kernel");
+}
+
+// -------------------------------------------------------------- gap-average
+size_t spx_gap_average_workspace_size(const spx_csr* csr, const spx_gap_params* params, const spx_batch_info* info) {
+  if (!csr || !params || !info) return 0;
+  const int64_t C = csr->n_clusters;
+  const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
+  return align256(sizeof(int32_t)) * 2 + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
+         (size_t)fallback_grid(C) * (size_t)spx::gap_slice_bytes(gap_wcap(params, info), (int)std::min<int64_t>(dcap, INT32_MAX));
+}
+
+int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_batch_info* info, spx_peaks_out* out,
+                    double* pepmass_out, int32_t* charge_out, double* rt_out, int32_t* status, void* workspace,
+                    size_t workspace_bytes, void* stream) {
+  if (!csr_ok(csr) || !params || !info || !out || !out->count || !pepmass_out || !charge_out || !rt_out || !status)
+    return fail(SPX_EINVAL, "spx_gap_average: null argument");
+  if (csr->n_spectra && !csr->rt) return fail(SPX_EINVAL, "spx_gap_average: rt array required");
+  if (!(params->mz_accuracy > 0)) return fail(SPX_EINVAL, "spx_gap_average: mz_accuracy must be > 0");
+  if (csr->n_peaks && (!out->mz || !out->inten)) return fail(SPX_EINVAL, "spx_gap_average: null output arrays");
+  const size_t need = spx_gap_average_workspace_size(csr, params, info);
+  if (!workspace || workspace_bytes < need) return fail(SPX_ENOSPACE, "spx_gap_average: workspace too small");
+  const int64_t C = csr->n_clusters;
+  if (C == 0) return SPX_SUCCESS;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
+  int32_t* n_def = w.take<int32_t>(1);
+  int32_t* unresolved = w.take<int32_t>(1);
+  int32_t* def = w.take<int32_t>((size_t)C);
+  char* scratch = w.base + w.used;
+  spx::GapParams P;
+  P.mz_accuracy = params->mz_accuracy;
+  P.dyn_range = params->dyn_range;
+  P.min_fraction = params->min_fraction;
+  P.proton = params->proton;
+  P.pepmass_mode = params->pepmass_mode;
+  P.rt_mode = params->rt_mode;
+  P.bucket_w = params->mz_accuracy;
+  P.inv_bucket_w = 1.0 / params->mz_accuracy;
+  spx::PeaksOut O{out->mz, out->inten, out->count};
+  const spx::CsrView V = view(csr);
+  const int wcap = gap_wcap(params, info);
+  const int dcap = (int)std::min<int64_t>(std::max<int64_t>(1, info->max_cluster_peaks), INT32_MAX);
+
+  if (hipMemsetAsync(n_def, 0, 512, s) != hipSuccess) return check_launch("spx_gap_average memset");
+  hipLaunchKernelGGL(spx::gap_average_lds_kernel, dim3((unsigned)C), dim3(spx::GA_BLOCK), 0, s, V, P, O, pepmass_out,
+                     charge_out, rt_out, status, def, n_def);
+  if (int rc = check_launch("gap_average_lds_kernel")) return rc;
+  spx::GapParams P2 = P;  // half-width buckets: no gap can hide inside one
+  P2.bucket_w = params->mz_accuracy * 0.5;
+  P2.inv_bucket_w = 1.0 / P2.bucket_w;
+  hipLaunchKernelGGL(spx::gap_average_global_kernel, dim3((unsigned)fallback_grid(C)), dim3(spx::GA_BLOCK), 0, s, V,
+                     P2, O, pepmass_out, charge_out, rt_out, status, def, n_def, scratch,
+                     spx::gap_slice_bytes(wcap, dcap), wcap, dcap, unresolved);
+  return check_launch("gap_average_global_kernel");
+}
+
+// ------------------------------------------------------------------- medoid
+size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t C) {
+  if (C < 0 || (C > 0 && (!hco || !hso))) return 0;
+  size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) +
+                 align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
+                 align256(sizeof(spx::MedoidMeta) * (size_t)std::max<int64_t>(C, 1)) +
+                 align256(sizeof(int64_t) * (size_t)(C + 1));
+  size_t arena = 0, margin = 0;
+  for (int64_t c = 0; c < C; ++c) {
+    const int64_t n = hco[c + 1] - hco[c];
+    const int64_t p = hso[hco[c + 1]] - hso[hco[c]];
+    const int64_t K = std::min<int64_t>(std::max<int64_t>(p, 1), (int64_t)spx::MD_WMAX * 64);
+    const int64_t KW = (K + 63) / 64;
+    const int64_t T = (n + spx::MD_TILE - 1) / spx::MD_TILE;
+    const size_t bytes = (size_t)(T * spx::MD_TILE * KW * 8) + align256((size_t)(n * n * 4));
+    if (n > spx::MD_NMAX) arena += bytes;
+    else if (n > 1) margin = std::max(margin, bytes);
+  }
+  // small clusters that overflow LDS at run time land in the arena too: keep room
+  // for a few of the largest ones on top of the clusters routed there by size.
+  return fixed + arena + 8 * margin + (size_t(1) << 20);
+}
+
+int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep, double* totals, void* workspace,
+               size_t workspace_bytes, void* stream) {
+  if (!csr_ok(csr) || !params || !rep) return fail(SPX_EINVAL, "spx_medoid: null argument");
+  if (!(params->tolerance > 0)) return fail(SPX_EINVAL, "spx_medoid: tolerance must be > 0");
+  const int64_t C = csr->n_clusters;
+  if (C == 0) return SPX_SUCCESS;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
+  if (!workspace) return fail(SPX_ENOSPACE, "spx_medoid: no workspace");
+  int32_t* n_def = w.take<int32_t>(1);
+  unsigned long long* bump = w.take<unsigned long long>(1);
+  int32_t* def = w.take<int32_t>((size_t)C);
+  spx::MedoidMeta* meta = w.take<spx::MedoidMeta>((size_t)C);
+  int64_t* tile_base = w.take<int64_t>((size_t)C + 1);
+  if (w.used >= workspace_bytes) return fail(SPX_ENOSPACE, "spx_medoid: workspace too small");
+  char* arena = w.base + w.used;
+  const int64_t arena_bytes = (int64_t)(workspace_bytes - w.used);
+  spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance};
+  const spx::CsrView V = view(csr);
+
+  if (hipMemsetAsync(n_def, 0, 512, s) != hipSuccess) return check_launch("spx_medoid memset");
+  hipLaunchKernelGGL(spx::medoid_small_kernel, dim3((unsigned)C), dim3(spx::MD_BLOCK), 0, s, V, P, rep, totals, def,
+                     n_def);
+  if (int rc = check_launch("medoid_small_kernel")) return rc;
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024));
+  hipLaunchKernelGGL(spx::medoid_build_kernel, dim3(g), dim3(spx::MD_BLOCK), 0, s, V, P, def, n_def, meta, arena,
+                     bump, arena_bytes, rep);
+  if (int rc = check_launch("medoid_build_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_tile_scan_kernel, dim3(1), dim3(spx::MD_BLOCK), 0, s, meta, n_def, tile_base);
+  if (int rc = check_launch("medoid_tile_scan_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_gram_kernel, dim3(2048), dim3(spx::MD_BLOCK), 0, s, meta, n_def, tile_base, arena);
+  if (int rc = check_launch("medoid_gram_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_totals_kernel, dim3(g), dim3(spx::MD_BLOCK), 0, s, V, meta, n_def, arena, rep,
+                     totals);
+  return check_launch("medoid_totals_kernel");
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- compaction
+namespace spx {
+__global__ __launch_bounds__(256) void compact_kernel(CsrView v, const double* __restrict__ smz,
+                                                      const double* __restrict__ sint, const int64_t* __restrict__ count,
+                                                      const int64_t* __restrict__ out_off, double* __restrict__ dmz,
+                                                      double* __restrict__ dint) {
+  for (int64_t c = blockIdx.x; c < v.n_clusters; c += gridDim.x) {
+    const int64_t src = v.spec_off[v.cluster_off[c]], dst = out_off[c], n = count[c];
+    for (int64_t k = threadIdx.x; k < n; k += 256) {
+      dmz[dst + k] = smz[src + k];
+      dint[dst + k] = sint[src + k];
+    }
+  }
+}
+}  // namespace spx
+
+extern "C" int spx_compact_peaks(const spx_csr* csr, const spx_peaks_out* src, const int64_t* out_off, double* dst_mz,
+                                 double* dst_inten, void* stream) {
+  if (!csr_ok(csr) || !src || !src->count || !out_off) return fail(SPX_EINVAL, "spx_compact_peaks: null argument");
+  if (csr->n_clusters == 0) return SPX_SUCCESS;
+  const unsigned g = (unsigned)std::min<int64_t>(csr->n_clusters, 65535);
+  hipLaunchKernelGGL(spx::compact_kernel, dim3(g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), view(csr),
+                     src->mz, src->inten, src->count, out_off, dst_mz, dst_inten);
+  return check_launch("compact_kernel");
+}

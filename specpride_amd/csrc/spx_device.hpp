@@ -1,0 +1,244 @@
+// Shared device-side helpers for the specpride gfx950 kernels.
+//
+// Everything here is written for CDNA4: 64-lane wavefronts, 256-thread
+// workgroups (4 waves, one per SIMD), LDS-resident per-cluster state.  Exact
+// IEEE f64 arithmetic is required on the parity path (bin indices, masses,
+// precursor means): the library is compiled with -ffp-contract=off and these
+// helpers never use fast-math intrinsics.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace spx {
+
+constexpr int kWave = 64;
+
+// ----------------------------------------------------------------- CSR views
+struct CsrView {
+  int64_t n_clusters, n_spectra, n_peaks;
+  const int64_t* __restrict__ cluster_off;
+  const int64_t* __restrict__ spec_off;
+  const double* __restrict__ mz;
+  const double* __restrict__ inten;
+  const double* __restrict__ prec_mz;
+  const int32_t* __restrict__ charge;
+  const double* __restrict__ rt;
+};
+
+// Per-cluster peak output, written at the cluster's own input peak offset
+// (capacity of cluster c = its input peak count, so no planning pass).
+struct PeaksOut {
+  double* __restrict__ mz;
+  double* __restrict__ inten;
+  int64_t* __restrict__ count;
+};
+
+enum : int32_t { kOk = 0, kMixedCharge = 1, kNoGap = 2, kEmpty = 3, kDeferred = 100 };
+
+// --------------------------------------------------------- wave primitives
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+__device__ __forceinline__ int wave_id() { return threadIdx.x / kWave; }
+
+template <class T>
+__device__ __forceinline__ T wave_inclusive_sum(T x) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    T y = __shfl_up(x, o, kWave);
+    if (lane_id() >= o) x += y;
+  }
+  return x;
+}
+
+template <class T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, kWave);
+  return x;
+}
+
+__device__ __forceinline__ double wave_max(double x) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) {
+    double y = __shfl_xor(x, o, kWave);
+    x = (y > x || (y != y)) ? y : x;  // NaN propagates like numpy max
+  }
+  return x;
+}
+
+__device__ __forceinline__ double wave_min_d(double x) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o, kWave));
+  return x;
+}
+
+// Block exclusive scan of one int per thread.  `tmp` holds BLOCK/64 + 1 ints
+// in LDS.  Returns the exclusive prefix; `total` receives the block sum.
+template <int BLOCK, class T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* tmp, T& total) {
+  static_assert(BLOCK % kWave == 0, "block must be whole waves");
+  constexpr int NW = BLOCK / kWave;
+  T inc = wave_inclusive_sum(v);
+  if (lane_id() == kWave - 1) tmp[wave_id()] = inc;
+  __syncthreads();
+  T base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    T t = tmp[w];
+    base += (w < wave_id()) ? t : T(0);
+    tot += t;
+  }
+  __syncthreads();
+  total = tot;
+  return base + inc - v;
+}
+
+// ------------------------------------------------------ exact bin indexing
+// trunc(fl((m - lo) / w)) and ceil(fl(m / w)) exactly as numpy / OpenMS compute
+// them (IEEE subtract + correctly rounded divide), without paying a f64 divide
+// per peak: q = x * (1/w) is within ~2 ulp of the exact quotient, so whenever q
+// is further than 2^-44 (relative) from an integer, the rounded quotient lies
+// on the same side and trunc/ceil agree.  Near an integer the exact divide runs.
+__device__ __forceinline__ int64_t trunc_div_exact(double x, double w, double inv_w) {
+  double q = x * inv_w;
+  double t = trunc(q);
+  double f = q - t;
+  double eps = fabs(q) * 0x1p-44;
+  if (f > eps && f < 1.0 - eps) return (int64_t)t;
+  return (int64_t)trunc(x / w);
+}
+
+__device__ __forceinline__ int64_t floor_div_exact(double x, double w, double inv_w) {
+  double q = x * inv_w;
+  double t = floor(q);
+  double f = q - t;
+  double eps = fabs(q) * 0x1p-44;
+  if (f > eps && f < 1.0 - eps) return (int64_t)t;
+  return (int64_t)floor(x / w);
+}
+
+__device__ __forceinline__ int64_t ceil_div_exact(double x, double w, double inv_w) {
+  double q = x * inv_w;
+  double t = ceil(q);
+  double f = t - q;
+  double eps = fabs(q) * 0x1p-44;
+  if (f > eps && f < 1.0 - eps) return (int64_t)t;
+  return (int64_t)ceil(x / w);
+}
+
+// f64 <-> order-preserving u64 (for LDS atomic min/max on doubles)
+__device__ __forceinline__ uint64_t f64_order_key(double x) {
+  uint64_t u = __double_as_longlong(x);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double f64_from_order_key(uint64_t k) {
+  uint64_t u = (k & 0x8000000000000000ull) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __longlong_as_double(u);
+}
+
+// ------------------------------------------------ numpy pairwise summation
+// The reduction numpy's add.reduce (np.mean, pandas .sum()) evaluates on a
+// float64 vector: n < 8 sequential; n <= 128 eight strided partial sums
+// combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus a sequential tail; larger n
+// split at n2 = n/2 - (n/2)%8 and recursed.  f(j) yields element j.
+template <class F>
+__device__ __forceinline__ double pw_leaf(const F& f, int64_t lo, int64_t n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int64_t i = 0; i < n; ++i) r += f(lo + i);
+    return r;
+  }
+  double r0 = f(lo + 0), r1 = f(lo + 1), r2 = f(lo + 2), r3 = f(lo + 3);
+  double r4 = f(lo + 4), r5 = f(lo + 5), r6 = f(lo + 6), r7 = f(lo + 7);
+  int64_t i = 8;
+  const int64_t lim = n - (n % 8);
+  for (; i < lim; i += 8) {
+    r0 += f(lo + i + 0); r1 += f(lo + i + 1); r2 += f(lo + i + 2); r3 += f(lo + i + 3);
+    r4 += f(lo + i + 4); r5 += f(lo + i + 5); r6 += f(lo + i + 6); r7 += f(lo + i + 7);
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += f(lo + i);
+  return res;
+}
+
+// Leaf-only form (n <= 128), usable in kernels that must not touch scratch.
+template <class F>
+__device__ __forceinline__ double pw_sum_small(const F& f, int64_t n) {
+  return 0.0 + pw_leaf(f, 0, n);
+}
+
+// General form: the recursion unrolled onto an explicit stack (depth <= 40).
+template <class F>
+__device__ double pw_sum(const F& f, int64_t n) {
+  if (n <= 128) return 0.0 + pw_leaf(f, 0, n);
+  int64_t lo[40], len[40];
+  double left[40];
+  int state[40];
+  int sp = 0;
+  lo[0] = 0; len[0] = n; state[0] = 0;
+  for (;;) {
+    const int64_t m = len[sp];
+    if (m <= 128) {
+      double val = pw_leaf(f, lo[sp], m);
+      for (;;) {
+        if (sp == 0) return 0.0 + val;
+        --sp;
+        if (state[sp] == 1) {
+          left[sp] = val;
+          state[sp] = 2;
+          int64_t h = len[sp] / 2;
+          h -= h % 8;
+          lo[sp + 1] = lo[sp] + h;
+          len[sp + 1] = len[sp] - h;
+          state[sp + 1] = 0;
+          ++sp;
+          break;
+        }
+        val = left[sp] + val;
+      }
+    } else {
+      int64_t h = m / 2;
+      h -= h % 8;
+      state[sp] = 1;
+      lo[sp + 1] = lo[sp];
+      len[sp + 1] = h;
+      state[sp + 1] = 0;
+      ++sp;
+    }
+  }
+}
+
+// Population count below bit `b` of a u64 bitmap with a per-word exclusive
+// prefix: the rank of bin b among the set bits (= its compact slot id).
+template <class PrefixT>
+__device__ __forceinline__ int bitmap_rank(const unsigned long long* bm, const PrefixT* pref, int64_t b) {
+  const int64_t w = b >> 6;
+  const unsigned long long mask = (1ull << (b & 63)) - 1ull;
+  return (int)pref[w] + __popcll(bm[w] & mask);
+}
+
+// Exclusive popcount prefix over `nw` bitmap words, in place into `pref`;
+// returns the total number of set bits.  Whole block participates.
+template <int BLOCK, class PrefixT>
+__device__ int bitmap_prefix(const unsigned long long* bm, PrefixT* pref, int nw, int* tmp) {
+  const int per = (nw + BLOCK - 1) / BLOCK;
+  const int w0 = threadIdx.x * per;
+  int local = 0;
+  for (int k = 0; k < per; ++k) {
+    int w = w0 + k;
+    if (w < nw) local += __popcll(bm[w]);
+  }
+  int total;
+  int base = block_exclusive_scan<BLOCK>(local, tmp, total);
+  for (int k = 0; k < per; ++k) {
+    int w = w0 + k;
+    if (w < nw) {
+      pref[w] = (PrefixT)base;
+      base += __popcll(bm[w]);
+    }
+  }
+  __syncthreads();
+  return total;
+}
+
+}  // namespace spx

@@ -1,0 +1,212 @@
+"""Batched device engine: the Python face of the C-ABI (include/specpride.h).
+
+A :class:`DeviceBatch` holds one cluster-segmented CSR batch resident in HBM
+(torch tensors are used purely as the allocator) plus the host-side facts the
+workspace queries need.  :func:`bin_mean`, :func:`gap_average` and
+:func:`medoid` enqueue the HIP kernels on the current torch stream and return
+device-resident results; ``.to_host()`` packs them (device compaction, then
+one D2H copy).
+
+This module is the product path: it never imports the oracle and has no CPU
+fallback -- without the HIP library it raises (see :mod:`specpride_amd._lib`).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from .csr import SpectraCSR
+
+STATUS_OK, STATUS_MIXED_CHARGE, STATUS_NO_GAP, STATUS_EMPTY, STATUS_NON_FINITE = 0, 1, 2, 3, 4
+STATUS_UNRESOLVED = 100
+PROTON = 1.00727646677  # pyteomics nist_mass['H+'][0][0] (average_spectrum_clustering.py:6)
+
+PEPMASS_MODES = {"lower_median": 0, "naive_average": 1, "neutral_average": 2}
+RT_MODES = {"median": 0, "mass_lower_median": 1}
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream_handle(stream=None) -> Optional[int]:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream or None
+
+
+class DeviceBatch:
+    """A SpectraCSR mirrored into HBM, with the host metadata the ABI needs."""
+
+    def __init__(self, tensors: dict, host_cluster_off: np.ndarray, host_spec_off: np.ndarray,
+                 max_mz_span: float, cluster_ids=None, titles=None):
+        self.t = tensors
+        self.n_clusters = int(tensors["n_clusters"])
+        self.n_spectra = int(tensors["n_spectra"])
+        self.n_peaks = int(tensors["n_peaks"])
+        self.host_cluster_off = np.ascontiguousarray(host_cluster_off, np.int64)
+        self.host_spec_off = np.ascontiguousarray(host_spec_off, np.int64)
+        sizes = np.diff(self.host_cluster_off)
+        peaks = self.host_spec_off[self.host_cluster_off[1:]] - self.host_spec_off[self.host_cluster_off[:-1]]
+        self.info = _lib.SpxBatchInfo(int(peaks.max(initial=0)), int(sizes.max(initial=0)), float(max_mz_span))
+        self.csr = _lib.SpxCsr(self.n_clusters, self.n_spectra, self.n_peaks,
+                               _ptr(tensors["cluster_off"]), _ptr(tensors["spec_off"]), _ptr(tensors["mz"]),
+                               _ptr(tensors["inten"]), _ptr(tensors["prec_mz"]), _ptr(tensors["charge"]),
+                               _ptr(tensors.get("rt")))
+        self.cluster_ids = cluster_ids or []
+        self.titles = titles or []
+        self._ws = {}
+
+    @classmethod
+    def from_host(cls, csr: SpectraCSR, device="cuda") -> "DeviceBatch":
+        span = 0.0
+        if csr.n_peaks:
+            span = float(np.nanmax(csr.mz) - np.nanmin(csr.mz)) if np.isfinite(csr.mz).any() else 0.0
+        return cls(csr.to_device(device), csr.cluster_off, csr.spec_off, span,
+                   cluster_ids=csr.cluster_ids, titles=csr.titles)
+
+    @classmethod
+    def from_device(cls, tensors: dict) -> "DeviceBatch":
+        """Wrap tensors already in HBM (e.g. synthetic.make_clusters_torch)."""
+        mz = tensors["mz"]
+        span = float((mz.max() - mz.min()).item()) if mz.numel() else 0.0
+        return cls(tensors, tensors["cluster_off"].cpu().numpy(), tensors["spec_off"].cpu().numpy(), span)
+
+    def workspace(self, key: str, nbytes: int):
+        import torch
+
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.t["mz"].device)
+            self._ws[key] = ws
+        return ws
+
+    @property
+    def device(self):
+        return self.t["mz"].device
+
+
+@dataclass
+class PeaksResult:
+    """Per-cluster peak lists in the capacity layout (cluster c at its input
+    peak offset), plus per-cluster scalars, all device tensors."""
+    batch: DeviceBatch
+    mz: object
+    inten: object
+    count: object
+    status: object
+    prec: object
+    charge: object
+    rt: object = None
+
+    def compact(self):
+        """Dense device arrays: (out_off [C+1], mz, inten)."""
+        import torch
+
+        C = self.batch.n_clusters
+        out_off = torch.zeros(C + 1, dtype=torch.int64, device=self.count.device)
+        if C:
+            torch.cumsum(self.count, 0, out=out_off[1:])
+        n = int(out_off[-1].item()) if C else 0
+        dmz = torch.empty(max(n, 1), dtype=torch.float64, device=self.count.device)
+        dint = torch.empty_like(dmz)
+        src = _lib.SpxPeaksOut(_ptr(self.mz), _ptr(self.inten), _ptr(self.count))
+        _lib.check(_lib.lib().spx_compact_peaks(ctypes.byref(self.batch.csr), ctypes.byref(src), _ptr(out_off),
+                                                _ptr(dmz), _ptr(dint), _stream_handle()), "spx_compact_peaks")
+        return out_off, dmz[:n], dint[:n]
+
+    def to_host(self) -> dict:
+        out_off, mz, inten = self.compact()
+        d = dict(out_off=out_off.cpu().numpy(), out_mz=mz.cpu().numpy(), out_int=inten.cpu().numpy(),
+                 status=self.status.cpu().numpy(), prec=self.prec.cpu().numpy(), charge=self.charge.cpu().numpy())
+        if self.rt is not None:
+            d["rt"] = self.rt.cpu().numpy()
+        return d
+
+
+def _alloc_peaks(batch: DeviceBatch):
+    import torch
+
+    dev = batch.device
+    P, C = max(batch.n_peaks, 1), max(batch.n_clusters, 1)
+    return (torch.empty(P, dtype=torch.float64, device=dev), torch.empty(P, dtype=torch.float64, device=dev),
+            torch.zeros(C, dtype=torch.int64, device=dev), torch.zeros(C, dtype=torch.int32, device=dev),
+            torch.empty(C, dtype=torch.float64, device=dev), torch.zeros(C, dtype=torch.int32, device=dev))
+
+
+def bin_mean(batch: DeviceBatch, minimum=100.0, maximum=2000.0, binsize=0.02, apply_peak_quorum=True,
+             out: Optional[PeaksResult] = None, stream=None) -> PeaksResult:
+    """combine_bin_mean (binning.py:170-231) for every cluster of the batch."""
+    L = _lib.lib()
+    prm = _lib.SpxBinParams(float(minimum), float(maximum), float(binsize), int(apply_peak_quorum is True))
+    need = L.spx_bin_mean_workspace_size(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info))
+    ws = batch.workspace("bin_mean", need)
+    if out is None:
+        mz, it, cnt, st, prec, ch = _alloc_peaks(batch)
+        out = PeaksResult(batch, mz, it, cnt, st, prec, ch)
+    po = _lib.SpxPeaksOut(_ptr(out.mz), _ptr(out.inten), _ptr(out.count))
+    _lib.check(L.spx_bin_mean(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info), ctypes.byref(po),
+                              _ptr(out.prec), _ptr(out.charge), _ptr(out.status), _ptr(ws), ws.numel(),
+                              _stream_handle(stream)), "spx_bin_mean")
+    return out
+
+
+def gap_average(batch: DeviceBatch, mz_accuracy=0.01, dyn_range=1000.0, min_fraction=0.5,
+                pepmass="lower_median", rt="mass_lower_median", proton=PROTON,
+                out: Optional[PeaksResult] = None, stream=None) -> PeaksResult:
+    """average_spectrum (average_spectrum_clustering.py:26-103) + precursor helpers for every cluster."""
+    import torch
+
+    L = _lib.lib()
+    if batch.t.get("rt") is None:
+        raise ValueError("gap_average needs per-spectrum RT (NaN where absent)")
+    prm = _lib.SpxGapParams(float(mz_accuracy), float(dyn_range), float(min_fraction), float(proton),
+                            PEPMASS_MODES[pepmass], RT_MODES[rt])
+    need = L.spx_gap_average_workspace_size(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info))
+    ws = batch.workspace("gap_average", need)
+    if out is None:
+        mz, it, cnt, st, prec, ch = _alloc_peaks(batch)
+        out = PeaksResult(batch, mz, it, cnt, st, prec, ch,
+                          rt=torch.empty(max(batch.n_clusters, 1), dtype=torch.float64, device=batch.device))
+    po = _lib.SpxPeaksOut(_ptr(out.mz), _ptr(out.inten), _ptr(out.count))
+    _lib.check(L.spx_gap_average(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info),
+                                 ctypes.byref(po), _ptr(out.prec), _ptr(out.charge), _ptr(out.rt), _ptr(out.status),
+                                 _ptr(ws), ws.numel(), _stream_handle(stream)), "spx_gap_average")
+    return out
+
+
+@dataclass
+class MedoidResult:
+    rep: object     # [C] int64 global spectrum index (-1 empty, <= -2 unresolved)
+    totals: object  # [S] f64 or None
+
+    def to_host(self):
+        return self.rep.cpu().numpy(), (None if self.totals is None else self.totals.cpu().numpy())
+
+
+def medoid(batch: DeviceBatch, tolerance=0.1, with_totals=False, out: Optional[MedoidResult] = None,
+           stream=None) -> MedoidResult:
+    """distance() + the medoid loop (most_similar_representative.py:13-111) for every cluster."""
+    import torch
+
+    L = _lib.lib()
+    prm = _lib.SpxMedoidParams(float(tolerance))
+    key = "medoid_size"
+    need = batch._ws.get(key)
+    if need is None:
+        need = L.spx_medoid_workspace_size(batch.host_cluster_off.ctypes.data_as(ctypes.c_void_p),
+                                           batch.host_spec_off.ctypes.data_as(ctypes.c_void_p), batch.n_clusters)
+        batch._ws[key] = need
+    ws = batch.workspace("medoid", need)
+    if out is None:
+        out = MedoidResult(torch.empty(max(batch.n_clusters, 1), dtype=torch.int64, device=batch.device),
+                           torch.empty(max(batch.n_spectra, 1), dtype=torch.float64, device=batch.device)
+                           if with_totals else None)
+    _lib.check(L.spx_medoid(ctypes.byref(batch.csr), ctypes.byref(prm), _ptr(out.rep), _ptr(out.totals), _ptr(ws),
+                            ws.numel(), _stream_handle(stream)), "spx_medoid")
+    return out

@@ -1,0 +1,88 @@
+"""Pin the oracle (numpy + C restatements) to the reference's own outputs.
+
+The golden vectors in tests/golden/ were produced by running the reference
+(/root/reference/src) itself -- see tests/golden/make_golden.py.  Bin-mean and
+gap-average are bit-exact; medoid indices are exact given the restated OpenMS
+xcorr (parity unpinned at that boundary)."""
+import numpy as np
+import pytest
+
+from conftest import BIN_SETS, GAP_SETS, bin_params, gap_params, load_golden
+from oracle import c_oracle, np_oracle
+
+
+@pytest.mark.parametrize("name", BIN_SETS)
+@pytest.mark.parametrize("impl", ["numpy", "c"])
+def test_bin_mean_oracle_matches_reference(name, impl):
+    z, csr = load_golden(f"bin_mean_{name}.npz")
+    r = (np_oracle if impl == "numpy" else c_oracle).bin_mean(csr, **bin_params(z))
+    np.testing.assert_array_equal(r["status"], z["status"])
+    np.testing.assert_array_equal(r["out_off"], z["out_off"])
+    np.testing.assert_array_equal(r["out_mz"], z["out_mz"])          # bit-exact
+    np.testing.assert_array_equal(r["out_int"], z["out_int"])
+    ok = z["status"] == 0
+    np.testing.assert_array_equal(r["prec"][ok], z["out_prec"][ok])
+    np.testing.assert_array_equal(r["charge"][ok], z["out_charge"][ok])
+
+
+@pytest.mark.parametrize("name", GAP_SETS)
+def test_gap_average_numpy_oracle_bit_exact(name):
+    z, csr = load_golden(f"gap_average_{name}.npz")
+    r = np_oracle.gap_average(csr, **gap_params(z))
+    np.testing.assert_array_equal(r["status"], z["status"])
+    np.testing.assert_array_equal(r["out_off"], z["out_off"])
+    np.testing.assert_array_equal(r["out_mz"], z["out_mz"])
+    np.testing.assert_array_equal(r["out_int"], z["out_int"])
+
+
+@pytest.mark.parametrize("name", GAP_SETS)
+def test_gap_average_c_oracle(name):
+    z, csr = load_golden(f"gap_average_{name}.npz")
+    r = c_oracle.gap_average(csr, **gap_params(z))
+    np.testing.assert_array_equal(r["status"], z["status"])
+    np.testing.assert_array_equal(r["out_off"], z["out_off"])
+    np.testing.assert_allclose(r["out_mz"], z["out_mz"], rtol=1e-12)
+    np.testing.assert_allclose(r["out_int"], z["out_int"], rtol=1e-12)
+
+
+def test_precursor_helpers():
+    z, csr = load_golden("precursor_helpers.npz")
+    H = float(z["H"])
+    for c in range(csr.n_clusters):
+        s0, s1 = csr.cluster_off[c], csr.cluster_off[c + 1]
+        pr, ch, rt = csr.prec_mz[s0:s1], csr.charge[s0:s1], csr.rt[s0:s1]
+        m, zz = np_oracle.lower_median_mass(pr, ch, H)
+        assert m == z["lm_mz"][c] and zz == z["lm_z"][c]
+        assert np_oracle.lower_median_mass_rt(pr, ch, rt, H) == z["lm_rt"][c]
+        na = np_oracle.naive_average_mass_and_charge(pr, ch)
+        if z["na_status"][c]:
+            assert na is None
+        else:
+            assert na == (z["na_mz"][c], z["na_z"][c])
+        assert np_oracle.neutral_average_mass_and_charge(pr, ch, H) == (z["ne_mz"][c], z["ne_z"][c])
+        assert np_oracle.median_rt(rt) == z["med_rt"][c]
+
+
+@pytest.mark.parametrize("impl", ["numpy", "c"])
+def test_pairwise_sum_tree(impl):
+    z = np.load(__import__("conftest").GOLDEN + "/pairwise_sum.npz")
+    f = np_oracle.pairwise_sum if impl == "numpy" else c_oracle.pairwise_sum
+    for a, b, s in zip(z["off"][:-1], z["off"][1:], z["sums"]):
+        assert f(z["vals"][a:b]) == s
+
+
+def test_pairwise_sum_matches_numpy_reduce():
+    rng = np.random.default_rng(5)
+    for n in list(range(0, 300)) + [511, 512, 513, 1024, 2047, 4099, 8191]:
+        v = rng.random(n) * 10.0 ** rng.uniform(-5, 5, n)
+        assert c_oracle.pairwise_sum(v) == np.add.reduce(v)
+
+
+@pytest.mark.parametrize("impl", ["numpy", "c", "c_dense"])
+def test_medoid_oracle_matches_reference(impl):
+    z, csr = load_golden("medoid_main.npz")
+    if impl == "numpy":
+        rep = np_oracle.medoid(csr)
+    else:
+        rep = c_oracle.medoid(csr, dense_tables=(impl == "c_dense"))
+    np.testing.assert_array_equal(rep, z["rep_index"])
