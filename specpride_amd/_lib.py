@@ -17,7 +17,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libspecpride_hip.so")
+LIB_PATH = os.environ.get("SPX_LIB") or os.path.join(LIB_DIR, "libspecpride_hip.so")
 CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SPX_OFFLOAD_ARCH", "gfx950")
@@ -71,6 +71,10 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp")))
 
 
+def build_all(force: bool = False):
+    return build(force), build_mgf(force)
+
+
 def build(force: bool = False) -> str:
     """Compile the HIP engine for gfx950 into specpride_amd/lib (cross-compiles without a GPU)."""
     os.makedirs(LIB_DIR, exist_ok=True)
@@ -82,6 +86,22 @@ def build(force: bool = False) -> str:
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
+
+
+MGF_LIB_PATH = os.path.join(LIB_DIR, "libspx_mgf.so")
+
+
+def build_mgf(force: bool = False) -> str:
+    """Host C++ MGF reader/writer (csrc/mgf_io.cpp) -> specpride_amd/lib/libspx_mgf.so."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    src = os.path.join(CSRC, "mgf_io.cpp")
+    if not force and os.path.exists(MGF_LIB_PATH) and os.path.getmtime(MGF_LIB_PATH) >= os.path.getmtime(src):
+        return MGF_LIB_PATH
+    tmp = MGF_LIB_PATH + ".tmp"
+    subprocess.run([os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread",
+                    "-Wall", "-o", tmp, src], check=True)
+    os.replace(tmp, MGF_LIB_PATH)
+    return MGF_LIB_PATH
 
 
 def lib():

@@ -240,6 +240,24 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_lds_kernel(CsrView v, BinMe
   }
 }
 
+// Scratch slice of the deferred path, every array 256-B aligned.
+struct BinSliceLayout {
+  int64_t bitmap, wprefix, cnt, acc_i, acc_m, owner, total;
+};
+__host__ __device__ inline BinSliceLayout bin_slice_layout(int64_t n_words, int64_t dcap) {
+  BinSliceLayout L;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) { const int64_t at = o; o += (bytes + 255) & ~int64_t(255); return at; };
+  L.bitmap = take(n_words * 8);
+  L.wprefix = take(n_words * 4);
+  L.cnt = take(dcap * 4);
+  L.acc_i = take(dcap * 4);
+  L.acc_m = take(dcap * 4);
+  L.owner = take(dcap * 4);
+  L.total = o;
+  return L;
+}
+
 // Deferred clusters: same body, state in global scratch (slice per workgroup).
 __global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, BinMeanParams P, PeaksOut out,
                                                                    double* prec_out, int32_t* charge_out,
@@ -249,14 +267,14 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, Bi
   __shared__ int tmp[BM_BLOCK / kWave + 1];
   __shared__ int flag;
   char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
-  const int64_t nw = P.n_words;
+  const BinSliceLayout Lo = bin_slice_layout(P.n_words, dcap);
   BinMeanState<uint32_t> S;
-  S.bitmap = reinterpret_cast<unsigned long long*>(base);
-  S.wprefix = reinterpret_cast<uint32_t*>(base + nw * 8);
-  S.cnt = reinterpret_cast<uint32_t*>(base + nw * 12);
-  S.acc_i = reinterpret_cast<float*>(base + nw * 12 + (int64_t)dcap * 4);
-  S.acc_m = reinterpret_cast<float*>(base + nw * 12 + (int64_t)dcap * 8);
-  S.owner = reinterpret_cast<uint32_t*>(base + nw * 12 + (int64_t)dcap * 12);
+  S.bitmap = reinterpret_cast<unsigned long long*>(base + Lo.bitmap);
+  S.wprefix = reinterpret_cast<uint32_t*>(base + Lo.wprefix);
+  S.cnt = reinterpret_cast<uint32_t*>(base + Lo.cnt);
+  S.acc_i = reinterpret_cast<float*>(base + Lo.acc_i);
+  S.acc_m = reinterpret_cast<float*>(base + Lo.acc_m);
+  S.owner = reinterpret_cast<uint32_t*>(base + Lo.owner);
   S.dcap = dcap;
   S.nmax = 0x7fffffff;
   const int32_t nd = *n_deferred;
@@ -269,9 +287,6 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, Bi
 }
 
 // bytes of one fallback slice
-__host__ int64_t bin_mean_slice_bytes(int32_t n_words, int64_t dcap) {
-  int64_t b = (int64_t)n_words * 12 + dcap * 16;
-  return (b + 255) & ~int64_t(255);
-}
+__host__ int64_t bin_mean_slice_bytes(int32_t n_words, int64_t dcap) { return bin_slice_layout(n_words, dcap).total; }
 
 }  // namespace spx

@@ -232,6 +232,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   __syncthreads();
   for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
     const int64_t b = floor_div_exact(v.mz[k], P.bucket_w, P.inv_bucket_w) - kb;
+    SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
     atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
   }
   __syncthreads();
@@ -250,6 +251,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     const double m = v.mz[k];
     const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
     const uint64_t key = f64_order_key(m);
+    SPX_GUARD(slot >= 0 && slot < D, "gap slot c=%ld slot=%d D=%d\n", (long)c, slot, D)
     atomicAdd(&S.cnt[slot], 1u);
     atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)key);
     atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)key);
@@ -295,6 +297,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     const double m = v.mz[k], it = v.inten[k];
     const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
     const uint32_t eg = S.cnt[slot];
+    SPX_GUARD(slot >= 0 && slot < D && (int)eg < E, "gap eg c=%ld slot=%d eg=%u E=%d\n", (long)c, slot, eg, E)
     atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), (unsigned long long)__double2ll_rn(ldexp(m, sc_m)));
     atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[eg]), (unsigned long long)__double2ll_rn(ldexp(it, sc_i)));
   }
@@ -330,6 +333,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     if (e >= E || (double)S.gcnt[e] < min_len) continue;
     const double iv = ldexp((double)(int64_t)S.kmax[e], -sc_i) / (double)n;
     if (!(iv >= thr)) continue;
+    SPX_GUARD(o < N, "gap out c=%ld o=%d N=%ld\n", (long)c, o, (long)N)
     out.mz[p0 + o] = ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e];
     out.inten[p0 + o] = iv;
     ++o;
@@ -377,6 +381,25 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_lds_kernel(CsrView v, Ga
   gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status);
 }
 
+// Scratch slice of the deferred path: every array starts 256-B aligned (the
+// 64-bit atomics on kmin/kmax fault on a misaligned address).
+struct GapSliceLayout {
+  int64_t bitmap, wprefix, cnt, gcnt, kmin, kmax, total;
+};
+__host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
+  GapSliceLayout L;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) { const int64_t at = o; o += (bytes + 255) & ~int64_t(255); return at; };
+  L.bitmap = take((int64_t)wcap * 8);
+  L.wprefix = take((int64_t)wcap * 4);
+  L.cnt = take((int64_t)dcap * 4);
+  L.gcnt = take((int64_t)dcap * 4);
+  L.kmin = take((int64_t)dcap * 8);
+  L.kmax = take((int64_t)dcap * 8);
+  L.total = o;
+  return L;
+}
+
 __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v, GapParams P, PeaksOut out,
                                                                       double* prec_out, int32_t* charge_out,
                                                                       double* rt_out, int32_t* status,
@@ -387,13 +410,14 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
   __shared__ int tmp[GA_BLOCK / kWave + 1];
   __shared__ double red[GA_BLOCK / kWave * 3];
   char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
+  const GapSliceLayout Lo = gap_slice_layout(wcap, dcap);
   GapState<uint32_t> S;
-  S.bitmap = reinterpret_cast<unsigned long long*>(base);
-  S.wprefix = reinterpret_cast<uint32_t*>(base + (int64_t)wcap * 8);
-  S.cnt = reinterpret_cast<uint32_t*>(base + (int64_t)wcap * 12);
-  S.gcnt = reinterpret_cast<uint32_t*>(base + (int64_t)wcap * 12 + (int64_t)dcap * 4);
-  S.kmin = reinterpret_cast<uint64_t*>(base + (int64_t)wcap * 12 + (int64_t)dcap * 8);
-  S.kmax = reinterpret_cast<uint64_t*>(base + (int64_t)wcap * 12 + (int64_t)dcap * 16);
+  S.bitmap = reinterpret_cast<unsigned long long*>(base + Lo.bitmap);
+  S.wprefix = reinterpret_cast<uint32_t*>(base + Lo.wprefix);
+  S.cnt = reinterpret_cast<uint32_t*>(base + Lo.cnt);
+  S.gcnt = reinterpret_cast<uint32_t*>(base + Lo.gcnt);
+  S.kmin = reinterpret_cast<uint64_t*>(base + Lo.kmin);
+  S.kmax = reinterpret_cast<uint64_t*>(base + Lo.kmax);
   S.wcap = wcap;
   S.dcap = dcap;
   const int32_t nd = *n_deferred;
@@ -411,9 +435,6 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
   }
 }
 
-__host__ int64_t gap_slice_bytes(int wcap, int dcap) {
-  int64_t b = (int64_t)wcap * 12 + (int64_t)dcap * 24;
-  return (b + 255) & ~int64_t(255);
-}
+__host__ int64_t gap_slice_bytes(int wcap, int dcap) { return gap_slice_layout(wcap, dcap).total; }
 
 }  // namespace spx

@@ -230,14 +230,19 @@ struct MedoidMeta {
   int32_t n, KW, tiles, ok;
 };
 
-// One workgroup per deferred cluster: union bitmap in LDS, rows + count matrix
-// bump-allocated from the scratch arena.
+// One workgroup per deferred cluster.  Compact column ids come from a
+// two-level occupancy bitmap so any bin range works: level 1 (LDS) has one bit
+// per block of 64 bins, level 2 (arena) one u64 word per OCCUPIED block; the
+// column of bin b is prefix2[block slot] + popcount(word & below(b)).  Rows and
+// the count matrix are bump-allocated from the same arena.
+constexpr int MD_L1WORDS = 1024;  // level-1 bits: 65,536 blocks = 4.2M bins
+
 __global__ __launch_bounds__(MD_BLOCK) void medoid_build_kernel(CsrView v, MedoidParams P, const int32_t* deferred,
                                                                 const int32_t* n_deferred, MedoidMeta* meta,
                                                                 char* scratch, unsigned long long* bump,
                                                                 int64_t scratch_bytes, int64_t* rep) {
-  __shared__ unsigned long long bitmap[MD_WMAX];
-  __shared__ uint32_t wprefix[MD_WMAX];
+  __shared__ unsigned long long l1[MD_L1WORDS];
+  __shared__ uint32_t l1pre[MD_L1WORDS];
   __shared__ int tmp[MD_BLOCK / kWave + 1];
   __shared__ long long red[2 * (MD_BLOCK / kWave)];
   __shared__ unsigned long long base_sh;
@@ -250,25 +255,53 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_build_kernel(CsrView v, Medoi
     const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
     int64_t blo, bhi;
     const bool any = cluster_bin_range(v, p0, p1, P, red, blo, bhi);
-    const int64_t nw = any ? (bhi - blo) / 64 + 1 : 0;
+    const int64_t nblk = any ? ((bhi - blo) >> 6) + 1 : 0;
+    const int64_t nw1 = (nblk + 63) / 64;
     MedoidMeta M{c, s0, 0, 0, n, 0, 0, 0};
-    if (nw > MD_WMAX) {  // bin range beyond 65,536 bins: reported, not approximated
+    if (nw1 > MD_L1WORDS) {  // > 4.2M bins: reported, not approximated
       if (tid == 0) { meta[di] = M; rep[c] = -2; }
       continue;
     }
-    for (int w = tid; w < nw; w += MD_BLOCK) bitmap[w] = 0ull;
+    // level 1
+    for (int w = tid; w < nw1; w += MD_BLOCK) l1[w] = 0ull;
     __syncthreads();
     for (int64_t k = p0 + tid; k < p1; k += MD_BLOCK) {
-      const int64_t b = md_bin(v.mz[k], P) - blo;
-      atomicOr(&bitmap[b >> 6], 1ull << (b & 63));
+      const int64_t blk = (md_bin(v.mz[k], P) - blo) >> 6;
+      atomicOr(&l1[blk >> 6], 1ull << (blk & 63));
     }
     __syncthreads();
-    const int K = bitmap_prefix<MD_BLOCK>(bitmap, wprefix, (int)nw, tmp);
+    const int B1 = bitmap_prefix<MD_BLOCK>(l1, l1pre, (int)nw1, tmp);
+    // arena: level-2 words + their prefix, then rows and counts (sized after K)
+    const int64_t l2_bytes = (((int64_t)B1 * 12) + 255) & ~int64_t(255);
+    if (tid == 0) base_sh = atomicAdd(bump, (unsigned long long)l2_bytes);
+    __syncthreads();
+    const int64_t l2_base = (int64_t)base_sh;
+    if (l2_base + l2_bytes > scratch_bytes) {
+      if (tid == 0) { meta[di] = M; rep[c] = -3; }
+      __syncthreads();
+      continue;
+    }
+    unsigned long long* l2 = reinterpret_cast<unsigned long long*>(scratch + l2_base);
+    uint32_t* l2pre = reinterpret_cast<uint32_t*>(scratch + l2_base + (int64_t)B1 * 8);
+    for (int w = tid; w < B1; w += MD_BLOCK) l2[w] = 0ull;
+    __syncthreads();
+    auto block_slot = [&](int64_t rel) { return bitmap_rank(l1, l1pre, rel >> 6); };
+    for (int64_t k = p0 + tid; k < p1; k += MD_BLOCK) {
+      const int64_t rel = md_bin(v.mz[k], P) - blo;
+      atomicOr(&l2[block_slot(rel)], 1ull << (rel & 63));
+    }
+    __syncthreads();
+    const int K = bitmap_prefix<MD_BLOCK>(l2, l2pre, B1, tmp);
+    auto column = [&](int64_t rel) {
+      const int bs = block_slot(rel);
+      return (int)l2pre[bs] + __popcll(l2[bs] & ((1ull << (rel & 63)) - 1ull));
+    };
     const int KW = (K + 63) / 64 > 0 ? (K + 63) / 64 : 1;
     const int T = (n + MD_TILE - 1) / MD_TILE;
     // rows padded to whole tiles so the Gram kernel never reads past them
     const int64_t rows_bytes = (int64_t)T * MD_TILE * KW * 8;
     const int64_t cmat_bytes = (((int64_t)n * n * 4) + 255) & ~int64_t(255);
+    __syncthreads();
     if (tid == 0) base_sh = atomicAdd(bump, (unsigned long long)(rows_bytes + cmat_bytes));
     __syncthreads();
     const int64_t base = (int64_t)base_sh;
@@ -284,7 +317,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_build_kernel(CsrView v, Medoi
       const int64_t a = v.spec_off[s], e = v.spec_off[s + 1];
       unsigned long long* row = rows + (s - s0) * KW;
       for (int64_t k = a + tid; k < e; k += MD_BLOCK) {
-        const int col = bitmap_rank(bitmap, wprefix, md_bin(v.mz[k], P) - blo);
+        const int col = column(md_bin(v.mz[k], P) - blo);
         atomicOr(&row[col >> 6], 1ull << (col & 63));
       }
     }

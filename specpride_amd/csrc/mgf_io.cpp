@@ -1,0 +1,431 @@
+// Native clustered-MGF ingest and emit for the bin-mean CLI path
+// (reference: src/binning.py:122-167 parser,
+// src/binning.py:234-245 writer).  Host C++ (no GPU), built into
+// specpride_amd/lib/libspx_mgf.so with g++ -O3 -pthread.
+//
+// Parser contract = the reference's line loop, restricted to the well-formed
+// subset whose Python meaning is unambiguous:
+//   TITLE=<id;usi> starts a spectrum; PEPMASS=<float>; CHARGE=<int>[+];
+//   a line whose first char is an ASCII digit is "mz intensity" (single space,
+//   extra fields ignored); a stripped "END IONS" stores the spectrum.
+// Numbers use the plain decimal grammar [+-]digits[.digits][e[+-]digits]; the
+// values equal Python float() because strtod is correctly rounded too.  Any
+// line outside that subset (underscores in numbers, inf/nan, tabs between
+// fields, non-ASCII text, PEPMASS before the first TITLE, a repeated END IONS,
+// a TITLE without ';') makes the parse report "fallback: ..." and the caller
+// re-reads the file with the Python line loop, which then behaves (or raises)
+// exactly like the reference.
+//
+// Files are split into per-thread byte ranges that begin at a "TITLE=" line:
+// the reference's state is reset at every TITLE, so the ranges parse
+// independently and concatenate in order.
+//
+// Writer: Python repr() of a float64 (numpy's str() of np.float64 is the same):
+// shortest round-trip digits (std::to_chars), positional for 1e-4 <= |x| < 1e16,
+// else d.ddde+XX.
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+struct Chunk {
+  std::vector<int64_t> npk;     // peaks per spectrum
+  std::vector<double> mz, it, prec;
+  std::vector<int64_t> charge;
+  std::vector<int32_t> flags;   // bit0 PEPMASS seen, bit1 CHARGE seen
+  std::string titles;           // '\n'-joined
+  std::string error;
+};
+
+struct Result {
+  std::vector<int64_t> spec_off;
+  std::vector<double> mz, it, prec;
+  std::vector<int64_t> charge;
+  std::vector<int32_t> flags;
+  std::string titles, error;
+};
+
+inline bool is_py_space(unsigned char c) {
+  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\x0b' || c == '\x0c' || (c >= 0x1c && c <= 0x1f);
+}
+
+inline void strip(const char*& b, const char*& e) {
+  while (b < e && is_py_space((unsigned char)*b)) ++b;
+  while (e > b && is_py_space((unsigned char)e[-1])) --e;
+}
+
+// plain decimal float grammar; returns false on anything else
+bool parse_float(const char* b, const char* e, double& out) {
+  const char* p = b;
+  if (p < e && (*p == '+' || *p == '-')) ++p;
+  const char* d0 = p;
+  while (p < e && *p >= '0' && *p <= '9') ++p;
+  bool digits = p > d0;
+  if (p < e && *p == '.') {
+    ++p;
+    const char* f0 = p;
+    while (p < e && *p >= '0' && *p <= '9') ++p;
+    digits |= p > f0;
+  }
+  if (!digits) return false;
+  if (p < e && (*p == 'e' || *p == 'E')) {
+    ++p;
+    if (p < e && (*p == '+' || *p == '-')) ++p;
+    const char* x0 = p;
+    while (p < e && *p >= '0' && *p <= '9') ++p;
+    if (p == x0) return false;
+  }
+  if (p != e) return false;
+  char buf[128];
+  const size_t n = (size_t)(e - b);
+  if (n >= sizeof(buf)) {
+    std::string s(b, e);
+    out = std::strtod(s.c_str(), nullptr);
+  } else {
+    std::memcpy(buf, b, n);
+    buf[n] = 0;
+    out = std::strtod(buf, nullptr);
+  }
+  return true;
+}
+
+bool parse_charge(const char* b, const char* e, int64_t& out) {
+  strip(b, e);
+  while (b < e && *b == '+') ++b;  // .strip("+")
+  while (e > b && e[-1] == '+') --e;
+  strip(b, e);                     // int() tolerates surrounding whitespace
+  const char* p = b;
+  bool neg = false;
+  if (p < e && (*p == '-' || *p == '+')) { neg = *p == '-'; ++p; }
+  if (p == e || e - p > 17) return false;
+  int64_t v = 0;
+  for (; p < e; ++p) {
+    if (*p < '0' || *p > '9') return false;
+    v = v * 10 + (*p - '0');
+  }
+  out = neg ? -v : v;
+  return true;
+}
+
+void parse_range(const char* b, const char* e, Chunk& C) {
+  bool have = false, stored = true;  // `stored`: END IONS already taken for this TITLE
+  int64_t cur_np = 0;
+  double cur_prec = 0.0;
+  int64_t cur_z = 0;
+  int32_t cur_f = 0;
+  std::string cur_title;
+  size_t mark = 0;  // peaks of the current spectrum start at C.mz[mark]
+  const char* p = b;
+  auto fail = [&](const char* why) { if (C.error.empty()) C.error = std::string("fallback: ") + why; };
+  while (p < e && C.error.empty()) {
+    const char* ls = p;
+    const char* le = p;
+    while (le < e && *le != '\n' && *le != '\r') ++le;
+    p = le;  // universal newlines, like Python text mode: \n, \r\n or \r
+    if (p < e) {
+      if (*p == '\r') {
+        ++p;
+        if (p < e && *p == '\n') ++p;
+      } else {
+        ++p;
+      }
+    }
+    for (const char* q = ls; q < le; ++q)
+      if ((unsigned char)*q >= 0x80) { fail("non-ASCII text"); break; }
+    if (!C.error.empty()) break;
+    const size_t n = (size_t)(le - ls);
+    if (n >= 6 && std::memcmp(ls, "TITLE=", 6) == 0) {
+      const char *tb = ls + 6, *te = le;
+      strip(tb, te);
+      if (!std::memchr(tb, ';', (size_t)(te - tb))) { fail("TITLE without ';'"); break; }
+      // a new spectrum: drop the previous one's un-stored peaks
+      C.mz.resize(mark);
+      C.it.resize(mark);
+      have = true;
+      stored = false;
+      cur_np = 0;
+      cur_f = 0;
+      cur_title.assign(tb, te);
+      continue;
+    }
+    if (n >= 8 && std::memcmp(ls, "PEPMASS=", 8) == 0) {
+      if (!have || stored) { fail("PEPMASS outside a spectrum"); break; }
+      const char *vb = ls + 8, *ve = le;
+      strip(vb, ve);
+      if (!parse_float(vb, ve, cur_prec)) { fail("PEPMASS value"); break; }
+      cur_f |= 1;
+      continue;
+    }
+    if (n >= 7 && std::memcmp(ls, "CHARGE=", 7) == 0) {
+      if (!have || stored) { fail("CHARGE outside a spectrum"); break; }
+      if (!parse_charge(ls + 7, le, cur_z)) { fail("CHARGE value"); break; }
+      cur_f |= 2;
+      continue;
+    }
+    if (n >= 1 && *ls >= '0' && *ls <= '9') {
+      if (!have || stored) { fail("peak outside a spectrum"); break; }
+      const char *vb = ls, *ve = le;
+      strip(vb, ve);
+      const char* sp = (const char*)std::memchr(vb, ' ', (size_t)(ve - vb));
+      if (!sp) { fail("peak line without ' '"); break; }
+      const char* t1 = sp + 1;
+      const char* sp2 = (const char*)std::memchr(t1, ' ', (size_t)(ve - t1));
+      const char* t1e = sp2 ? sp2 : ve;
+      double a, v;
+      if (!parse_float(vb, sp, a) || !parse_float(t1, t1e, v)) { fail("peak value"); break; }
+      C.mz.push_back(a);
+      C.it.push_back(v);
+      ++cur_np;
+      continue;
+    }
+    const char *sb = ls, *se = le;
+    strip(sb, se);
+    if (se - sb == 8 && std::memcmp(sb, "END IONS", 8) == 0) {
+      if (!have || stored) { fail("END IONS without a new TITLE"); break; }
+      C.npk.push_back(cur_np);
+      C.prec.push_back(cur_prec);
+      C.charge.push_back(cur_z);
+      C.flags.push_back(cur_f);
+      C.titles += cur_title;
+      C.titles += '\n';
+      mark = C.mz.size();
+      stored = true;
+    }
+  }
+  C.mz.resize(mark);
+  C.it.resize(mark);
+}
+
+bool read_file(const char* path, std::string& data, std::string& err) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) { err = std::string("cannot open ") + path; return false; }
+  std::fseek(f, 0, SEEK_END);
+  long sz = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  data.resize(sz > 0 ? (size_t)sz : 0);
+  size_t got = sz > 0 ? std::fread(&data[0], 1, (size_t)sz, f) : 0;
+  std::fclose(f);
+  if (got != data.size()) { err = "short read"; return false; }
+  return true;
+}
+
+// ------------------------------------------------------------ repr writer
+// Python repr(float) into out; returns bytes written.
+int py_repr(double x, char* out) {
+  if (std::isnan(x)) { std::memcpy(out, "nan", 3); return 3; }
+  if (std::isinf(x)) {
+    if (x < 0) { std::memcpy(out, "-inf", 4); return 4; }
+    std::memcpy(out, "inf", 3);
+    return 3;
+  }
+  char sci[64];
+  auto r = std::to_chars(sci, sci + sizeof(sci) - 1, x, std::chars_format::scientific);
+  *r.ptr = '\0';  // atoi below reads the exponent up to the terminator
+  const char* s = sci;
+  const char* end = r.ptr;
+  char* o = out;
+  if (*s == '-') { *o++ = '-'; ++s; }
+  // digits: s[0] [. s[2..epos)] e[+-]XX
+  char digs[32];
+  int nd = 0;
+  const char* ep = (const char*)std::memchr(s, 'e', (size_t)(end - s));
+  for (const char* q = s; q < ep; ++q)
+    if (*q != '.') digs[nd++] = *q;
+  int exp10 = std::atoi(ep + 1);
+  while (nd > 1 && digs[nd - 1] == '0') --nd;  // to_chars gives shortest already; be safe
+  if (exp10 >= -4 && exp10 < 16) {
+    if (exp10 >= nd - 1) {            // integer valued: digits, zeros, ".0"
+      for (int i = 0; i < nd; ++i) *o++ = digs[i];
+      for (int i = nd - 1; i < exp10; ++i) *o++ = '0';
+      *o++ = '.';
+      *o++ = '0';
+    } else if (exp10 < 0) {           // 0.000ddd
+      *o++ = '0';
+      *o++ = '.';
+      for (int i = -1; i > exp10; --i) *o++ = '0';
+      for (int i = 0; i < nd; ++i) *o++ = digs[i];
+    } else {                          // ddd.ddd
+      for (int i = 0; i <= exp10; ++i) *o++ = digs[i];
+      *o++ = '.';
+      for (int i = exp10 + 1; i < nd; ++i) *o++ = digs[i];
+    }
+  } else {
+    *o++ = digs[0];
+    if (nd > 1) {
+      *o++ = '.';
+      for (int i = 1; i < nd; ++i) *o++ = digs[i];
+    }
+    *o++ = 'e';
+    *o++ = exp10 < 0 ? '-' : '+';
+    int a = exp10 < 0 ? -exp10 : exp10;
+    if (a < 10) *o++ = '0';
+    char tmp[8];
+    int k = std::snprintf(tmp, sizeof(tmp), "%d", a);
+    std::memcpy(o, tmp, (size_t)k);
+    o += k;
+  }
+  return (int)(o - out);
+}
+
+int64_t format_binning(char* buf, int64_t cap, const char* cid, const char* charge_str, double prec,
+                       const double* mz, const double* it, int64_t n, int skip_nan) {
+  // worst case per peak: two 24-byte floats + space + newline
+  const size_t need = 64 + std::strlen(cid) + std::strlen(charge_str) + (size_t)n * 52;
+  if ((int64_t)need > cap) return -1;
+  char* o = buf;
+  auto put = [&](const char* s) { size_t k = std::strlen(s); std::memcpy(o, s, k); o += k; };
+  put("BEGIN IONS\nTITLE=");
+  put(cid);
+  put("\nPEPMASS=");
+  o += py_repr(prec, o);
+  put("\nCHARGE=");
+  put(charge_str);
+  put("+\n");
+  for (int64_t k = 0; k < n; ++k) {
+    if (skip_nan && std::isnan(it[k])) continue;
+    o += py_repr(mz[k], o);
+    *o++ = ' ';
+    o += py_repr(it[k], o);
+    *o++ = '\n';
+  }
+  put("END IONS\n\n");
+  return (int64_t)(o - buf);
+}
+
+}  // namespace
+
+extern "C" {
+
+void* spx_mgf_parse(const char* path, int threads) {
+  Result* R = new Result();
+  std::string data;
+  if (!read_file(path, data, R->error)) return R;
+  const char* b = data.data();
+  const char* e = b + data.size();
+  int T = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (data.size() < (1u << 20)) T = 1;
+  // split points at "TITLE=" line starts
+  std::vector<const char*> cuts{b};
+  for (int t = 1; t < T; ++t) {
+    const char* q = b + data.size() * (size_t)t / (size_t)T;
+    if (q <= cuts.back()) continue;
+    while (q < e) {
+      const char* nl = (const char*)std::memchr(q, '\n', (size_t)(e - q));
+      if (!nl) { q = e; break; }
+      q = nl + 1;
+      if (e - q >= 6 && std::memcmp(q, "TITLE=", 6) == 0) break;
+    }
+    if (q < e && q > cuts.back()) cuts.push_back(q);
+  }
+  cuts.push_back(e);
+  const int nc = (int)cuts.size() - 1;
+  std::vector<Chunk> chunks((size_t)nc);
+  std::vector<std::thread> pool;
+  for (int i = 0; i < nc; ++i) pool.emplace_back(parse_range, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
+  for (auto& th : pool) th.join();
+  size_t S = 0, P = 0;
+  for (auto& c : chunks) {
+    if (!c.error.empty()) { R->error = c.error; return R; }
+    S += c.npk.size();
+    P += c.mz.size();
+  }
+  R->spec_off.resize(S + 1);
+  R->mz.reserve(P);
+  R->it.reserve(P);
+  R->spec_off[0] = 0;
+  size_t s = 0;
+  for (auto& c : chunks) {
+    for (size_t k = 0; k < c.npk.size(); ++k, ++s) R->spec_off[s + 1] = R->spec_off[s] + c.npk[k];
+    R->mz.insert(R->mz.end(), c.mz.begin(), c.mz.end());
+    R->it.insert(R->it.end(), c.it.begin(), c.it.end());
+    R->prec.insert(R->prec.end(), c.prec.begin(), c.prec.end());
+    R->charge.insert(R->charge.end(), c.charge.begin(), c.charge.end());
+    R->flags.insert(R->flags.end(), c.flags.begin(), c.flags.end());
+    R->titles += c.titles;
+  }
+  return R;
+}
+
+const char* spx_mgf_error(void* h) {
+  Result* R = static_cast<Result*>(h);
+  return R->error.empty() ? nullptr : R->error.c_str();
+}
+int64_t spx_mgf_n_spectra(void* h) { return (int64_t)static_cast<Result*>(h)->prec.size(); }
+int64_t spx_mgf_n_peaks(void* h) { return (int64_t)static_cast<Result*>(h)->mz.size(); }
+void spx_mgf_copy(void* h, int64_t* spec_off, double* mz, double* it, double* prec, int64_t* charge, int32_t* flags) {
+  Result* R = static_cast<Result*>(h);
+  std::copy(R->spec_off.begin(), R->spec_off.end(), spec_off);
+  std::copy(R->mz.begin(), R->mz.end(), mz);
+  std::copy(R->it.begin(), R->it.end(), it);
+  std::copy(R->prec.begin(), R->prec.end(), prec);
+  std::copy(R->charge.begin(), R->charge.end(), charge);
+  std::copy(R->flags.begin(), R->flags.end(), flags);
+}
+const char* spx_mgf_titles(void* h) { return static_cast<Result*>(h)->titles.c_str(); }
+void spx_mgf_free(void* h) { delete static_cast<Result*>(h); }
+
+int64_t spx_mgf_format_binning(char* buf, int64_t cap, const char* cid, const char* charge_str, double prec,
+                               const double* mz, const double* it, int64_t n, int skip_nan) {
+  return format_binning(buf, cap, cid, charge_str, prec, mz, it, n, skip_nan);
+}
+
+int spx_py_repr(double x, char* out) { return py_repr(x, out); }
+
+// Write C consensus spectra (dense layout: cluster c = peaks [off[c], off[c+1]))
+// as binning.py:234-245 text, formatted in parallel, written in order.
+// ids: '\n'-joined cluster ids.  Returns 0, or -1 on an I/O error.
+int spx_mgf_write_binning_batch(const char* path, int64_t C, const char* ids, const int64_t* charge,
+                                const double* prec, const int64_t* off, const double* mz, const double* it,
+                                int threads) {
+  std::vector<const char*> idp((size_t)C);
+  std::vector<size_t> idl((size_t)C);
+  const char* q = ids;
+  for (int64_t c = 0; c < C; ++c) {
+    const char* nl = std::strchr(q, '\n');
+    idp[(size_t)c] = q;
+    idl[(size_t)c] = nl ? (size_t)(nl - q) : std::strlen(q);
+    q = nl ? nl + 1 : q + idl[(size_t)c];
+  }
+  int T = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return -1;
+  const int64_t block = 4096;
+  int rc = 0;
+  for (int64_t c0 = 0; c0 < C && rc == 0; c0 += block * T) {
+    std::vector<std::string> parts((size_t)T);
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) {
+      pool.emplace_back([&, t]() {
+        const int64_t a = c0 + t * block, b = std::min(C, a + block);
+        std::string& out = parts[(size_t)t];
+        std::vector<char> buf;
+        for (int64_t c = a; c < b; ++c) {
+          std::string cid(idp[(size_t)c], idl[(size_t)c]);
+          char zs[32];
+          std::snprintf(zs, sizeof(zs), "%lld", (long long)charge[c]);
+          const int64_t n = off[c + 1] - off[c];
+          const size_t cap = 128 + cid.size() + (size_t)n * 52;
+          if (buf.size() < cap) buf.resize(cap);
+          const int64_t w = format_binning(buf.data(), (int64_t)cap, cid.c_str(), zs, prec[c], mz + off[c],
+                                           it + off[c], n, 1);
+          out.append(buf.data(), (size_t)w);
+        }
+      });
+    }
+    for (auto& th : pool) th.join();
+    for (auto& s : parts)
+      if (!s.empty() && std::fwrite(s.data(), 1, s.size(), f) != s.size()) rc = -1;
+  }
+  if (std::fclose(f) != 0) rc = -1;
+  return rc;
+}
+
+}  // extern "C"

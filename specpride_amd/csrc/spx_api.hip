@@ -193,10 +193,11 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
   for (int64_t c = 0; c < C; ++c) {
     const int64_t n = hco[c + 1] - hco[c];
     const int64_t p = hso[hco[c + 1]] - hso[hco[c]];
-    const int64_t K = std::min<int64_t>(std::max<int64_t>(p, 1), (int64_t)spx::MD_WMAX * 64);
+    const int64_t K = std::max<int64_t>(p, 1);  // occupied bins <= peaks
     const int64_t KW = (K + 63) / 64;
     const int64_t T = (n + spx::MD_TILE - 1) / spx::MD_TILE;
-    const size_t bytes = (size_t)(T * spx::MD_TILE * KW * 8) + align256((size_t)(n * n * 4));
+    const size_t bytes = (size_t)(T * spx::MD_TILE * KW * 8) + align256((size_t)(n * n * 4)) +
+                         align256((size_t)K * 12);  // + level-2 occupancy words
     if (n > spx::MD_NMAX) arena += bytes;
     else if (n > 1) margin = std::max(margin, bytes);
   }

@@ -10,6 +10,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#ifdef SPX_DEBUG
+#include <stdio.h>
+// Debug builds only: report an out-of-range index instead of touching memory.
+#define SPX_GUARD(cond, ...)        \
+  if (!(cond)) {                    \
+    printf(__VA_ARGS__);            \
+  } else
+#else
+#define SPX_GUARD(cond, ...)
+#endif
+
 namespace spx {
 
 constexpr int kWave = 64;
