@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU quick loop: parity tests then bench (no CPU baseline).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$PWD}
+cd "$R"
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
+echo "pytest rc=$?" >> gpurun_out/gpu_tests.log
+tail -3 gpurun_out/gpu_tests.log
+grep -q "pytest rc=0" gpurun_out/gpu_tests.log || exit 1
+timeout -k 10 600 python bench.py --no-cpu-baseline "$@" > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log

@@ -46,6 +46,8 @@ struct BinMeanState {
   float* acc_i;
   float* acc_m;
   uint32_t* owner;
+  int32_t* soff;  // LDS copy of the spectrum offsets (nullptr: read spec_off)
+  int* votes;
   int dcap;
   int nmax;  // clusters with more spectra are deferred (leaf-only pairwise mean)
 };
@@ -62,6 +64,8 @@ struct BinMeanSmem {
   float acc_i[BM_DCAP];
   float acc_m[BM_DCAP];
   uint32_t owner[BM_DCAP];
+  int32_t soff[BM_NMAX + 1];  // the cluster's spectrum offsets, relative to its first peak
+  int votes[2 * (BM_BLOCK / kWave)];
   int tmp[BM_BLOCK / kWave + 1];
   int flag;
 };
@@ -119,25 +123,67 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   }
   if (n > S.nmax || P.n_words > (kSmall ? BM_WMAX : 0x7fffffff)) return kDeferred;
 
+  // spectrum boundaries, from LDS when the cluster is small enough
+  if constexpr (kSmall)
+    for (int64_t j = tid; j <= n; j += BM_BLOCK) S.soff[j] = (int32_t)(v.spec_off[s0 + j] - p0);
+  auto spec_a = [&](int64_t s) -> int64_t {
+    if constexpr (kSmall) return p0 + S.soff[s - s0];
+    else return v.spec_off[s];
+  };
+  auto spec_e = [&](int64_t s) -> int64_t {
+    if constexpr (kSmall) return p0 + S.soff[s - s0 + 1];
+    else return v.spec_off[s + 1];
+  };
+
   // charge check (binning.py:205-206) -- nothing is emitted for a mixed cluster
   const int32_t z0 = v.charge[s0];
   int mixed = 0;
   for (int64_t s = s0 + 1 + tid; s < s1; s += BM_BLOCK) mixed |= v.charge[s] != z0;
   for (int w = tid; w < P.n_words; w += BM_BLOCK) S.bitmap[w] = 0ull;
-  if (__syncthreads_or(mixed)) {
+  // (a full barrier on the global path: the bitmap zeroing must land before
+  // any wave's phase-1 atomicOr; hip's __syncthreads_or orders LDS only)
+  if (block_any<BM_BLOCK, kSmall>(mixed, S.votes, 1)) {
     if (tid == 0) { out.count[c] = 0; prec_out[c] = __longlong_as_double(0x7ff8000000000000ll); charge_out[c] = 0; }
     return kMixedCharge;
   }
 
-  // phase 1: occupied-bin bitmap
-  for (int64_t k = p0 + tid; k < p1; k += BM_BLOCK) {
-    const double m = v.mz[k];
-    if (in_range(m, P)) {
-      const int64_t b = bin_of(m, P);
-      atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
+  // phase 1: occupied-bin bitmap (8 independent loads in flight per thread).
+  // The small path also checks that every spectrum is m/z-sorted (the common
+  // case: it lets phase 3 use a neighbour compare and a branch-free prefetch).
+  int irregular = 0;
+  if constexpr (kSmall) {
+    for (int64_t j = tid; j < n; j += BM_BLOCK) irregular |= (S.soff[j + 1] - S.soff[j]) > BM_BLOCK;
+  }
+  for (int64_t k0 = p0 + tid; k0 < p1; k0 += 8 * BM_BLOCK) {
+    double m[8], mn[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = k0 + (int64_t)u * BM_BLOCK;
+      m[u] = v.mz[k < p1 ? k : p0];
+      if constexpr (kSmall) mn[u] = v.mz[k + 1 < p1 ? k + 1 : p0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = k0 + (int64_t)u * BM_BLOCK;
+      if (k >= p1) continue;
+      if constexpr (kSmall) {
+        // k+1 starts a new spectrum iff it is one of the LDS offsets
+        if (k + 1 < p1 && !(m[u] <= mn[u])) {
+          const int32_t r = (int32_t)(k + 1 - p0);
+          int lo = 0, hi = (int)n;  // soff[lo] <= r
+          while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (S.soff[mid] <= r) lo = mid; else hi = mid; }
+          irregular |= S.soff[lo] != r;
+        }
+      }
+      if (in_range(m[u], P)) {
+        const int64_t b = bin_of(m[u], P);
+        atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
+      }
     }
   }
-  __syncthreads();
+  // (the vote is also the barrier between phase-1 ORs and phase-2 reads: always taken)
+  const int irregular_any = block_any<BM_BLOCK, kSmall>(irregular, S.votes, 0);
+  const bool fast = kSmall && !irregular_any && p1 > p0;
 
   // phase 2: compact slot ids in bin order
   const int D = bitmap_prefix<BM_BLOCK>(S.bitmap, S.wprefix, P.n_words, tmp);
@@ -151,43 +197,69 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   __syncthreads();
 
   // phase 3: ordered accumulation, one spectrum at a time
-  for (int64_t s = s0; s < s1; ++s) {
-    const int64_t a = v.spec_off[s], e = v.spec_off[s + 1];
-    if (e - a <= BM_BLOCK) {
-      const PeakLane L = load_lane(v, a + tid, e);
-      const int unsorted = L.active && L.has_next && !(L.m <= L.mn);
-      if (!__syncthreads_or(unsorted)) {
-        sorted_lane(S, P, L);
-        continue;
+  if (fast) {
+    // Every spectrum sorted and <= 256 peaks: lane t holds peak t.  The lanes
+    // of the next PF spectra are in flight in a register ring; loads are
+    // unconditional (clamped addresses) so the wait before each use is a
+    // counted vmcnt, and one barrier per spectrum orders the slot updates.
+    if constexpr (kSmall) {
+      auto fetch = [&](int64_t j) {
+        const int64_t jj = j < n ? j : n - 1;
+        const int64_t a = p0 + S.soff[jj], e = p0 + S.soff[jj + 1];
+        const int64_t k = a + tid;
+        PeakLane L;
+        L.m = v.mz[k < e ? k : p0];
+        L.it = v.inten[k < e ? k : p0];
+        L.mn = v.mz[k + 1 < e ? k + 1 : p0];
+        L.active = j < n && k < e;
+        L.has_next = j < n && k + 1 < e;
+        return L;
+      };
+      constexpr int PF = 8;
+      PeakLane ring[PF];
+#pragma unroll
+      for (int j = 0; j < PF; ++j) ring[j] = fetch(j);
+      for (int64_t jb = 0; jb < n; jb += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) {
+          if (jb + j < n) {
+            lds_barrier();
+            sorted_lane(S, P, ring[j]);
+            ring[j] = fetch(jb + j + PF);  // refill the slot just consumed
+          }
+        }
       }
-    } else {
+    }
+  } else {
+    for (int64_t s = s0; s < s1; ++s) {
+      const int64_t a = spec_a(s), e = spec_e(s);
       int unsorted = 0;
       for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
         const PeakLane L = load_lane(v, k, e);
         unsorted |= L.active && L.has_next && !(L.m <= L.mn);
       }
-      if (!__syncthreads_or(unsorted)) {
+      if (!block_any<BM_BLOCK, kSmall>(unsorted, S.votes, (int)(s & 1))) {
         for (int64_t k = a + tid; k < e; k += BM_BLOCK) sorted_lane(S, P, load_lane(v, k, e));
         continue;
       }
-    }
-    // unsorted spectrum: the highest file position per slot wins (tags grow
-    // monotonically through the cluster, so stale tags never win)
-    if (*flag == 0) {
-      for (int d = tid; d < D; d += BM_BLOCK) S.owner[d] = 0u;
+      // unsorted spectrum: the highest file position per slot wins (tags grow
+      // monotonically through the cluster, so stale tags never win)
+      if (*flag == 0) {
+        for (int d = tid; d < D; d += BM_BLOCK) S.owner[d] = 0u;
+        __syncthreads();
+        if (tid == 0) *flag = 1;
+      }
+      for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
+        const double m = v.mz[k];
+        if (in_range(m, P)) atomicMax(&S.owner[bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P))], (uint32_t)(k - p0 + 1));
+      }
       __syncthreads();
-      if (tid == 0) *flag = 1;
-    }
-    for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
-      const double m = v.mz[k];
-      if (in_range(m, P)) atomicMax(&S.owner[bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P))], (uint32_t)(k - p0 + 1));
-    }
-    __syncthreads();
-    for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
-      const double m = v.mz[k];
-      if (!in_range(m, P)) continue;
-      const int slot = bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P));
-      if (S.owner[slot] == (uint32_t)(k - p0 + 1)) accumulate(S, slot, m, v.inten[k]);
+      for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
+        const double m = v.mz[k];
+        if (!in_range(m, P)) continue;
+        const int slot = bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P));
+        if (S.owner[slot] == (uint32_t)(k - p0 + 1)) accumulate(S, slot, m, v.inten[k]);
+      }
     }
   }
   __syncthreads();
@@ -232,7 +304,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_lds_kernel(CsrView v, BinMe
                                                                 int32_t* n_deferred) {
   __shared__ BinMeanSmem L;
   const int64_t c = blockIdx.x;
-  BinMeanState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, L.owner, BM_DCAP, BM_NMAX};
+  BinMeanState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, L.owner, L.soff, L.votes, BM_DCAP, BM_NMAX};
   const int32_t st = bin_mean_body<true>(v, P, S, c, out, prec_out, charge_out, L.tmp, &L.flag);
   if (threadIdx.x == 0) {
     status[c] = st;
@@ -265,6 +337,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, Bi
                                                                    const int32_t* n_deferred, char* scratch,
                                                                    int64_t slice_bytes, int dcap) {
   __shared__ int tmp[BM_BLOCK / kWave + 1];
+  __shared__ int votes[2 * (BM_BLOCK / kWave)];
   __shared__ int flag;
   char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
   const BinSliceLayout Lo = bin_slice_layout(P.n_words, dcap);
@@ -275,6 +348,8 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, Bi
   S.acc_i = reinterpret_cast<float*>(base + Lo.acc_i);
   S.acc_m = reinterpret_cast<float*>(base + Lo.acc_m);
   S.owner = reinterpret_cast<uint32_t*>(base + Lo.owner);
+  S.soff = nullptr;
+  S.votes = votes;
   S.dcap = dcap;
   S.nmax = 0x7fffffff;
   const int32_t nd = *n_deferred;

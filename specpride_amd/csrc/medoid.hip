@@ -160,23 +160,58 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
     return;
   }
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
+  // bin range from each spectrum's first and last peak (m/z-sorted spectra);
+  // pass 1 verifies every bin falls inside and defers the cluster otherwise
+  long long blo = 0x7fffffffffffffffll, bhi = -0x7fffffffffffffffll;
   if (tid <= n) L.soff[tid] = (int32_t)(v.spec_off[s0 + tid] - p0);
-
-  int64_t blo, bhi;
-  const bool any = cluster_bin_range(v, p0, p1, P, L.red, blo, bhi);
+  if (tid < n) {
+    const int64_t a = v.spec_off[s0 + tid], e = v.spec_off[s0 + tid + 1];
+    if (e > a) {
+      blo = md_bin(v.mz[a], P);
+      bhi = md_bin(v.mz[e - 1], P);
+    }
+  }
+  if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const long long l2 = __shfl_xor(blo, o, kWave), h2 = __shfl_xor(bhi, o, kWave);
+      blo = l2 < blo ? l2 : blo;
+      bhi = h2 > bhi ? h2 : bhi;
+    }
+    if (tid == 0) { L.red[0] = blo; L.red[1] = bhi; }
+  }
+  __syncthreads();
+  blo = L.red[0];
+  bhi = L.red[1];
+  const bool any = p1 > p0;
   const int64_t nw = any ? (bhi - blo) / 64 + 1 : 0;
-  if (nw > MD_WMAX) {
+  if (nw > MD_WMAX || (any && bhi < blo)) {
     if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
     return;
   }
-  // 1: union bitmap
+  // 1: union bitmap (8 loads in flight per thread)
   for (int w = tid; w < nw; w += MD_BLOCK) L.bitmap[w] = 0ull;
   __syncthreads();
-  for (int64_t k = p0 + tid; k < p1; k += MD_BLOCK) {
-    const int64_t b = md_bin(v.mz[k], P) - blo;
-    atomicOr(&L.bitmap[b >> 6], 1ull << (b & 63));
+  int outside = 0;
+  for (int64_t k0 = p0 + tid; k0 < p1; k0 += 8 * MD_BLOCK) {
+    double m[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = k0 + (int64_t)u * MD_BLOCK;
+      m[u] = k < p1 ? v.mz[k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (k0 + (int64_t)u * MD_BLOCK >= p1) continue;
+      const int64_t b = md_bin(m[u], P) - blo;
+      if (b < 0 || b >= nw * 64) { outside = 1; continue; }
+      atomicOr(&L.bitmap[b >> 6], 1ull << (b & 63));
+    }
   }
-  __syncthreads();
+  if (__syncthreads_or(outside)) {  // an unsorted spectrum: general path
+    if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    return;
+  }
   // 2: compact columns
   const int K = bitmap_prefix<MD_BLOCK>(L.bitmap, L.wprefix, (int)nw, L.tmp);
   const int KW = (K + 63) / 64;
@@ -187,10 +222,21 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
   // 3: bit-packed rows
   for (int w = tid; w < n * KW; w += MD_BLOCK) L.rows[w] = 0ull;
   __syncthreads();
-  for (int64_t k = p0 + tid; k < p1; k += MD_BLOCK) {
-    const int col = bitmap_rank(L.bitmap, L.wprefix, md_bin(v.mz[k], P) - blo);
-    const int s = spectrum_of(L.soff, n, (int32_t)(k - p0));
-    atomicOr(&L.rows[s * KW + (col >> 6)], 1ull << (col & 63));
+  for (int64_t k0 = p0 + tid; k0 < p1; k0 += 8 * MD_BLOCK) {
+    double m[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = k0 + (int64_t)u * MD_BLOCK;
+      m[u] = k < p1 ? v.mz[k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = k0 + (int64_t)u * MD_BLOCK;
+      if (k >= p1) continue;
+      const int col = bitmap_rank(L.bitmap, L.wprefix, md_bin(m[u], P) - blo);
+      const int sp = spectrum_of(L.soff, n, (int32_t)(k - p0));
+      atomicOr(&L.rows[sp * KW + (col >> 6)], 1ull << (col & 63));
+    }
   }
   __syncthreads();
   // 4: shared-bin counts for every pair i <= j

@@ -104,6 +104,39 @@ __device__ __forceinline__ T block_exclusive_scan(T v, T* tmp, T& total) {
   return base + inc - v;
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a release/acquire
+// fence on ALL address spaces: its release waits for every outstanding global
+// load (vmcnt), which drains any prefetch in flight.  Steps that exchange data
+// only through LDS use this instead, so register prefetches survive it.
+// The LDS-scoped fences only pin the compiler's ordering (on gfx950 they emit
+// no wait); the explicit lgkmcnt(0) makes this wave's LDS writes complete
+// before the barrier releases the other waves.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: vmcnt/expcnt left alone
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Block-wide OR with ONE barrier: wave ballot, one LDS word per wave, barrier,
+// read.  `votes` holds 2 x (BLOCK/64) ints; alternate `parity` between
+// consecutive calls so a fast wave's next vote cannot overwrite a word a slow
+// wave is still reading.  (hip's __syncthreads_or costs three barriers.)
+// kLdsOnly: the barrier may ignore global memory (all shared state is in LDS);
+// otherwise it is a full __syncthreads() (state in global scratch).
+template <int BLOCK, bool kLdsOnly = true>
+__device__ __forceinline__ int block_any(int pred, int* votes, int parity) {
+  constexpr int NW = BLOCK / kWave;
+  const int w = __ballot(pred) != 0ull;
+  if (lane_id() == 0) votes[parity * NW + wave_id()] = w;
+  if constexpr (kLdsOnly) lds_barrier();
+  else __syncthreads();
+  int r = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) r |= votes[parity * NW + k];
+  return r;
+}
+
 // ------------------------------------------------------ exact bin indexing
 // trunc(fl((m - lo) / w)) and ceil(fl(m / w)) exactly as numpy / OpenMS compute
 // them (IEEE subtract + correctly rounded divide), without paying a f64 divide
