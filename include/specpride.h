@@ -13,6 +13,7 @@
  *                       + precursor helpers :106-148 (called from :151-165)
  *   spx_medoid       <- src/most_similar_representative.py:13-19 distance() and the
  *                       per-cluster medoid loop :60-111
+ *   spx_xcorr_distance <- src/most_similar_representative.py:13-19 distance() per pair
  *   spx_compact_peaks   (packing helper for the shims' output writers)
  *
  * Conventions
@@ -131,6 +132,12 @@ size_t spx_medoid_workspace_size(const int64_t *host_cluster_off, const int64_t 
  * totals (nullable) [n_spectra] = the reference's total_dist per spectrum. */
 int spx_medoid(const spx_csr *csr, const spx_medoid_params *params, int64_t *rep, double *totals,
                void *workspace, size_t workspace_bytes, void *stream);
+
+/* distance(spec1, spec2, 'xcorr') = 1 - xCorrelationPrescore for n_pairs (global
+ * spectrum index) pairs: out[p] for pairs[2p], pairs[2p+1].  The per-call API
+ * behind most_similar_representative.distance (:13-19); not the batched path. */
+int spx_xcorr_distance(const spx_csr *csr, const spx_medoid_params *params, const int64_t *pairs,
+                       int64_t n_pairs, double *out, void *stream);
 
 /* Pack the per-cluster outputs densely: dst[out_off[c] + k] = src[spec_off[cluster_off[c]] + k]
  * for k < count[c]; out_off is the exclusive prefix sum of count (device array [C+1]). */

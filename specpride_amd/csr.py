@@ -20,6 +20,18 @@ from typing import Iterable, Sequence
 import numpy as np
 
 
+def concat_ranges(starts: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """concatenate(arange(s, s + n) for s, n in zip(starts, lens)), vectorised."""
+    starts = np.asarray(starts, np.int64)
+    lens = np.asarray(lens, np.int64)
+    total = int(lens.sum())
+    if total == 0:
+        return np.zeros(0, np.int64)
+    first = np.zeros(len(lens), np.int64)
+    np.cumsum(lens[:-1], out=first[1:])
+    return np.repeat(starts - first, lens) + np.arange(total, dtype=np.int64)
+
+
 @dataclass
 class SpectraCSR:
     cluster_off: np.ndarray
@@ -127,19 +139,15 @@ class SpectraCSR:
 
     def select(self, clusters: Iterable[int]) -> "SpectraCSR":
         """A new batch holding only ``clusters`` (in the given order)."""
-        clusters = np.asarray(list(clusters), np.int64)
-        spec_ranges = [np.arange(self.cluster_off[c], self.cluster_off[c + 1]) for c in clusters]
-        spectra = np.concatenate(spec_ranges) if spec_ranges else np.zeros(0, np.int64)
-        sizes = np.array([len(r) for r in spec_ranges], np.int64)
+        clusters = np.asarray(list(clusters) if not isinstance(clusters, np.ndarray) else clusters, np.int64)
+        sizes = self.cluster_off[clusters + 1] - self.cluster_off[clusters]
         cluster_off = np.zeros(len(clusters) + 1, np.int64)
         np.cumsum(sizes, out=cluster_off[1:])
+        spectra = concat_ranges(self.cluster_off[clusters], sizes)
         lens = self.spec_off[spectra + 1] - self.spec_off[spectra]
         spec_off = np.zeros(len(spectra) + 1, np.int64)
         np.cumsum(lens, out=spec_off[1:])
-        if len(spectra):
-            idx = np.concatenate([np.arange(self.spec_off[s], self.spec_off[s + 1]) for s in spectra])
-        else:
-            idx = np.zeros(0, np.int64)
+        idx = concat_ranges(self.spec_off[spectra], lens)
         ids = [self.cluster_ids[c] for c in clusters] if self.cluster_ids else []
         titles = [self.titles[s] for s in spectra] if self.titles else []
         return SpectraCSR(cluster_off, spec_off, self.mz[idx], self.inten[idx], self.prec_mz[spectra],

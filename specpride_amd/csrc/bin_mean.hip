@@ -36,6 +36,7 @@ struct BinMeanParams {
   double minimum, maximum, binsize, inv_binsize;
   int32_t apply_quorum;
   int32_t n_words;  // ceil(n_bins / 64)
+  int32_t ablate;   // profiling only (SPX_ABLATE): 1 skip phase 3, 2 skip phase 4
 };
 
 template <class PrefixT>
@@ -48,6 +49,7 @@ struct BinMeanState {
   uint32_t* owner;
   int32_t* soff;  // LDS copy of the spectrum offsets (nullptr: read spec_off)
   int* votes;
+  int32_t* xch;
   int dcap;
   int nmax;  // clusters with more spectra are deferred (leaf-only pairwise mean)
 };
@@ -66,6 +68,7 @@ struct BinMeanSmem {
   uint32_t owner[BM_DCAP];
   int32_t soff[BM_NMAX + 1];  // the cluster's spectrum offsets, relative to its first peak
   int votes[2 * (BM_BLOCK / kWave)];
+  int32_t xch[2 * (BM_BLOCK / kWave)];  // lane-0 bin key of each wave (fast path neighbour)
   int tmp[BM_BLOCK / kWave + 1];
   int flag;
 };
@@ -147,35 +150,22 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
     return kMixedCharge;
   }
 
-  // phase 1: occupied-bin bitmap (8 independent loads in flight per thread).
-  // The small path also checks that every spectrum is m/z-sorted (the common
-  // case: it lets phase 3 use a neighbour compare and a branch-free prefetch).
-  int irregular = 0;
+  // phase 1: occupied-bin bitmap (16 independent loads in flight per thread)
+  int irregular = 0;  // a spectrum longer than the block: no fast path
   if constexpr (kSmall) {
     for (int64_t j = tid; j < n; j += BM_BLOCK) irregular |= (S.soff[j + 1] - S.soff[j]) > BM_BLOCK;
   }
-  for (int64_t k0 = p0 + tid; k0 < p1; k0 += 8 * BM_BLOCK) {
-    double m[8], mn[8];
+  constexpr int U1 = 16;
+  for (int64_t k0 = p0 + tid; k0 < p1; k0 += U1 * BM_BLOCK) {
+    double m[U1];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U1; ++u) {
       const int64_t k = k0 + (int64_t)u * BM_BLOCK;
       m[u] = v.mz[k < p1 ? k : p0];
-      if constexpr (kSmall) mn[u] = v.mz[k + 1 < p1 ? k + 1 : p0];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t k = k0 + (int64_t)u * BM_BLOCK;
-      if (k >= p1) continue;
-      if constexpr (kSmall) {
-        // k+1 starts a new spectrum iff it is one of the LDS offsets
-        if (k + 1 < p1 && !(m[u] <= mn[u])) {
-          const int32_t r = (int32_t)(k + 1 - p0);
-          int lo = 0, hi = (int)n;  // soff[lo] <= r
-          while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (S.soff[mid] <= r) lo = mid; else hi = mid; }
-          irregular |= S.soff[lo] != r;
-        }
-      }
-      if (in_range(m[u], P)) {
+    for (int u = 0; u < U1; ++u) {
+      if (k0 + (int64_t)u * BM_BLOCK < p1 && in_range(m[u], P)) {
         const int64_t b = bin_of(m[u], P);
         atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
       }
@@ -197,11 +187,17 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   __syncthreads();
 
   // phase 3: ordered accumulation, one spectrum at a time
-  if (fast) {
-    // Every spectrum sorted and <= 256 peaks: lane t holds peak t.  The lanes
-    // of the next PF spectra are in flight in a register ring; loads are
-    // unconditional (clamped addresses) so the wait before each use is a
-    // counted vmcnt, and one barrier per spectrum orders the slot updates.
+  int64_t slow_from = (P.ablate & 1) ? s1 : s0;
+  if (fast && !(P.ablate & 1)) {
+    // Optimistic fast path (every spectrum <= 256 peaks; lane t holds peak t).
+    // Each lane computes ONE bin key (-1 below min, INT_MAX at/above max) and
+    // takes its neighbour's key by shuffle (lane 63: from the next wave via
+    // LDS).  If keys are non-decreasing inside every spectrum, equal bins are
+    // contiguous and "last peak of its bin" is a neighbour compare.  A key
+    // inversion or a NaN anywhere sets a flag and the whole cluster is redone
+    // on the slow path below, so the fast path never commits a wrong answer.
+    // Slot lookups happen before the barrier; behind it only the slot
+    // read-modify-write, so one barrier per spectrum is the whole serial cost.
     if constexpr (kSmall) {
       auto fetch = [&](int64_t j) {
         const int64_t jj = j < n ? j : n - 1;
@@ -210,60 +206,99 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
         PeakLane L;
         L.m = v.mz[k < e ? k : p0];
         L.it = v.inten[k < e ? k : p0];
-        L.mn = v.mz[k + 1 < e ? k + 1 : p0];
+        L.mn = 0.0;
         L.active = j < n && k < e;
         L.has_next = j < n && k + 1 < e;
         return L;
       };
+      const int lane = lane_id(), wid = wave_id();
+      int bad = 0;
       constexpr int PF = 8;
-      PeakLane ring[PF];
+      PeakLane A[PF], B[PF];
 #pragma unroll
-      for (int j = 0; j < PF; ++j) ring[j] = fetch(j);
+      for (int j = 0; j < PF; ++j) A[j] = fetch(j);
       for (int64_t jb = 0; jb < n; jb += PF) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) B[j] = fetch(jb + PF + j);
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
           if (jb + j < n) {
+            const PeakLane& L = A[j];
+            const int par = (int)((jb + j) & 1);
+            int32_t key = L.m < P.minimum ? -1 : 0x7fffffff;
+            bad |= L.active && (L.m != L.m);
+            int slot = -1;
+            if (L.active && in_range(L.m, P)) {
+              const int64_t b = bin_of(L.m, P);
+              key = (int32_t)b;
+              slot = bitmap_rank(S.bitmap, S.wprefix, b);
+            }
+            const int32_t kn = __shfl_down(key, 1, kWave);
+            if (lane == 0) S.xch[par * (BM_BLOCK / kWave) + wid] = key;
+            if (lane < kWave - 1 && L.has_next) bad |= key > kn;
+            bool last = !(lane < kWave - 1 && L.has_next && kn == key);
             lds_barrier();
-            sorted_lane(S, P, ring[j]);
-            ring[j] = fetch(jb + j + PF);  // refill the slot just consumed
+            if (lane == kWave - 1 && L.has_next) {
+              const int32_t kx = S.xch[par * (BM_BLOCK / kWave) + wid + 1];
+              bad |= key > kx;
+              last = kx != key;
+            }
+            if (slot >= 0 && last) accumulate(S, slot, L.m, L.it);
           }
         }
+#pragma unroll
+        for (int j = 0; j < PF; ++j) A[j] = B[j];
+      }
+      if (block_any<BM_BLOCK, true>(bad, S.votes, 1)) {
+        // redo the cluster on the slow path from a clean slate
+        for (int d = tid; d < D; d += BM_BLOCK) {
+          S.cnt[d] = 0u;
+          S.acc_i[d] = 0.0f;
+          S.acc_m[d] = 0.0f;
+        }
+        __syncthreads();
+        slow_from = s0;
+      } else {
+        slow_from = s1;
       }
     }
-  } else {
-    for (int64_t s = s0; s < s1; ++s) {
-      const int64_t a = spec_a(s), e = spec_e(s);
-      int unsorted = 0;
-      for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
-        const PeakLane L = load_lane(v, k, e);
-        unsorted |= L.active && L.has_next && !(L.m <= L.mn);
-      }
-      if (!block_any<BM_BLOCK, kSmall>(unsorted, S.votes, (int)(s & 1))) {
-        for (int64_t k = a + tid; k < e; k += BM_BLOCK) sorted_lane(S, P, load_lane(v, k, e));
-        continue;
-      }
-      // unsorted spectrum: the highest file position per slot wins (tags grow
-      // monotonically through the cluster, so stale tags never win)
-      if (*flag == 0) {
-        for (int d = tid; d < D; d += BM_BLOCK) S.owner[d] = 0u;
-        __syncthreads();
-        if (tid == 0) *flag = 1;
-      }
-      for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
-        const double m = v.mz[k];
-        if (in_range(m, P)) atomicMax(&S.owner[bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P))], (uint32_t)(k - p0 + 1));
-      }
+  }
+  for (int64_t s = slow_from; s < s1; ++s) {
+    const int64_t a = spec_a(s), e = spec_e(s);
+    int unsorted = 0;
+    for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
+      const PeakLane L = load_lane(v, k, e);
+      unsorted |= L.active && L.has_next && !(L.m <= L.mn);
+    }
+    if (!block_any<BM_BLOCK, kSmall>(unsorted, S.votes, (int)((s - s0) & 1))) {
+      for (int64_t k = a + tid; k < e; k += BM_BLOCK) sorted_lane(S, P, load_lane(v, k, e));
+      continue;
+    }
+    // unsorted spectrum: the highest file position per slot wins (tags grow
+    // monotonically through the cluster, so stale tags never win)
+    if (*flag == 0) {
+      for (int d = tid; d < D; d += BM_BLOCK) S.owner[d] = 0u;
       __syncthreads();
-      for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
-        const double m = v.mz[k];
-        if (!in_range(m, P)) continue;
-        const int slot = bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P));
-        if (S.owner[slot] == (uint32_t)(k - p0 + 1)) accumulate(S, slot, m, v.inten[k]);
-      }
+      if (tid == 0) *flag = 1;
+    }
+    for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
+      const double m = v.mz[k];
+      if (in_range(m, P)) atomicMax(&S.owner[bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P))], (uint32_t)(k - p0 + 1));
+    }
+    __syncthreads();
+    for (int64_t k = a + tid; k < e; k += BM_BLOCK) {
+      const double m = v.mz[k];
+      if (!in_range(m, P)) continue;
+      const int slot = bitmap_rank(S.bitmap, S.wprefix, bin_of(m, P));
+      if (S.owner[slot] == (uint32_t)(k - p0 + 1)) accumulate(S, slot, m, v.inten[k]);
     }
   }
   __syncthreads();
 
+  if (P.ablate & 2) {
+    if (tid == 0) out.count[c] = 0;
+    return kOk;
+  }
   // phase 4: quorum filter and ordered output (binning.py:181-183, 209-222)
   const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
   const int per = (D + BM_BLOCK - 1) / BM_BLOCK;
@@ -304,7 +339,8 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_lds_kernel(CsrView v, BinMe
                                                                 int32_t* n_deferred) {
   __shared__ BinMeanSmem L;
   const int64_t c = blockIdx.x;
-  BinMeanState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, L.owner, L.soff, L.votes, BM_DCAP, BM_NMAX};
+  BinMeanState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, L.owner, L.soff, L.votes, L.xch, BM_DCAP,
+                           BM_NMAX};
   const int32_t st = bin_mean_body<true>(v, P, S, c, out, prec_out, charge_out, L.tmp, &L.flag);
   if (threadIdx.x == 0) {
     status[c] = st;
@@ -350,6 +386,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, Bi
   S.owner = reinterpret_cast<uint32_t*>(base + Lo.owner);
   S.soff = nullptr;
   S.votes = votes;
+  S.xch = nullptr;
   S.dcap = dcap;
   S.nmax = 0x7fffffff;
   const int32_t nd = *n_deferred;

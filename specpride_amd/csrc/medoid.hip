@@ -27,12 +27,14 @@ namespace spx {
 
 struct MedoidParams {
   double tol, inv_tol;
+  int32_t ablate;  // profiling only (SPX_ABLATE): 16 skip rows+pairs, 32 skip totals
 };
 
 constexpr int MD_BLOCK = 256;
 constexpr int MD_NMAX = 64;
 constexpr int MD_WMAX = 1024;    // union-bitmap words: bin range <= 65,536 (6,553 Da at 0.1)
-constexpr int MD_KWMAX = 32;     // row words: <= 2,048 occupied bins per small cluster
+constexpr int MD_KWMAX = 31;     // row words (odd stride): <= 1,984 occupied bins per small cluster
+constexpr int MD_PMAX = 16384;   // peaks per small cluster (spectrum-start bitmap)
 constexpr int MD_TILE = 64;      // Gram tile (large path)
 constexpr int MD_KCHUNK = 32;    // u64 words per LDS stage (large path)
 
@@ -42,6 +44,8 @@ struct MedoidSmem {
   unsigned long long rows[MD_NMAX * MD_KWMAX];
   uint16_t cmat[MD_NMAX * MD_NMAX];
   int32_t soff[MD_NMAX + 1];
+  unsigned long long sbits[MD_PMAX / 64];  // bit k set: peak k starts spectrum >= 1
+  uint8_t spre[MD_PMAX / 64];              // spectra started before word w
   double totals[MD_NMAX];
   int tmp[MD_BLOCK / kWave + 1];
   long long red[2 * (MD_BLOCK / kWave)];
@@ -160,6 +164,12 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
     return;
   }
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
+  if (p1 - p0 > MD_PMAX) {
+    if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    return;
+  }
+  const int nsw = (int)((p1 - p0 + 63) / 64);
+  for (int w = tid; w < nsw; w += MD_BLOCK) L.sbits[w] = 0ull;
   // bin range from each spectrum's first and last peak (m/z-sorted spectra);
   // pass 1 verifies every bin falls inside and defers the cluster otherwise
   long long blo = 0x7fffffffffffffffll, bhi = -0x7fffffffffffffffll;
@@ -172,26 +182,45 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
     }
   }
   if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
+    const bool empty_spec = tid < n && v.spec_off[s0 + tid + 1] == v.spec_off[s0 + tid];
+    const unsigned long long any_empty = __ballot(empty_spec);
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
       const long long l2 = __shfl_xor(blo, o, kWave), h2 = __shfl_xor(bhi, o, kWave);
       blo = l2 < blo ? l2 : blo;
       bhi = h2 > bhi ? h2 : bhi;
     }
-    if (tid == 0) { L.red[0] = blo; L.red[1] = bhi; }
+    if (tid == 0) { L.red[0] = blo; L.red[1] = bhi; L.red[2] = any_empty != 0ull; }
   }
   __syncthreads();
   blo = L.red[0];
   bhi = L.red[1];
+  const bool has_empty = L.red[2] != 0;
   const bool any = p1 > p0;
   const int64_t nw = any ? (bhi - blo) / 64 + 1 : 0;
   if (nw > MD_WMAX || (any && bhi < blo)) {
     if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
     return;
   }
+  // spectrum of a peak in O(1): a start bit at every spectrum boundary and a
+  // per-word count of the boundaries before it
+  for (int j = 1 + tid; j < n; j += MD_BLOCK) {
+    const int r = L.soff[j];
+    if (r < p1 - p0) atomicOr(&L.sbits[r >> 6], 1ull << (r & 63));
+  }
   // 1: union bitmap (8 loads in flight per thread)
   for (int w = tid; w < nw; w += MD_BLOCK) L.bitmap[w] = 0ull;
   __syncthreads();
+  if (tid < kWave) {  // prefix of start bits (<= 256 words, one wave)
+    int carry = 0;
+    for (int w0 = 0; w0 < nsw; w0 += kWave) {
+      const int w = w0 + tid;
+      const int c1 = w < nsw ? __popcll(L.sbits[w]) : 0;
+      const int inc = wave_inclusive_sum(c1);
+      if (w < nsw) L.spre[w] = (uint8_t)(carry + inc - c1);
+      carry += __shfl(inc, kWave - 1, kWave);
+    }
+  }
   int outside = 0;
   for (int64_t k0 = p0 + tid; k0 < p1; k0 += 8 * MD_BLOCK) {
     double m[8];
@@ -214,7 +243,9 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
   }
   // 2: compact columns
   const int K = bitmap_prefix<MD_BLOCK>(L.bitmap, L.wprefix, (int)nw, L.tmp);
-  const int KW = (K + 63) / 64;
+  // row stride KW is odd: lanes reading rows j, j+1, ... at one word hit
+  // different LDS banks (an even stride of u64s would fold them together)
+  const int KW = ((K + 63) / 64) | 1;
   if (KW > MD_KWMAX) {
     if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
     return;
@@ -222,6 +253,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
   // 3: bit-packed rows
   for (int w = tid; w < n * KW; w += MD_BLOCK) L.rows[w] = 0ull;
   __syncthreads();
+  if (P.ablate & 16) { if (tid == 0) rep[c] = s0; return; }
   for (int64_t k0 = p0 + tid; k0 < p1; k0 += 8 * MD_BLOCK) {
     double m[8];
 #pragma unroll
@@ -234,15 +266,27 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
       const int64_t k = k0 + (int64_t)u * MD_BLOCK;
       if (k >= p1) continue;
       const int col = bitmap_rank(L.bitmap, L.wprefix, md_bin(m[u], P) - blo);
-      const int sp = spectrum_of(L.soff, n, (int32_t)(k - p0));
+      const int r = (int)(k - p0);
+      // empty spectra share a start bit: then fall back to the binary search
+      const int sp = has_empty ? spectrum_of(L.soff, n, r)
+                               : (int)L.spre[r >> 6] + __popcll(L.sbits[r >> 6] & ((2ull << (r & 63)) - 1ull));
       atomicOr(&L.rows[sp * KW + (col >> 6)], 1ull << (col & 63));
     }
   }
   __syncthreads();
-  // 4: shared-bin counts for every pair i <= j
-  for (int idx = tid; idx < n * n; idx += MD_BLOCK) {
-    const int i = idx / n, j = idx - i * n;
-    if (j < i) continue;
+  // 4: shared-bin counts for every pair i <= j: pair p of the row-major upper
+  // triangle, row i starting at i*n - i*(i-1)/2 (recovered by a float sqrt +
+  // integer fix-up: no idle half, no integer division per pair)
+  if (P.ablate & 64) { if (tid == 0) rep[c] = s0; return; }
+  const int NP = n * (n + 1) / 2;
+  auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
+  for (int p = tid; p < NP; p += MD_BLOCK) {
+    const float b2 = 2.0f * n + 1.0f;
+    int i = (int)((b2 - sqrtf(b2 * b2 - 8.0f * (float)p)) * 0.5f);
+    i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+    while (i > 0 && row_start(i) > p) --i;
+    while (i + 1 < n && row_start(i + 1) <= p) ++i;
+    const int j = i + (p - row_start(i));
     uint32_t cnt = 0;
     for (int w = 0; w < KW; ++w) cnt += (uint32_t)__popcll(L.rows[i * KW + w] & L.rows[j * KW + w]);
     L.cmat[i * n + j] = (uint16_t)cnt;
@@ -250,6 +294,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
   }
   __syncthreads();
   // 5: totals (most_similar_representative.py:98-100)
+  if (P.ablate & 32) { if (tid == 0) rep[c] = s0; return; }
   if (tid < n) {
     const int i = tid;
     const int64_t pi = L.soff[i + 1] - L.soff[i];
@@ -502,6 +547,31 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_totals_kernel(CsrView v, cons
     }
     __syncthreads();
   }
+}
+
+// ---------------------------------------------------------- pair distances
+// distance(spec1, spec2) of most_similar_representative.py:13-19 for arbitrary
+// (global) spectrum pairs: one wave per pair.  |B_a ∩ B_b| counts the distinct
+// bins of a (first occurrence in a) that occur in b.  O(p_a * (p_a + p_b)) per
+// pair: this is the per-call API, not the batched medoid path.
+__global__ __launch_bounds__(256) void xcorr_pairs_kernel(CsrView v, MedoidParams P, const int64_t* __restrict__ pairs,
+                                                          int64_t n_pairs, double* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * 4 + wave_id();
+  if (p >= n_pairs) return;
+  const int64_t sa = pairs[2 * p], sb = pairs[2 * p + 1];
+  const int64_t a0 = v.spec_off[sa], a1 = v.spec_off[sa + 1], b0 = v.spec_off[sb], b1 = v.spec_off[sb + 1];
+  uint32_t cnt = 0;
+  for (int64_t ka = a0 + lane_id(); ka < a1; ka += kWave) {
+    const int64_t bk = md_bin(v.mz[ka], P);
+    bool first = true;
+    for (int64_t kk = a0; kk < ka && first; ++kk) first = md_bin(v.mz[kk], P) != bk;
+    if (!first) continue;
+    bool found = false;
+    for (int64_t kb = b0; kb < b1 && !found; ++kb) found = md_bin(v.mz[kb], P) == bk;
+    cnt += found;
+  }
+  cnt = wave_sum(cnt);
+  if (lane_id() == 0) out[p] = md_dist(cnt, a1 - a0, b1 - b0);
 }
 
 }  // namespace spx

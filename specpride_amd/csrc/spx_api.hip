@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/specpride.h"
@@ -63,6 +64,12 @@ constexpr int kFallbackBlocks = 64;
 
 int64_t fallback_grid(int64_t C) { return std::max<int64_t>(1, std::min<int64_t>(C, kFallbackBlocks)); }
 
+// Profiling-only phase ablation (SPX_ABLATE bitmask, see the kernels); 0 in normal use.
+int32_t ablate_mask() {
+  const char* e = std::getenv("SPX_ABLATE");
+  return e ? (int32_t)std::atoi(e) : 0;
+}
+
 int32_t bin_words(const spx_bin_params* p) {
   const double nb = std::trunc((p->maximum - p->minimum) / p->binsize) + 1.0;  // binning.py:172
   return (int32_t)((nb + 63.0) / 64.0);
@@ -114,6 +121,7 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   P.inv_binsize = 1.0 / params->binsize;
   P.apply_quorum = params->apply_peak_quorum ? 1 : 0;
   P.n_words = bin_words(params);
+  P.ablate = ablate_mask();
   spx::PeaksOut O{out->mz, out->inten, out->count};
   const spx::CsrView V = view(csr);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
@@ -223,7 +231,7 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   if (w.used >= workspace_bytes) return fail(SPX_ENOSPACE, "spx_medoid: workspace too small");
   char* arena = w.base + w.used;
   const int64_t arena_bytes = (int64_t)(workspace_bytes - w.used);
-  spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance};
+  spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance, ablate_mask()};
   const spx::CsrView V = view(csr);
 
   if (hipMemsetAsync(n_def, 0, 512, s) != hipSuccess) return check_launch("spx_medoid memset");
@@ -244,6 +252,18 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
 }
 
 }  // extern "C"
+
+extern "C" int spx_xcorr_distance(const spx_csr* csr, const spx_medoid_params* params, const int64_t* pairs,
+                                  int64_t n_pairs, double* out, void* stream) {
+  if (!csr_ok(csr) || !params || (n_pairs > 0 && (!pairs || !out)))
+    return fail(SPX_EINVAL, "spx_xcorr_distance: null argument");
+  if (!(params->tolerance > 0)) return fail(SPX_EINVAL, "spx_xcorr_distance: tolerance must be > 0");
+  if (n_pairs <= 0) return SPX_SUCCESS;
+  spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance, 0};
+  hipLaunchKernelGGL(spx::xcorr_pairs_kernel, dim3((unsigned)((n_pairs + 3) / 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), view(csr), P, pairs, n_pairs, out);
+  return check_launch("xcorr_pairs_kernel");
+}
 
 // ---------------------------------------------------------------- compaction
 namespace spx {

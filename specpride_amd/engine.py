@@ -210,3 +210,16 @@ def medoid(batch: DeviceBatch, tolerance=0.1, with_totals=False, out: Optional[M
     _lib.check(L.spx_medoid(ctypes.byref(batch.csr), ctypes.byref(prm), _ptr(out.rep), _ptr(out.totals), _ptr(ws),
                             ws.numel(), _stream_handle(stream)), "spx_medoid")
     return out
+
+
+def xcorr_distance(batch: DeviceBatch, pairs, tolerance=0.1, stream=None):
+    """1 - xcorr prescore (most_similar_representative.py:13-19) for (global
+    spectrum index) pairs; returns a device f64 tensor."""
+    import torch
+
+    pairs_t = torch.as_tensor(np.asarray(pairs, np.int64).reshape(-1, 2), device=batch.device).contiguous()
+    out = torch.empty(max(len(pairs_t), 1), dtype=torch.float64, device=batch.device)
+    prm = _lib.SpxMedoidParams(float(tolerance))
+    _lib.check(_lib.lib().spx_xcorr_distance(ctypes.byref(batch.csr), ctypes.byref(prm), _ptr(pairs_t),
+                                             len(pairs_t), _ptr(out), _stream_handle(stream)), "spx_xcorr_distance")
+    return out[:len(pairs_t)]

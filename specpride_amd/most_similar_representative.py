@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Drop-in for the reference's ``src/most_similar_representative.py`` (medoid
+representative), running the all-pairs xcorr + summed-distance argmin on
+MI355X through ``spx_medoid``.
+
+Kept from the reference:
+
+* ``distance(spec1, spec2, method='xcorr')`` (:13-19): ``1 - xcorr`` with
+  OpenMS ``XQuestScores::xCorrelationPrescore(spec1, spec2, 0.1)`` semantics
+  (restated); any other ``method`` returns 0.  Spectra may be
+  pyteomics/binning-style dicts, ``(mz, intensity)`` tuples or bare m/z arrays.
+* ``main(argv)`` (:22-115): ``-i <input> -o <output>`` (``-h`` usage, exit 2 on a
+  bad option); cluster names in first-appearance order; each cluster is the
+  FIRST contiguous run at or after the previous cluster's run (the reference's
+  ``range_start`` scan, :64-75 -- later runs of a split cluster are ignored,
+  SURVEY.md A.4); singletons pass through; the representative is the lowest
+  index among the minima of ``(rowsum + colsum)/n`` of the upper-triangular
+  distance matrix (pairwise-summation order, :98-110).  Prints the cluster
+  name and size per cluster and the final count, as the reference does.
+  Output: the chosen spectra, written back verbatim as MGF (OpenMS
+  ``MascotGenericFile.store`` formatting is not reproduced: parity is on the
+  chosen spectrum and its title).
+
+All clusters of a file are scored in ONE device pass.
+"""
+from __future__ import annotations
+
+import getopt
+import sys
+
+import numpy as np
+
+from . import engine
+from .csr import SpectraCSR
+from .mgf import format_charge, read_mgf
+
+TOLERANCE = 0.1  # most_similar_representative.py:15
+
+
+def _mz_of(spec):
+    if isinstance(spec, dict):
+        return np.asarray(spec["m/z array"], np.float64)
+    if isinstance(spec, tuple) and len(spec) == 2:
+        return np.asarray(spec[0], np.float64)
+    return np.asarray(spec, np.float64)
+
+
+def distance(spec1, spec2, method="xcorr"):
+    """1.0 - XQuestScores().xCorrelationPrescore(spec1, spec2, 0.1), on the GPU."""
+    if method != "xcorr":
+        return 0
+    m1, m2 = _mz_of(spec1), _mz_of(spec2)
+    csr = SpectraCSR.from_clusters([[{"m/z array": m1, "intensity array": np.zeros_like(m1)},
+                                     {"m/z array": m2, "intensity array": np.zeros_like(m2)}]])
+    d = engine.xcorr_distance(engine.DeviceBatch.from_host(csr), [(0, 1)], TOLERANCE)
+    return float(d.cpu().numpy()[0])
+
+
+def _first_runs(names):
+    """The reference's cluster scan (most_similar_representative.py:49-75)."""
+    order = list(dict.fromkeys(names))
+    runs, range_start = [], 0
+    for cl in order:
+        members, reached = [], False
+        for i in range(range_start, len(names)):
+            if names[i] == cl:
+                members.append(i)
+                reached = True
+            elif reached:
+                range_start = i - 1
+                break
+        runs.append((cl, members))
+    return runs
+
+
+def _write_spectra(spectra, path):
+    with open(path, "w") as fh:
+        for sp in spectra:
+            p = sp["params"]
+            fh.write("BEGIN IONS\n")
+            if "title" in p:
+                fh.write(f"TITLE={p['title']}\n")
+            if "pepmass" in p:
+                fh.write(f"PEPMASS={float(p['pepmass'][0])!r}\n")
+            if "charge" in p and len(p["charge"]):
+                fh.write(f"CHARGE={format_charge(p['charge'])}\n")
+            if "rtinseconds" in p:
+                fh.write(f"RTINSECONDS={float(p['rtinseconds'])!r}\n")
+            fh.write("".join(f"{float(a)!r} {float(b)!r}\n" for a, b in zip(sp["m/z array"], sp["intensity array"])))
+            fh.write("END IONS\n\n")
+
+
+def representatives(spectra, names):
+    """Indices (into ``spectra``) of the representative of every cluster run."""
+    runs = [(cl, m) for cl, m in _first_runs(names) if m]
+    csr = SpectraCSR.from_clusters([[spectra[i] for i in members] for _cl, members in runs])
+    rep, _ = engine.medoid(engine.DeviceBatch.from_host(csr), TOLERANCE).to_host()
+    if np.any(rep < 0):
+        raise RuntimeError("medoid engine could not resolve a cluster (see DESIGN.md limits)")
+    out = []
+    for c, (cl, members) in enumerate(runs):
+        out.append((cl, members, members[int(rep[c] - csr.cluster_off[c])]))
+    return out
+
+
+def main(argv):
+    inputfile, outputfile = "", ""
+    try:
+        opts, _args = getopt.getopt(argv, "hi:o:")
+    except getopt.GetoptError:
+        print("most_similar_representative.py -i <inputfile> -o <outputfile>")
+        sys.exit(2)
+    for opt, arg in opts:
+        if opt == "-h":
+            print("most_similar_representative.py -i <inputfile> -o <outputfile>")
+            sys.exit()
+        elif opt in ("-i",):
+            inputfile = arg
+        elif opt in ("-o",):
+            outputfile = arg
+    spectra = read_mgf(inputfile)
+    names = [s["params"]["title"].split(";")[0] for s in spectra]
+    chosen = []
+    for cl, members, best in representatives(spectra, names):
+        print(cl)
+        print(len(members))
+        chosen.append(spectra[best])
+    print(len(chosen))
+    _write_spectra(chosen, outputfile)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,216 @@
+"""Multi-GPU driver: clusters sharded over ranks, one gather to rank 0.
+
+Clusters are independent, so the hot path has no data-path collective: each
+rank owns a cost-balanced subset of clusters (LPT greedy bucketing -- the
+longest job goes to the least-loaded rank), packs its own CSR, runs the
+kernels on its own GPU, and the only exchange is a gatherv of the results to
+rank 0, which reorders them by global cluster ordinal so the output order is
+the reference's.  On MI355X the process group is ``nccl`` (= RCCL): the gather
+is point-to-point ``isend/irecv`` of device tensors over xGMI, one link per
+peer, no ring.  The same code runs under ``gloo`` on CPU tensors, which is how
+the CPU test suite covers it (tests/test_distributed.py).
+
+Per-rank compute is injectable (``compute=``) so the sharding, gather and
+reassembly logic can be tested without a GPU; the default is the HIP engine.
+
+Cost model: consensus paths are HBM-bound, cost = Σpeaks;
+medoid is Gram-bound, cost = n² · K_c with K_c approximated by the cluster's
+peak count / n (mean distinct bins per spectrum) times n, i.e. n · Σpeaks.
+"""
+from __future__ import annotations
+
+import heapq
+from typing import Callable, Optional
+
+import numpy as np
+
+from .csr import SpectraCSR, concat_ranges
+
+CONSENSUS_KEYS = ("count", "status", "prec", "charge", "rt")
+
+
+# ------------------------------------------------------------------ planning
+def cluster_costs(csr: SpectraCSR, method: str) -> np.ndarray:
+    peaks = csr.cluster_peaks().astype(np.float64)
+    n = csr.cluster_sizes().astype(np.float64)
+    if method in ("bin_mean", "gap_average"):
+        return peaks + 1.0
+    if method == "medoid":
+        return n * peaks + 1.0
+    if method == "both":
+        return peaks + n * peaks / 64.0 + 1.0
+    raise ValueError(f"unknown method {method!r}")
+
+
+def plan(csr: SpectraCSR, world: int, method: str = "bin_mean") -> list:
+    """LPT greedy assignment: rank -> ascending array of global cluster ids."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    cost = cluster_costs(csr, method)
+    order = np.argsort(-cost, kind="stable")
+    heap = [(0.0, r) for r in range(world)]
+    owner = np.empty(csr.n_clusters, np.int64)
+    for c in order:
+        load, r = heapq.heappop(heap)
+        owner[c] = r
+        heapq.heappush(heap, (load + float(cost[c]), r))
+    return [np.flatnonzero(owner == r) for r in range(world)]
+
+
+# ---------------------------------------------------------------- collectives
+def gatherv(tensors: list, root: int = 0, group=None) -> Optional[list]:
+    """Gather a list of 1-D tensors (same dtypes on every rank, any lengths) to
+    ``root``.  Returns ``out[rank][i]`` on root, None elsewhere.  Lengths travel
+    first (one small all_gather), then payloads point-to-point."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    dev = tensors[0].device if tensors else torch.device("cpu")
+    lens = torch.tensor([t.numel() for t in tensors], dtype=torch.int64, device=dev)
+    all_lens = [torch.empty_like(lens) for _ in range(world)]
+    dist.all_gather(all_lens, lens, group=group)
+    all_lens = [x.cpu().tolist() for x in all_lens]
+    if rank != root:
+        reqs = [dist.isend(t.contiguous(), dst=root, group=group) for t in tensors if t.numel()]
+        for q in reqs:
+            q.wait()
+        return None
+    out, reqs = [], []
+    for r in range(world):
+        if r == root:
+            out.append([t for t in tensors])
+            continue
+        bufs = [torch.empty(n, dtype=t.dtype, device=dev) for n, t in zip(all_lens[r], tensors)]
+        reqs += [dist.irecv(b, src=r, group=group) for b in bufs if b.numel()]
+        out.append(bufs)
+    for q in reqs:
+        q.wait()
+    return out
+
+
+# ------------------------------------------------------------ default compute
+def _engine_consensus(method: str, params: dict, device):
+    def run(sub: SpectraCSR) -> dict:
+        from . import engine
+
+        batch = engine.DeviceBatch.from_host(sub, device)
+        res = getattr(engine, method)(batch, **params)
+        out_off, mz, inten = res.compact()
+        d = dict(count=res.count[:sub.n_clusters], status=res.status[:sub.n_clusters],
+                 prec=res.prec[:sub.n_clusters], charge=res.charge[:sub.n_clusters], mz=mz, inten=inten)
+        if res.rt is not None:
+            d["rt"] = res.rt[:sub.n_clusters]
+        return d
+    return run
+
+
+def _engine_medoid(params: dict, device):
+    def run(sub: SpectraCSR) -> dict:
+        import torch
+
+        from . import engine
+
+        batch = engine.DeviceBatch.from_host(sub, device)
+        res = engine.medoid(batch, **params)
+        rep = res.rep[:sub.n_clusters]
+        first = batch.t["cluster_off"][:-1]
+        member = torch.where(rep >= 0, rep - first, rep)  # index within the cluster (<0 passes through)
+        d = dict(member=member)
+        if res.totals is not None:
+            d["totals"] = res.totals[:sub.n_spectra]
+        return d
+    return run
+
+
+# ----------------------------------------------------------------- drivers
+def _my_shard(csr: SpectraCSR, method: str, group):
+    import torch.distributed as dist
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    parts = plan(csr, world, method)
+    return parts, rank, csr.select(parts[rank])
+
+
+def consensus_sharded(csr: SpectraCSR, method: str = "bin_mean", params: Optional[dict] = None,
+                      device=None, group=None, compute: Optional[Callable] = None) -> Optional[dict]:
+    """Run ``engine.bin_mean`` / ``engine.gap_average`` over the ranks of ``group``;
+    rank 0 returns the host dict of :meth:`engine.PeaksResult.to_host` for the
+    WHOLE batch in global cluster order; other ranks return None.  Every rank
+    passes the same ``csr`` (e.g. each parsed the same file, or rank-local
+    ingest wrote the full index)."""
+    import torch
+
+    params = params or {}
+    parts, rank, sub = _my_shard(csr, method, group)
+    run = compute or _engine_consensus(method, params, device)
+    res = run(sub)
+    with_rt = "rt" in res
+    keys = [k for k in CONSENSUS_KEYS if k in res]
+    dev = res["count"].device
+    payload = [res[k].contiguous() for k in keys] + [res["mz"].contiguous(), res["inten"].contiguous()]
+    got = gatherv(payload, group=group)
+    if got is None:
+        return None
+    C = csr.n_clusters
+    full = {}
+    for i, k in enumerate(keys):
+        t0 = got[0][i]
+        buf = torch.zeros(C, dtype=t0.dtype, device=dev)
+        for r, ids in enumerate(parts):
+            if len(ids):
+                buf[torch.from_numpy(ids).to(dev)] = got[r][i]
+        full[k] = buf
+    count = full["count"].to(torch.int64)
+    out_off = torch.zeros(C + 1, dtype=torch.int64, device=dev)
+    if C:
+        torch.cumsum(count, 0, out=out_off[1:])
+    total = int(out_off[-1].item()) if C else 0
+    mz = torch.empty(total, dtype=torch.float64, device=dev)
+    inten = torch.empty(total, dtype=torch.float64, device=dev)
+    for r, ids in enumerate(parts):
+        if not len(ids):
+            continue
+        ids_np = np.asarray(ids, np.int64)
+        cnt = count[torch.from_numpy(ids_np).to(dev)].cpu().numpy()
+        dst = concat_ranges(out_off.cpu().numpy()[ids_np], cnt)
+        if len(dst):
+            dst_t = torch.from_numpy(dst).to(dev)
+            mz[dst_t] = got[r][len(keys)]
+            inten[dst_t] = got[r][len(keys) + 1]
+    out = dict(out_off=out_off.cpu().numpy(), out_mz=mz.cpu().numpy(), out_int=inten.cpu().numpy(),
+               status=full["status"].cpu().numpy(), prec=full["prec"].cpu().numpy(),
+               charge=full["charge"].cpu().numpy())
+    if with_rt:
+        out["rt"] = full["rt"].cpu().numpy()
+    return out
+
+
+def medoid_sharded(csr: SpectraCSR, params: Optional[dict] = None, device=None, group=None,
+                   compute: Optional[Callable] = None):
+    """Sharded ``engine.medoid``: rank 0 returns ``(rep [C] global spectrum index,
+    totals [S] or None)`` in global order; other ranks return None."""
+    import torch
+
+    params = params or {}
+    parts, rank, sub = _my_shard(csr, "medoid", group)
+    run = compute or _engine_medoid(params, device)
+    res = run(sub)
+    with_totals = "totals" in res
+    payload = [res["member"].contiguous()] + ([res["totals"].contiguous()] if with_totals else [])
+    got = gatherv(payload, group=group)
+    if got is None:
+        return None
+    C, S = csr.n_clusters, csr.n_spectra
+    rep = np.full(C, -1, np.int64)
+    totals = np.full(S, np.nan) if with_totals else None
+    for r, ids in enumerate(parts):
+        if not len(ids):
+            continue
+        member = got[r][0].cpu().numpy()
+        first = csr.cluster_off[ids]
+        rep[ids] = np.where(member >= 0, first + member, member)
+        if with_totals:
+            sizes = csr.cluster_off[ids + 1] - first
+            totals[concat_ranges(first, sizes)] = got[r][1].cpu().numpy()
+    return rep, totals

@@ -1,0 +1,61 @@
+"""Phase ablation timing of the two headline kernels (profiling aid, not a test).
+
+Times spx_bin_mean and spx_medoid on the bench batch with SPX_ABLATE masks that
+skip phases, so the cost of each phase is the difference.  Prints JSON."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from specpride_amd import engine  # noqa: E402
+from specpride_amd.synthetic import make_clusters_torch  # noqa: E402
+
+
+def timed(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    n = 100_000
+    b = engine.DeviceBatch.from_device(make_clusters_torch(n, seed=0, device="cuda"))
+    bm = engine.bin_mean(b)
+    md = engine.medoid(b)
+    res = {}
+    for mask in (0, 1, 3):
+        os.environ["SPX_ABLATE"] = str(mask)
+        res[f"bin_mean_ablate{mask}_ms"] = timed(lambda: engine.bin_mean(b, out=bm))
+    for mask in (0, 16, 64, 32):
+        os.environ["SPX_ABLATE"] = str(mask)
+        res[f"medoid_ablate{mask}_ms"] = timed(lambda: engine.medoid(b, out=md))
+    os.environ["SPX_ABLATE"] = "0"
+    print(json.dumps(res))
+
+
+
+
+def plain(n=100_000, reps=3):
+    """Just the two headline calls, for counter collection."""
+    b = engine.DeviceBatch.from_device(make_clusters_torch(n, seed=0, device="cuda"))
+    bm = engine.bin_mean(b)
+    md = engine.medoid(b)
+    for _ in range(reps):
+        engine.bin_mean(b, out=bm)
+        engine.medoid(b, out=md)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "plain":
+        plain()
+    else:
+        main()
