@@ -1,5 +1,5 @@
 #!/bin/bash
-# Iteration loop: parity tests -> bench -> phase ablation -> per-kernel stats.
+# Medoid large-path iteration: parity tests -> bench -> config-4 check + kernel stats.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
@@ -10,11 +10,9 @@ echo "pytest rc=$?" >> gpurun_out/gpu_tests.log
 tail -3 gpurun_out/gpu_tests.log
 grep -q "pytest rc=0" gpurun_out/gpu_tests.log || { grep -E "^(FAILED|E  )" gpurun_out/gpu_tests.log | head -30; exit 1; }
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
-tail -1 gpurun_out/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernels'], d['roofline']['frac'])"
-timeout -k 10 300 python tools/profile_phases.py > gpurun_out/phases.json 2>gpurun_out/phases.err || { tail -5 gpurun_out/phases.err; exit 1; }
-cat gpurun_out/phases.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_plain -o run -- python3 tools/profile_phases.py plain > gpurun_out/prof_plain.log 2>&1 || { tail -5 gpurun_out/prof_plain.log; exit 1; }
+tail -1 gpurun_out/bench.log
 timeout -k 10 400 python tools/bench_medoid_large.py --check > gpurun_out/medoid_large.log 2>&1 || { tail -5 gpurun_out/medoid_large.log; exit 1; }
 tail -1 gpurun_out/medoid_large.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_md -o run -- python3 tools/bench_medoid_large.py > gpurun_out/prof_md.log 2>&1 || { tail -5 gpurun_out/prof_md.log; exit 1; }
-echo done
+f=$(find gpurun_out/prof_md -name "*kernel_stats.csv" | head -1)
+cut -d, -f1-4 "$f" | head -14

@@ -59,7 +59,7 @@ class SpxMedoidParams(ctypes.Structure):
     _fields_ = [("tolerance", _dbl)]
 
 
-# every symbol include/specpride.h declares (checked by tests/test_abi.py)
+# every symbol include/specpride.h declares (checked by tests/test_host.py)
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_gap_average_workspace_size", "spx_gap_average",
             "spx_medoid_workspace_size", "spx_medoid", "spx_xcorr_distance", "spx_compact_peaks", "spx_abi_version",
             "spx_last_error"]

@@ -348,6 +348,307 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_lds_kernel(CsrView v, BinMe
   }
 }
 
+// ------------------------------------------------------------------------
+// bin_mean_list_kernel: the per-cluster fast path (one workgroup per cluster).
+//
+// No spectrum-serial loop: the reference's float32 accumulation order (spectrum
+// order within each bin) is rebuilt as an explicit per-bin list instead.
+//   P1  every peak once (flat, coalesced; <= 48 peaks per thread kept in
+//       registers): exact bin, LDS occupancy bitmap, and "last peak of its bin
+//       in its spectrum" (numpy fancy-index "+=" keeps the last,
+//       binning.py:197-199) = the next peak of the same spectrum has another
+//       bin -- a neighbour compare, valid because keys are checked to be
+//       non-decreasing inside every spectrum (else the cluster is deferred).
+//   P2  popcount prefix -> compact slots in ascending bin order.
+//   P3a each last peak sets bit s (its spectrum) of smask[slot]:
+//       count(slot) = popcount(smask[slot]) = the reference's n[b].
+//   P3b one block scan: kept slots (count >= int(0.25 n)+1) in bin order and
+//       their list offsets.
+//   P3c each last peak of a kept slot writes its position to
+//       list[off[slot] + popcount(smask[slot] & below(s))]: the slot's list is in
+//       spectrum order by construction (no atomics, no sort).
+//   P3d one thread per kept slot folds I = f32(f64(I) + it), M = f32(f64(M) + mz)
+//       along its list (the reference's order) and writes the means.
+// Deferred to bin_mean_global_kernel (the generic spectrum-serial body): more
+// than 64 spectra or BL_PCAP peaks, empty spectra, NaN m/z or non-finite means,
+// a key inversion inside a spectrum (unsorted), > BL_DCAP slots or > BL_LCAP kept
+// contributions.
+constexpr int BL_UMAX = 48;                  // peaks per thread
+constexpr int BL_PCAP = BL_UMAX * BM_BLOCK;  // 12,288 peaks per cluster
+constexpr int BL_LCAP = 10240;               // kept (spectrum, bin) contributions
+constexpr int BL_DCAP = 1536;                // occupied bins (slots)
+constexpr int BL_NMAX = 64;                  // spectra (one u64 mask per slot)
+constexpr int BL_SW = BL_PCAP / 64;          // spectrum-start bitmap words
+constexpr uint16_t BL_DROP = 0xFFFFu;
+constexpr int BL_PB = 16;                    // P1 loads in flight per thread
+
+struct BinListSmem {
+  union {
+    struct {
+      unsigned long long bitmap[BM_WMAX];
+      uint16_t wprefix[BM_WMAX];
+    } b;                      // P1..P3a
+    uint16_t list[BL_LCAP];   // P3c..P3d (peak offsets within the cluster)
+  } u;
+  unsigned long long smask[BL_DCAP];
+  uint16_t loff[BL_DCAP];     // list offset of a kept slot (BL_DROP: below quorum)
+  uint16_t kslot[BL_DCAP];    // slot of the j-th kept slot (= output order)
+  unsigned long long sbits[BL_SW];  // bit r: peak r starts spectrum >= 1
+  uint8_t spre[BL_SW];              // spectra started before word w
+  int32_t xch[BL_UMAX * (BM_BLOCK / kWave)];  // lane-0 key of (iteration, wave)
+  int votes[2 * (BM_BLOCK / kWave)];
+  int tmp[BM_BLOCK / kWave + 1];
+  long long tmp64[BM_BLOCK / kWave + 1];
+};
+
+// register entry: P1 holds (bin | flags), P3a on (slot | spectrum << 16 | flags)
+constexpr uint32_t BL_IN = 1u << 31;    // peak exists and min <= mz < max
+constexpr uint32_t BL_LAST = 1u << 30;  // last peak of its bin in its spectrum
+constexpr uint32_t BL_NXT = 1u << 29;   // lane 63 only: the next peak is in the same spectrum
+constexpr uint32_t BL_HI = 1u << 28;    // out of range at/above maximum (key INT_MAX; else -1)
+constexpr uint32_t BL_VAL = (1u << 28) - 1u;
+
+__device__ __forceinline__ void bl_finish_empty(const PeaksOut& out, double* prec_out, int32_t* charge_out, int64_t c) {
+  out.count[c] = 0;
+  prec_out[c] = __longlong_as_double(0x7ff8000000000000ll);
+  charge_out[c] = 0;
+}
+
+__global__ __launch_bounds__(BM_BLOCK) void bin_mean_list_kernel(CsrView v, BinMeanParams P, PeaksOut out,
+                                                                 double* prec_out, int32_t* charge_out,
+                                                                 int32_t* status, int32_t* deferred,
+                                                                 int32_t* n_deferred) {
+  __shared__ BinListSmem L;
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  constexpr int NW = BM_BLOCK / kWave;
+  const int64_t c = blockIdx.x;
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+  const int n = (int)(s1 - s0);
+  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
+  const int np = (int)(p1 - p0);
+  auto defer = [&]() {
+    if (tid == 0) {
+      status[c] = kDeferred;
+      deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    }
+  };
+  if (n == 0) {
+    if (tid == 0) { bl_finish_empty(out, prec_out, charge_out, c); status[c] = kEmpty; }
+    return;
+  }
+  if (n > BL_NMAX || p1 - p0 > BL_PCAP || P.n_words > BM_WMAX) { defer(); return; }
+
+  // P0: charge check (binning.py:205-206), zero the bitmaps, spectrum starts
+  const int32_t z0 = v.charge[s0];
+  int mixed = 0, empty_spec = 0;
+  if (tid < n) {
+    mixed = v.charge[s0 + tid] != z0;
+    empty_spec = v.spec_off[s0 + tid + 1] == v.spec_off[s0 + tid];
+  }
+  const int nsw = (np + 63) / 64;
+  for (int w = tid; w < P.n_words; w += BM_BLOCK) L.u.b.bitmap[w] = 0ull;
+  for (int w = tid; w < nsw; w += BM_BLOCK) L.sbits[w] = 0ull;
+  if (block_any<BM_BLOCK, true>(mixed, L.votes, 0)) {
+    if (tid == 0) { bl_finish_empty(out, prec_out, charge_out, c); status[c] = kMixedCharge; }
+    return;
+  }
+  if (tid >= 1 && tid < n) {
+    const int r = (int)(v.spec_off[s0 + tid] - p0);
+    if (r < np) atomicOr(&L.sbits[r >> 6], 1ull << (r & 63));
+  }
+  if (block_any<BM_BLOCK, true>(empty_spec, L.votes, 1)) { defer(); return; }
+
+  // P1: one exact bin per peak, bitmap, neighbour keys.  Loads are issued in
+  // batches of BL_PB (all in flight together), then the batch is processed.
+  uint32_t ent[BL_UMAX];
+  int bad = 0;
+#pragma unroll
+  for (int u = 0; u < BL_UMAX; ++u) ent[u] = 0u;
+#pragma unroll
+  for (int u0 = 0; u0 < BL_UMAX; u0 += BL_PB) {
+    if (u0 * BM_BLOCK < np) {  // uniform
+      double mb[BL_PB];
+#pragma unroll
+      for (int q = 0; q < BL_PB; ++q) {
+        const int r = (u0 + q) * BM_BLOCK + tid;
+        mb[q] = v.mz[p0 + (r < np ? r : 0)];
+      }
+#pragma unroll
+      for (int q = 0; q < BL_PB; ++q) {
+        const int u = u0 + q;
+        if (u * BM_BLOCK < np) {  // uniform
+          const int r = u * BM_BLOCK + tid;
+          const bool valid = r < np;
+          const double m = mb[q];
+          bad |= valid && (m != m);
+          int32_t key = m < P.minimum ? -1 : 0x7fffffff;
+          const bool inr = valid && in_range(m, P);
+          if (inr) {
+            const int64_t b = bin_of(m, P);
+            key = (int32_t)b;
+            atomicOr(&L.u.b.bitmap[b >> 6], 1ull << (b & 63));
+          }
+          const int32_t kn = __shfl_down(key, 1, kWave);
+          if (lane == 0) L.xch[u * NW + wid] = key;
+          const int rn = r + 1;
+          const bool same = valid && rn < np && !((L.sbits[rn >> 6] >> (rn & 63)) & 1ull);
+          uint32_t e = inr ? (BL_IN | (uint32_t)key) : (key == 0x7fffffff ? BL_HI : 0u);
+          if (lane < kWave - 1) {
+            bad |= same && key > kn;
+            if (!(same && kn == key)) e |= BL_LAST;
+          } else if (same) {
+            e |= BL_NXT;  // decided after the barrier from the next wave's lane-0 key
+          } else {
+            e |= BL_LAST;
+          }
+          ent[u] = e;
+        }
+      }
+    }
+  }
+  // spectra started before each start-bit word (wave 0; n <= 64 fits a u8)
+  if (wid == 0) {
+    int carry = 0;
+    for (int w0 = 0; w0 < nsw; w0 += kWave) {
+      const int w = w0 + lane;
+      const int pc = w < nsw ? __popcll(L.sbits[w]) : 0;
+      int inc = pc;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int t = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += t;
+      }
+      if (w < nsw) L.spre[w] = (uint8_t)(carry + inc - pc);
+      carry += __shfl(inc, kWave - 1, kWave);
+    }
+  }
+  if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) { defer(); return; }
+
+  // P2: compact slots in bin order
+  const int D = bitmap_prefix<BM_BLOCK>(L.u.b.bitmap, L.u.b.wprefix, P.n_words, L.tmp);
+  if (D > BL_DCAP) { defer(); return; }
+  for (int d = tid; d < D; d += BM_BLOCK) L.smask[d] = 0ull;
+  lds_barrier();
+
+  // P3a: spectrum masks per slot; lane 63 resolves its cross-wave neighbour
+#pragma unroll
+  for (int u = 0; u < BL_UMAX; ++u) {
+    if (u * BM_BLOCK < np) {
+      uint32_t e = ent[u];
+      if (e & BL_NXT) {
+        const int32_t kx = wid < NW - 1 ? L.xch[u * NW + wid + 1] : L.xch[(u + 1) * NW];
+        const int32_t key = (e & BL_IN) ? (int32_t)(e & BL_VAL) : ((e & BL_HI) ? 0x7fffffff : -1);
+        bad |= key > kx;
+        if (kx != key) e |= BL_LAST;
+      }
+      if (e & BL_IN) {
+        const int r = u * BM_BLOCK + tid;
+        const int slot = bitmap_rank(L.u.b.bitmap, L.u.b.wprefix, (int64_t)(e & BL_VAL));
+        const int sp = (int)L.spre[r >> 6] + __popcll(L.sbits[r >> 6] & ((2ull << (r & 63)) - 1ull));
+        if (e & BL_LAST) atomicOr(&L.smask[slot], 1ull << sp);
+        e = (e & (BL_IN | BL_LAST)) | (uint32_t)slot | ((uint32_t)sp << 16);
+      }
+      ent[u] = e;
+    }
+  }
+  if (block_any<BM_BLOCK, true>(bad, L.votes, 1)) { defer(); return; }
+  if (P.ablate & 1) {
+    if (tid == 0) { out.count[c] = 0; status[c] = kOk; }
+    return;
+  }
+
+  // P3b: kept slots in bin order and their list offsets (one 64-bit scan)
+  const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
+  const int per = (D + BM_BLOCK - 1) / BM_BLOCK;
+  const int d0 = tid * per;
+  long long mine = 0;
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d < D) {
+      const uint32_t cn = (uint32_t)__popcll(L.smask[d]);
+      if (cn >= quorum) mine += (1ll << 32) | (long long)cn;
+    }
+  }
+  long long tot;
+  long long ex = block_exclusive_scan<BM_BLOCK>(mine, L.tmp64, tot);
+  const int K = (int)(tot >> 32), LN = (int)(tot & 0xffffffffll);
+  if (LN > BL_LCAP) { defer(); return; }
+  int kj = (int)(ex >> 32), lo = (int)(ex & 0xffffffffll);
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d < D) {
+      const uint32_t cn = (uint32_t)__popcll(L.smask[d]);
+      if (cn >= quorum) {
+        L.loff[d] = (uint16_t)lo;
+        L.kslot[kj] = (uint16_t)d;
+        lo += (int)cn;
+        ++kj;
+      } else {
+        L.loff[d] = BL_DROP;
+      }
+    }
+  }
+  lds_barrier();  // also: the bitmap (aliased by the list) is dead from here
+
+  // P3c: spectrum-ordered lists of the kept slots
+#pragma unroll
+  for (int u = 0; u < BL_UMAX; ++u) {
+    if (u * BM_BLOCK < np) {
+      const uint32_t e = ent[u];
+      if ((e & BL_IN) && (e & BL_LAST)) {
+        const int slot = (int)(e & 0xffffu), sp = (int)((e >> 16) & 0xffu);
+        const uint16_t base = L.loff[slot];
+        if (base != BL_DROP)
+          L.u.list[base + __popcll(L.smask[slot] & ((1ull << sp) - 1ull))] = (uint16_t)(u * BM_BLOCK + tid);
+      }
+    }
+  }
+  lds_barrier();
+
+  // P3d: the reference's float32 folds, one thread per kept slot, means out
+  int nonfinite = 0;
+  if (!(P.ablate & 2)) {
+    for (int j = tid; j < K; j += BM_BLOCK) {
+      const int d = L.kslot[j];
+      const int base = L.loff[d], cn = __popcll(L.smask[d]);
+      float am = 0.0f, ai = 0.0f;
+      // gathers in batches of 8 (16 loads in flight), folded in list order
+      for (int e0 = 0; e0 < cn; e0 += 8) {
+        double mm[8], ii[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int e = e0 + q < cn ? e0 + q : cn - 1;
+          const int64_t k = p0 + L.u.list[base + e];
+          mm[q] = v.mz[k];
+          ii[q] = v.inten[k];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (e0 + q < cn) {
+            ai = (float)((double)ai + ii[q]);
+            am = (float)((double)am + mm[q]);
+          }
+        }
+      }
+      const double cnd = (double)cn;
+      const double mi = (double)ai / cnd;
+      nonfinite |= isnan(mi);
+      out.inten[p0 + j] = mi;
+      out.mz[p0 + j] = am == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)am / cnd;
+    }
+  }
+  // a NaN mean would be dropped by the reference (binning.py:209-222): the
+  // generic path redoes such clusters with that filter
+  if (block_any<BM_BLOCK, true>(nonfinite, L.votes, 0)) { defer(); return; }
+  if (tid == 0) {
+    out.count[c] = (P.ablate & 2) ? 0 : K;
+    charge_out[c] = z0;
+    const double* pr = v.prec_mz + s0;
+    prec_out[c] = pw_sum_small([&](int64_t j) { return pr[j]; }, n) / (double)n;  // np.mean, n <= 64
+    status[c] = kOk;
+  }
+}
+
 // Scratch slice of the deferred path, every array 256-B aligned.
 struct BinSliceLayout {
   int64_t bitmap, wprefix, cnt, acc_i, acc_m, owner, total;

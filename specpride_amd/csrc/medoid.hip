@@ -35,8 +35,6 @@ constexpr int MD_NMAX = 64;
 constexpr int MD_WMAX = 1024;    // union-bitmap words: bin range <= 65,536 (6,553 Da at 0.1)
 constexpr int MD_KWMAX = 31;     // row words (odd stride): <= 1,984 occupied bins per small cluster
 constexpr int MD_PMAX = 16384;   // peaks per small cluster (spectrum-start bitmap)
-constexpr int MD_TILE = 64;      // Gram tile (large path)
-constexpr int MD_KCHUNK = 32;    // u64 words per LDS stage (large path)
 
 struct MedoidSmem {
   unsigned long long bitmap[MD_WMAX];
@@ -144,16 +142,35 @@ __device__ __forceinline__ int spectrum_of(const int32_t* soff, int n, int32_t k
 }
 
 // --------------------------------------------------------- small clusters
+// Per deferred cluster state of the large path (zero-initialised at deferral).
+struct MedoidMeta {
+  unsigned long long lo_key, hi_key;  // bin range, order-preserving keys (atomicMax; 0 = none)
+  int64_t c, s0, blo;
+  int64_t l1_off, l2_off, rows_off, cmat_off, leaf_off, lsum_off, tot_off;  // arena byte offsets
+  int32_t n, nw1, B1, KW, L, tiles, units, ok;
+};
+
+__device__ __forceinline__ void md_defer(int64_t c, int64_t s0, int n, int32_t* deferred, int32_t* n_deferred,
+                                         MedoidMeta* meta) {
+  const int32_t slot = atomicAdd(n_deferred, 1);
+  deferred[slot] = (int32_t)c;
+  MedoidMeta M = {};
+  M.c = c;
+  M.s0 = s0;
+  M.n = n;
+  meta[slot] = M;
+}
+
 __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, MedoidParams P, int64_t* rep,
                                                                 double* totals_out, int32_t* deferred,
-                                                                int32_t* n_deferred) {
+                                                                int32_t* n_deferred, MedoidMeta* meta) {
   __shared__ MedoidSmem L;
   const int tid = threadIdx.x;
   const int64_t c = blockIdx.x;
   const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
   const int n = (int)(s1 - s0);
   if (s1 - s0 > MD_NMAX) {
-    if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
     return;
   }
   if (n <= 1) {
@@ -165,7 +182,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
   }
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
   if (p1 - p0 > MD_PMAX) {
-    if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
     return;
   }
   const int nsw = (int)((p1 - p0 + 63) / 64);
@@ -199,7 +216,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
   const bool any = p1 > p0;
   const int64_t nw = any ? (bhi - blo) / 64 + 1 : 0;
   if (nw > MD_WMAX || (any && bhi < blo)) {
-    if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
     return;
   }
   // spectrum of a peak in O(1): a start bit at every spectrum boundary and a
@@ -238,7 +255,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
     }
   }
   if (__syncthreads_or(outside)) {  // an unsorted spectrum: general path
-    if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
     return;
   }
   // 2: compact columns
@@ -247,7 +264,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
   // different LDS banks (an even stride of u64s would fold them together)
   const int KW = ((K + 63) / 64) | 1;
   if (KW > MD_KWMAX) {
-    if (tid == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
     return;
   }
   // 3: bit-packed rows
@@ -316,197 +333,600 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
 }
 
 // ------------------------------------------------------------ large path
-struct MedoidMeta {
-  int64_t c, s0, rows_off, cmat_off;  // byte offsets into scratch
-  int32_t n, KW, tiles, ok;
+// Clusters the LDS kernel defers (n > 64, or too many bins/peaks) go through
+// grid-parallel passes over ONE bump-allocated arena (one workgroup per
+// cluster only for the small planning steps):
+//   range   (grid)   bin range; allocates the level-1 bitmap
+//   l1      (grid)   level-1 occupancy (one bit per 64-bin block), LDS-staged
+//   plan1   (WG/cl)  level-1 prefix; allocates the level-2 words
+//   l2      (grid)   level-2 occupancy (one bit per occupied bin)
+//   plan2   (WG/cl)  level-2 prefix -> K compact columns; allocates rows, counts,
+//                    numpy's leaf segmentation and leaf sums
+//   scan    (1 WG)   Gram-tile and leaf-unit bases over the deferred clusters
+//   fill    (grid)   bit rows, 1 bit per occupied column (the OpenMS binary
+//                    ion table, compacted)
+//   gram    (MFMA)   c_ij = |B_i ∩ B_j|, v_mfma_i32_32x32x32_i8 on 0/1 bytes
+//   leaves  (grid)   numpy pairwise-tree leaf sums of row i and column i
+//   combine (WG/cl)  the tree over the leaf sums -> totals, lowest-index argmin
+constexpr int MD_L1WORDS = 1024;  // level-1 bits: 65,536 blocks = 4.2M bins
+constexpr int MD_L2LDS = 4096;    // level-2 words staged in LDS (else global atomics)
+constexpr int MD_GT = 128;        // MFMA Gram tile (rows padded to a multiple)
+constexpr int MD_GROW = 80;       // LDS bytes per expanded row (64 + 16: conflict-free b128)
+constexpr int MD_GRIDX = 64;      // blocks per cluster in the grid-parallel passes
+
+__host__ __device__ __forceinline__ int64_t md_align(int64_t b) { return (b + 255) & ~int64_t(255); }
+__host__ __device__ __forceinline__ int64_t md_l1_bytes() { return md_align((int64_t)MD_L1WORDS * 12); }
+__host__ __device__ __forceinline__ int64_t md_max_leaves(int64_t n) { return n / 32 + 2; }
+
+__device__ __forceinline__ unsigned long long md_key(int64_t b) {
+  return (unsigned long long)b ^ 0x8000000000000000ull;
+}
+__device__ __forceinline__ int64_t md_unkey(unsigned long long k) { return (int64_t)(k ^ 0x8000000000000000ull); }
+
+struct MedoidTables {  // views into the arena
+  const unsigned long long* l1;
+  const uint32_t* l1pre;
+  const unsigned long long* l2;
+  const uint32_t* l2pre;
+  __device__ __forceinline__ int column(int64_t rel) const {
+    const int bs = bitmap_rank(l1, l1pre, rel >> 6);
+    return (int)l2pre[bs] + __popcll(l2[bs] & ((1ull << (rel & 63)) - 1ull));
+  }
 };
 
-// One workgroup per deferred cluster.  Compact column ids come from a
-// two-level occupancy bitmap so any bin range works: level 1 (LDS) has one bit
-// per block of 64 bins, level 2 (arena) one u64 word per OCCUPIED block; the
-// column of bin b is prefix2[block slot] + popcount(word & below(b)).  Rows and
-// the count matrix are bump-allocated from the same arena.
-constexpr int MD_L1WORDS = 1024;  // level-1 bits: 65,536 blocks = 4.2M bins
+__device__ __forceinline__ MedoidTables md_tables(const char* arena, const MedoidMeta& M) {
+  MedoidTables T;
+  T.l1 = reinterpret_cast<const unsigned long long*>(arena + M.l1_off);
+  T.l1pre = reinterpret_cast<const uint32_t*>(arena + M.l1_off + (int64_t)MD_L1WORDS * 8);
+  T.l2 = reinterpret_cast<const unsigned long long*>(arena + M.l2_off);
+  T.l2pre = reinterpret_cast<const uint32_t*>(arena + M.l2_off + (int64_t)M.B1 * 8);
+  return T;
+}
 
-__global__ __launch_bounds__(MD_BLOCK) void medoid_build_kernel(CsrView v, MedoidParams P, const int32_t* deferred,
-                                                                const int32_t* n_deferred, MedoidMeta* meta,
-                                                                char* scratch, unsigned long long* bump,
-                                                                int64_t scratch_bytes, int64_t* rep) {
-  __shared__ unsigned long long l1[MD_L1WORDS];
-  __shared__ uint32_t l1pre[MD_L1WORDS];
+__device__ __forceinline__ int64_t md_bump(unsigned long long* bump, int64_t bytes, int64_t cap) {
+  const int64_t b = (int64_t)atomicAdd(bump, (unsigned long long)bytes);
+  return b + bytes > cap ? -1 : b;
+}
+
+// Pass 1: bin range of every deferred cluster (wave-reduced atomics on
+// order-preserving keys; lo is stored complemented so both are maxima).
+// Block x == 0 also allocates and zeroes the cluster's level-1 bitmap.
+__global__ __launch_bounds__(MD_BLOCK) void medoid_range_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
+                                                                MedoidMeta* meta, char* arena,
+                                                                unsigned long long* bump, int64_t arena_bytes) {
+  __shared__ int64_t base_sh;
+  const int tid = threadIdx.x;
+  const int32_t nd = *n_deferred;
+  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
+    MedoidMeta* M = meta + di;
+    const int64_t s0 = M->s0;
+    const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s0 + M->n];
+    if (blockIdx.x == 0) {
+      if (tid == 0) base_sh = md_bump(bump, md_l1_bytes(), arena_bytes);
+      __syncthreads();
+      const int64_t base = base_sh;
+      if (base >= 0) {
+        unsigned long long* l1 = reinterpret_cast<unsigned long long*>(arena + base);
+        for (int w = tid; w < MD_L1WORDS; w += MD_BLOCK) l1[w] = 0ull;
+      }
+      if (tid == 0) M->l1_off = base;
+      __syncthreads();
+    }
+    long long lo = 0x7fffffffffffffffll, hi = -0x7fffffffffffffffll - 1;
+    for (int64_t k = p0 + (int64_t)blockIdx.x * MD_BLOCK + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
+      const long long b = md_bin(v.mz[k], P);
+      lo = b < lo ? b : lo;
+      hi = b > hi ? b : hi;
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const long long l2 = __shfl_xor(lo, o, kWave), h2 = __shfl_xor(hi, o, kWave);
+      lo = l2 < lo ? l2 : lo;
+      hi = h2 > hi ? h2 : hi;
+    }
+    if (lane_id() == 0 && lo <= hi) {
+      atomicMax(&M->hi_key, md_key(hi));
+      atomicMax(&M->lo_key, ~md_key(lo));
+    }
+  }
+}
+
+__device__ __forceinline__ bool md_range(const MedoidMeta& M, int64_t& blo, int& nw1) {
+  if (M.hi_key == 0ull) { blo = 0; nw1 = 0; return true; }  // no peaks at all
+  blo = md_unkey(~M.lo_key);
+  const int64_t bhi = md_unkey(M.hi_key);
+  const int64_t nblk = ((bhi - blo) >> 6) + 1;
+  const int64_t w = (nblk + 63) / 64;
+  nw1 = w > MD_L1WORDS ? -1 : (int)w;
+  return w <= MD_L1WORDS;
+}
+
+// Pass 2: level-1 occupancy, staged in LDS, merged with one atomicOr per word.
+__global__ __launch_bounds__(MD_BLOCK) void medoid_l1_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
+                                                             const MedoidMeta* meta, char* arena) {
+  __shared__ unsigned long long l1s[MD_L1WORDS];
+  const int tid = threadIdx.x;
+  const int32_t nd = *n_deferred;
+  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
+    const MedoidMeta M = meta[di];
+    int64_t blo;
+    int nw1;
+    if (M.l1_off < 0 || !md_range(M, blo, nw1) || nw1 == 0) continue;
+    const int64_t p0 = v.spec_off[M.s0], p1 = v.spec_off[M.s0 + M.n];
+    const int64_t k0 = p0 + (int64_t)blockIdx.x * MD_BLOCK;
+    if (k0 >= p1) continue;  // uniform per block: no barrier divergence
+    for (int w = tid; w < nw1; w += MD_BLOCK) l1s[w] = 0ull;
+    __syncthreads();
+    for (int64_t k = k0 + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
+      const int64_t blk = (md_bin(v.mz[k], P) - blo) >> 6;
+      atomicOr(&l1s[blk >> 6], 1ull << (blk & 63));
+    }
+    __syncthreads();
+    unsigned long long* l1 = reinterpret_cast<unsigned long long*>(arena + M.l1_off);
+    for (int w = tid; w < nw1; w += MD_BLOCK)
+      if (l1s[w]) atomicOr(&l1[w], l1s[w]);
+    __syncthreads();
+  }
+}
+
+// Plan 1 (one workgroup per cluster): level-1 prefix, allocate + zero level 2.
+__global__ __launch_bounds__(MD_BLOCK) void medoid_plan1_kernel(const int32_t* n_deferred, MedoidMeta* meta,
+                                                                char* arena, unsigned long long* bump,
+                                                                int64_t arena_bytes, int64_t* rep) {
+  __shared__ unsigned long long l1s[MD_L1WORDS];
+  __shared__ uint32_t pre[MD_L1WORDS];
   __shared__ int tmp[MD_BLOCK / kWave + 1];
-  __shared__ long long red[2 * (MD_BLOCK / kWave)];
-  __shared__ unsigned long long base_sh;
+  __shared__ int64_t base_sh;
   const int tid = threadIdx.x;
   const int32_t nd = *n_deferred;
   for (int32_t di = blockIdx.x; di < nd; di += gridDim.x) {
-    const int64_t c = deferred[di];
-    const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
-    const int n = (int)(s1 - s0);
-    const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
-    int64_t blo, bhi;
-    const bool any = cluster_bin_range(v, p0, p1, P, red, blo, bhi);
-    const int64_t nblk = any ? ((bhi - blo) >> 6) + 1 : 0;
-    const int64_t nw1 = (nblk + 63) / 64;
-    MedoidMeta M{c, s0, 0, 0, n, 0, 0, 0};
-    if (nw1 > MD_L1WORDS) {  // > 4.2M bins: reported, not approximated
-      if (tid == 0) { meta[di] = M; rep[c] = -2; }
+    MedoidMeta* M = meta + di;
+    int64_t blo;
+    int nw1;
+    const bool fits = md_range(*M, blo, nw1);
+    if (M->l1_off < 0 || !fits) {  // > 4.2M bins (-2) or arena exhausted (-3): reported, not approximated
+      if (tid == 0) rep[M->c] = fits ? -3 : -2;
       continue;
     }
-    // level 1
-    for (int w = tid; w < nw1; w += MD_BLOCK) l1[w] = 0ull;
+    const unsigned long long* l1 = reinterpret_cast<const unsigned long long*>(arena + M->l1_off);
+    for (int w = tid; w < nw1; w += MD_BLOCK) l1s[w] = l1[w];
     __syncthreads();
-    for (int64_t k = p0 + tid; k < p1; k += MD_BLOCK) {
-      const int64_t blk = (md_bin(v.mz[k], P) - blo) >> 6;
-      atomicOr(&l1[blk >> 6], 1ull << (blk & 63));
-    }
+    const int B1 = bitmap_prefix<MD_BLOCK>(l1s, pre, nw1, tmp);
+    uint32_t* l1pre = reinterpret_cast<uint32_t*>(arena + M->l1_off + (int64_t)MD_L1WORDS * 8);
+    for (int w = tid; w < nw1; w += MD_BLOCK) l1pre[w] = pre[w];
+    if (tid == 0) base_sh = md_bump(bump, md_align((int64_t)B1 * 12 + 8), arena_bytes);
     __syncthreads();
-    const int B1 = bitmap_prefix<MD_BLOCK>(l1, l1pre, (int)nw1, tmp);
-    // arena: level-2 words + their prefix, then rows and counts (sized after K)
-    const int64_t l2_bytes = (((int64_t)B1 * 12) + 255) & ~int64_t(255);
-    if (tid == 0) base_sh = atomicAdd(bump, (unsigned long long)l2_bytes);
-    __syncthreads();
-    const int64_t l2_base = (int64_t)base_sh;
-    if (l2_base + l2_bytes > scratch_bytes) {
-      if (tid == 0) { meta[di] = M; rep[c] = -3; }
+    const int64_t base = base_sh;
+    if (base < 0) {
+      if (tid == 0) { rep[M->c] = -3; M->l1_off = -1; }
       __syncthreads();
       continue;
     }
-    unsigned long long* l2 = reinterpret_cast<unsigned long long*>(scratch + l2_base);
-    uint32_t* l2pre = reinterpret_cast<uint32_t*>(scratch + l2_base + (int64_t)B1 * 8);
+    unsigned long long* l2 = reinterpret_cast<unsigned long long*>(arena + base);
     for (int w = tid; w < B1; w += MD_BLOCK) l2[w] = 0ull;
+    if (tid == 0) { M->blo = blo; M->nw1 = nw1; M->B1 = B1; M->l2_off = base; }
     __syncthreads();
-    auto block_slot = [&](int64_t rel) { return bitmap_rank(l1, l1pre, rel >> 6); };
-    for (int64_t k = p0 + tid; k < p1; k += MD_BLOCK) {
-      const int64_t rel = md_bin(v.mz[k], P) - blo;
-      atomicOr(&l2[block_slot(rel)], 1ull << (rel & 63));
+  }
+}
+
+// Pass 3: level-2 occupancy (LDS-staged when the cluster's level-2 fits).
+__global__ __launch_bounds__(MD_BLOCK) void medoid_l2_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
+                                                             const MedoidMeta* meta, char* arena) {
+  __shared__ unsigned long long l2s[MD_L2LDS];
+  const int tid = threadIdx.x;
+  const int32_t nd = *n_deferred;
+  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
+    const MedoidMeta M = meta[di];
+    if (M.l1_off < 0 || M.l2_off == 0 || M.B1 == 0) continue;
+    const int64_t p0 = v.spec_off[M.s0], p1 = v.spec_off[M.s0 + M.n];
+    const int64_t k0 = p0 + (int64_t)blockIdx.x * MD_BLOCK;
+    if (k0 >= p1) continue;
+    const MedoidTables T = md_tables(arena, M);
+    unsigned long long* l2 = reinterpret_cast<unsigned long long*>(arena + M.l2_off);
+    const bool staged = M.B1 <= MD_L2LDS;
+    if (staged) {
+      for (int w = tid; w < M.B1; w += MD_BLOCK) l2s[w] = 0ull;
+      __syncthreads();
     }
+    for (int64_t k = k0 + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
+      const int64_t rel = md_bin(v.mz[k], P) - M.blo;
+      const int bs = bitmap_rank(T.l1, T.l1pre, rel >> 6);
+      if (staged) atomicOr(&l2s[bs], 1ull << (rel & 63));
+      else atomicOr(&l2[bs], 1ull << (rel & 63));
+    }
+    if (staged) {
+      __syncthreads();
+      for (int w = tid; w < M.B1; w += MD_BLOCK)
+        if (l2s[w]) atomicOr(&l2[w], l2s[w]);
+      __syncthreads();
+    }
+  }
+}
+
+// Plan 2 (one workgroup per cluster): level-2 prefix -> K columns; allocate
+// rows (bit-packed, KW multiple of 8 words, rows padded to Gram tiles), the
+// count matrix, numpy's leaf segmentation of [0, n) and the leaf sums.
+__global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n_deferred, MedoidMeta* meta,
+                                                                char* arena, unsigned long long* bump,
+                                                                int64_t arena_bytes, int64_t* rep) {
+  __shared__ int tmp[MD_BLOCK / kWave + 1];
+  __shared__ int64_t base_sh;
+  const int tid = threadIdx.x;
+  const int32_t nd = *n_deferred;
+  for (int32_t di = blockIdx.x; di < nd; di += gridDim.x) {
+    MedoidMeta* M = meta + di;
+    if (M->l1_off < 0) continue;
+    int K = 0;
+    if (M->B1 > 0) {
+      unsigned long long* l2 = reinterpret_cast<unsigned long long*>(arena + M->l2_off);
+      uint32_t* l2pre = reinterpret_cast<uint32_t*>(arena + M->l2_off + (int64_t)M->B1 * 8);
+      K = bitmap_prefix<MD_BLOCK>(l2, l2pre, M->B1, tmp);
+    }
+    const int n = M->n;
+    const int KW = ((K + 63) / 64 + 7) / 8 * 8 > 0 ? ((K + 63) / 64 + 7) / 8 * 8 : 8;
+    const int T = (n + MD_GT - 1) / MD_GT;
+    const int64_t maxL = md_max_leaves(n);
+    const int64_t rows_b = md_align((int64_t)T * MD_GT * KW * 8);
+    const int64_t cmat_b = md_align((int64_t)n * n * 4);
+    const int64_t leaf_b = md_align((5 * maxL + 1) * 4);        // starts, leaf nodes, program
+    const int64_t lsum_b = md_align(2 * (2 * maxL) * (int64_t)n * 8);  // node values, row and column
+    const int64_t tot_b = md_align((int64_t)n * 8);
+    if (tid == 0) base_sh = md_bump(bump, rows_b + cmat_b + leaf_b + lsum_b + tot_b, arena_bytes);
     __syncthreads();
-    const int K = bitmap_prefix<MD_BLOCK>(l2, l2pre, B1, tmp);
-    auto column = [&](int64_t rel) {
-      const int bs = block_slot(rel);
-      return (int)l2pre[bs] + __popcll(l2[bs] & ((1ull << (rel & 63)) - 1ull));
-    };
-    const int KW = (K + 63) / 64 > 0 ? (K + 63) / 64 : 1;
-    const int T = (n + MD_TILE - 1) / MD_TILE;
-    // rows padded to whole tiles so the Gram kernel never reads past them
-    const int64_t rows_bytes = (int64_t)T * MD_TILE * KW * 8;
-    const int64_t cmat_bytes = (((int64_t)n * n * 4) + 255) & ~int64_t(255);
-    __syncthreads();
-    if (tid == 0) base_sh = atomicAdd(bump, (unsigned long long)(rows_bytes + cmat_bytes));
-    __syncthreads();
-    const int64_t base = (int64_t)base_sh;
-    if (base + rows_bytes + cmat_bytes > scratch_bytes) {
-      if (tid == 0) { meta[di] = M; rep[c] = -3; }
+    const int64_t base = base_sh;
+    if (base < 0) {
+      if (tid == 0) rep[M->c] = -3;
       __syncthreads();
       continue;
     }
-    unsigned long long* rows = reinterpret_cast<unsigned long long*>(scratch + base);
-    for (int64_t w = tid; w < (int64_t)T * MD_TILE * KW; w += MD_BLOCK) rows[w] = 0ull;
+    if (tid == 0) {
+      // numpy's recursion over [0, n) as a post-order program: every node gets
+      // a value slot when it completes; leaves in order, internal nodes as
+      // (left slot, right slot, out slot) with children before parents.
+      int32_t* start = reinterpret_cast<int32_t*>(arena + base + rows_b + cmat_b);  // [maxL + 1]
+      int32_t* lnode = start + (maxL + 1);                                           // [maxL]
+      int32_t* prog = lnode + maxL;                                                  // [3 * maxL]
+      int nl = 0, nq = 0, nid = 0, ret = 0;
+      int64_t lo[40], len[40];
+      int st[40], lft[40];
+      int sp = 0;
+      lo[0] = 0; len[0] = n; st[0] = 0;
+      for (;;) {
+        if (st[sp] == 0 && len[sp] <= 128) {  // leaf
+          start[nl] = (int32_t)lo[sp];
+          lnode[nl++] = nid;
+          ret = nid++;
+        } else if (st[sp] == 0) {  // descend left
+          int64_t h = len[sp] / 2;
+          h -= h % 8;
+          st[sp] = 1;
+          lo[sp + 1] = lo[sp]; len[sp + 1] = h; st[sp + 1] = 0;
+          ++sp;
+          continue;
+        } else if (st[sp] == 1) {  // left done: descend right
+          int64_t h = len[sp] / 2;
+          h -= h % 8;
+          lft[sp] = ret;
+          st[sp] = 2;
+          lo[sp + 1] = lo[sp] + h; len[sp + 1] = len[sp] - h; st[sp + 1] = 0;
+          ++sp;
+          continue;
+        } else {  // both done: internal node
+          prog[3 * nq] = lft[sp]; prog[3 * nq + 1] = ret; prog[3 * nq + 2] = nid;
+          ++nq;
+          ret = nid++;
+        }
+        if (sp == 0) break;
+        --sp;
+      }
+      start[nl] = n;
+      M->KW = KW;
+      M->L = nl;
+      M->rows_off = base;
+      M->cmat_off = base + rows_b;
+      M->leaf_off = base + rows_b + cmat_b;
+      M->lsum_off = base + rows_b + cmat_b + leaf_b;
+      M->tot_off = base + rows_b + cmat_b + leaf_b + lsum_b;
+      M->tiles = T * (T + 1) / 2;
+      M->units = ((n + MD_BLOCK - 1) / MD_BLOCK) * nl;
+      M->ok = 1;
+    }
     __syncthreads();
-    for (int64_t s = s0; s < s1; ++s) {
-      const int64_t a = v.spec_off[s], e = v.spec_off[s + 1];
-      unsigned long long* row = rows + (s - s0) * KW;
-      for (int64_t k = a + tid; k < e; k += MD_BLOCK) {
-        const int col = column(md_bin(v.mz[k], P) - blo);
+  }
+}
+
+// Exclusive scans of Gram tiles and leaf units over the deferred clusters (one workgroup).
+__global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
+                                                               int64_t* tile_base, int64_t* unit_base,
+                                                               int64_t* chunk_base) {
+  __shared__ int64_t tmp[MD_BLOCK / kWave + 1];
+  const int32_t nd = *n_deferred;
+  int64_t ct = 0, cu = 0, cc = 0;
+  for (int32_t i0 = 0; i0 < nd; i0 += MD_BLOCK) {
+    const int32_t i = i0 + threadIdx.x;
+    const bool ok = i < nd && meta[i].ok;
+    int64_t tot;
+    const int64_t et = block_exclusive_scan<MD_BLOCK>(ok ? (int64_t)meta[i].tiles : 0, tmp, tot);
+    if (i < nd) tile_base[i] = ct + et;
+    ct += tot;
+    const int64_t eu = block_exclusive_scan<MD_BLOCK>(ok ? (int64_t)meta[i].units : 0, tmp, tot);
+    if (i < nd) unit_base[i] = cu + eu;
+    cu += tot;
+    const int64_t ec =
+        block_exclusive_scan<MD_BLOCK>(ok ? (int64_t)((meta[i].n + MD_BLOCK - 1) / MD_BLOCK) : 0, tmp, tot);
+    if (i < nd) chunk_base[i] = cc + ec;
+    cc += tot;
+  }
+  if (threadIdx.x == 0) { tile_base[nd] = ct; unit_base[nd] = cu; chunk_base[nd] = cc; }
+}
+
+// which deferred cluster owns work item t (base[lo] <= t < base[lo + 1], skipping empties)
+__device__ __forceinline__ int md_owner(const int64_t* base, int nd, int64_t t) {
+  int lo = 0, hi = nd;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (base[mid] <= t) lo = mid; else hi = mid;
+  }
+  while (lo + 1 < nd && base[lo + 1] <= t) ++lo;
+  return lo;
+}
+
+// Bit rows, one wave per (padded) row: zero the row's words, drain the stores,
+// then OR in one bit per peak (peaks may be unsorted; duplicates are idempotent).
+__global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, MedoidParams P, const MedoidMeta* meta,
+                                                               const int32_t* n_deferred, char* arena) {
+  const int32_t nd = *n_deferred;
+  constexpr int W = MD_BLOCK / kWave;
+  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
+    const MedoidMeta M = meta[di];
+    if (!M.ok) continue;
+    const MedoidTables Tb = md_tables(arena, M);
+    unsigned long long* rows = reinterpret_cast<unsigned long long*>(arena + M.rows_off);
+    const int npad = (M.n + MD_GT - 1) / MD_GT * MD_GT;
+    for (int r = blockIdx.x * W + wave_id(); r < npad; r += gridDim.x * W) {
+      unsigned long long* row = rows + (int64_t)r * M.KW;
+      for (int w = lane_id(); w < M.KW; w += kWave) row[w] = 0ull;
+      if (r >= M.n) continue;
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): zeros land before the ORs
+      const int64_t a = v.spec_off[M.s0 + r], e = v.spec_off[M.s0 + r + 1];
+      for (int64_t k = a + lane_id(); k < e; k += kWave) {
+        const int col = Tb.column(md_bin(v.mz[k], P) - M.blo);
         atomicOr(&row[col >> 6], 1ull << (col & 63));
       }
     }
-    if (tid == 0) {
-      M.rows_off = base;
-      M.cmat_off = base + rows_bytes;
-      M.KW = KW;
-      M.tiles = T * (T + 1) / 2;
-      M.ok = 1;
-      meta[di] = M;
-    }
-    __syncthreads();
   }
 }
 
-// Exclusive scan of Gram tiles over the deferred clusters (one workgroup).
-__global__ __launch_bounds__(MD_BLOCK) void medoid_tile_scan_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
-                                                                    int64_t* tile_base) {
-  __shared__ int64_t tmp[MD_BLOCK / kWave + 1];
-  const int32_t nd = *n_deferred;
-  int64_t carry = 0;
-  for (int32_t i0 = 0; i0 < nd; i0 += MD_BLOCK) {
-    const int32_t i = i0 + threadIdx.x;
-    const int64_t t = (i < nd && meta[i].ok) ? meta[i].tiles : 0;
-    int64_t tot;
-    const int64_t ex = block_exclusive_scan<MD_BLOCK>(t, tmp, tot);
-    if (i < nd) tile_base[i] = carry + ex;
-    carry += tot;
+typedef int md_i32x4 __attribute__((ext_vector_type(4)));
+typedef int md_i32x16 __attribute__((ext_vector_type(16)));
+
+// 64 bins (one u64 row word) -> 64 bytes of 0/1 in 4 x 16 B.  Byte p of dword
+// g (g < 8: low word) holds bin g + 8p -- a fixed permutation of the k axis,
+// identical for the A and B operands, so the dot products are unchanged.
+__device__ __forceinline__ void md_expand_store(unsigned long long w, char* dst) {
+  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+  md_i32x4 out[4];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    out[g >> 2][g & 3] = (int)((lo >> g) & 0x01010101u);
+    out[2 + (g >> 2)][g & 3] = (int)((hi >> g) & 0x01010101u);
   }
-  if (threadIdx.x == 0) tile_base[nd] = carry;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) *reinterpret_cast<md_i32x4*>(dst + 16 * q) = out[q];
 }
 
-// 64x64 tile of c_ij = popcount(row_i & row_j) per workgroup, grid-stride over
-// all tiles of all deferred clusters.  Thread (ty, tx) owns rows 4ty..4ty+3 x
-// columns 4tx..4tx+3; row words staged through LDS in 32-word chunks (rows
-// padded to 33 words: conflict-free column reads).
-__global__ __launch_bounds__(MD_BLOCK) void medoid_gram_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
-                                                               const int64_t* tile_base, char* scratch) {
-  __shared__ unsigned long long As[MD_TILE][MD_KCHUNK + 1];
-  __shared__ unsigned long long Bs[MD_TILE][MD_KCHUNK + 1];
-  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+// c_ij for one 128x128 upper tile (ti <= tj) per iteration, grid-stride over
+// all tiles of all deferred clusters.  4 waves in 2x2, each 64x64 = 2x2 MFMA
+// 32x32 tiles (int32 accumulators, exact).  Thread t streams one row (t < 128:
+// A row t, else B row t-128) through an 8-word register ring (the next 64-byte
+// line is in flight for 8 k-steps), expands one word (64 bins) per k-step into
+// LDS (double-buffered; LDS-only barrier, so the ring is never drained) and
+// each lane reads 16 B per operand per 32-k half (ds_read_b128) for the MFMAs.
+__global__ __launch_bounds__(MD_BLOCK) void medoid_gram_mfma_kernel(const MedoidMeta* meta,
+                                                                    const int32_t* n_deferred,
+                                                                    const int64_t* tile_base, char* arena) {
+  __shared__ __attribute__((aligned(16))) char st[2][2 * MD_GT * MD_GROW];  // [buf][A rows | B rows]
+  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int wm = wv >> 1, wn = wv & 1;
+  const int fr = lane & 31, fh = lane >> 5;
   const int32_t nd = *n_deferred;
   const int64_t total = tile_base[nd];
   for (int64_t t = blockIdx.x; t < total; t += gridDim.x) {
-    int lo = 0, hi = nd;  // tile_base[lo] <= t < tile_base[hi]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (tile_base[mid] <= t) lo = mid; else hi = mid;
-    }
-    while (lo + 1 < nd && tile_base[lo + 1] <= t) ++lo;  // skip empty entries
-    const MedoidMeta M = meta[lo];
-    int64_t r = t - tile_base[lo];
-    const int T = (M.n + MD_TILE - 1) / MD_TILE;
+    const int o = md_owner(tile_base, nd, t);
+    const MedoidMeta M = meta[o];
+    int64_t r = t - tile_base[o];
+    const int T = (M.n + MD_GT - 1) / MD_GT;
     int ti = 0;
     while (r >= T - ti) { r -= T - ti; ++ti; }
     const int tj = ti + (int)r;
-    const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(scratch + M.rows_off);
-    uint32_t* cmat = reinterpret_cast<uint32_t*>(scratch + M.cmat_off);
-    uint32_t acc[4][4] = {};
-    for (int w0 = 0; w0 < M.KW; w0 += MD_KCHUNK) {
-      const int wn = M.KW - w0 < MD_KCHUNK ? M.KW - w0 : MD_KCHUNK;
-      for (int e = tid; e < MD_TILE * MD_KCHUNK; e += MD_BLOCK) {
-        const int rr = e / MD_KCHUNK, ww = e % MD_KCHUNK;
-        const bool in = ww < wn;
-        As[rr][ww] = in ? rows[((int64_t)ti * MD_TILE + rr) * M.KW + w0 + ww] : 0ull;
-        Bs[rr][ww] = in ? rows[((int64_t)tj * MD_TILE + rr) * M.KW + w0 + ww] : 0ull;
+    const int KW = M.KW;  // multiple of 8
+    const int srow = tid < MD_GT ? ti * MD_GT + tid : tj * MD_GT + (tid - MD_GT);
+    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(
+        reinterpret_cast<const unsigned long long*>(arena + M.rows_off) + (int64_t)srow * KW);
+    char* mine[2] = {st[0] + tid * MD_GROW, st[1] + tid * MD_GROW};
+
+    md_i32x16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[a][b][q] = 0;
+
+    ulonglong2 cur[4], nxt[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = src[q];
+    // the ring's first line fully landed: keeps the waitcnt pass from merging
+    // this tile's prologue loads with the in-loop prefetch at the loop header
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    md_expand_store(cur[0].x, mine[0]);
+    lds_barrier();
+    for (int kc = 0; kc < KW; kc += 8) {
+      const bool more = kc + 8 < KW;
+      if (more) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nxt[q] = src[(kc + 8) / 2 + q];
       }
-      __syncthreads();
-      for (int w = 0; w < wn; ++w) {
-        unsigned long long a[4], b[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) { a[q] = As[4 * ty + q][w]; b[q] = Bs[4 * tx + q][w]; }
+      for (int u = 0; u < 8; ++u) {
+        const int buf = u & 1;  // kc is a multiple of 8: (kc + u) & 1 == u & 1
+        const char* A = st[buf] + (wm * 64) * MD_GROW;
+        const char* B = st[buf] + (MD_GT + wn * 64) * MD_GROW;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int h = 0; h < 2; ++h) {
+          md_i32x4 fa[2], fb[2];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) acc[q][u] += (uint32_t)__popcll(a[q] & b[u]);
-      }
-      __syncthreads();
-    }
+          for (int a = 0; a < 2; ++a)
+            fa[a] = *reinterpret_cast<const md_i32x4*>(A + (a * 32 + fr) * MD_GROW + 32 * h + 16 * fh);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+          for (int b = 0; b < 2; ++b)
+            fb[b] = *reinterpret_cast<const md_i32x4*>(B + (b * 32 + fr) * MD_GROW + 32 * h + 16 * fh);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = ti * MD_TILE + 4 * ty + q, j = tj * MD_TILE + 4 * tx + u;
-        if (i < M.n && j < M.n) {
-          cmat[(int64_t)i * M.n + j] = acc[q][u];
-          cmat[(int64_t)j * M.n + i] = acc[q][u];
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
         }
+        if (u < 7) {
+          const unsigned long long w = (u + 1) & 1 ? cur[(u + 1) >> 1].y : cur[(u + 1) >> 1].x;
+          md_expand_store(w, mine[buf ^ 1]);
+        } else if (more) {
+          md_expand_store(nxt[0].x, mine[buf ^ 1]);
+        }
+        lds_barrier();
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+    }
+    // C/D layout (32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+    uint32_t* cmat = reinterpret_cast<uint32_t*>(arena + M.cmat_off);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int i = ti * MD_GT + wm * 64 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
+          const int j = tj * MD_GT + wn * 64 + b * 32 + fr;
+          if (i < M.n && j < M.n) {
+            const uint32_t cnt = (uint32_t)acc[a][b][q];
+            cmat[(int64_t)i * M.n + j] = cnt;
+            cmat[(int64_t)j * M.n + i] = cnt;
+          }
+        }
   }
 }
 
-// Totals and argmin, one workgroup per deferred cluster.  Thread i walks
-// column i of the symmetric count matrix (coalesced across threads) and
-// evaluates numpy's pairwise tree for row i (j >= i) and column i (j <= i).
-__global__ __launch_bounds__(MD_BLOCK) void medoid_totals_kernel(CsrView v, const MedoidMeta* meta,
-                                                                 const int32_t* n_deferred, const char* scratch,
-                                                                 int64_t* rep, double* totals_out) {
+// Both pairwise leaf sums of thread i over j in [lo, lo + m) (m <= 128): row i
+// takes d(i, j) for j >= i, column i takes d(j, i) for j <= i (the reference's
+// upper-triangular matrix, most_similar_representative.py:91-100).
+template <class F>
+__device__ __forceinline__ void dual_leaf_at(const F& f, int lo, int m, int i, double& row, double& col) {
+  if (m < 8) {
+    double r = 0.0, cc = 0.0;
+    for (int j = lo; j < lo + m; ++j) {
+      const double d = f(j);
+      r += j >= i ? d : 0.0;
+      cc += j <= i ? d : 0.0;
+    }
+    row = r;
+    col = cc;
+    return;
+  }
+  double r[8], cc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const double d = f(lo + k);
+    r[k] = lo + k >= i ? d : 0.0;
+    cc[k] = lo + k <= i ? d : 0.0;
+  }
+  int j = 8;
+  const int lim = m - (m % 8);
+  for (; j < lim; j += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int jj = lo + j + k;
+      const double d = f(jj);
+      r[k] += jj >= i ? d : 0.0;
+      cc[k] += jj <= i ? d : 0.0;
+    }
+  }
+  double rs = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  double cs = ((cc[0] + cc[1]) + (cc[2] + cc[3])) + ((cc[4] + cc[5]) + (cc[6] + cc[7]));
+  for (; j < m; ++j) {
+    const int jj = lo + j;
+    const double d = f(jj);
+    rs += jj >= i ? d : 0.0;
+    cs += jj <= i ? d : 0.0;
+  }
+  row = rs;
+  col = cs;
+}
+
+// Leaf sums, grid-stride over (cluster, leaf, 256-wide chunk of i): thread i
+// reads column i of the symmetric count matrix (coalesced across i).
+__global__ __launch_bounds__(MD_BLOCK) void medoid_leaves_kernel(CsrView v, const MedoidMeta* meta,
+                                                                 const int32_t* n_deferred, const int64_t* unit_base,
+                                                                 char* arena) {
+  const int32_t nd = *n_deferred;
+  const int64_t total = unit_base[nd];
+  for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {
+    const int o = md_owner(unit_base, nd, u);
+    const MedoidMeta M = meta[o];
+    const int n = M.n;
+    const int nch = (n + MD_BLOCK - 1) / MD_BLOCK;
+    const int64_t r = u - unit_base[o];
+    const int leaf = (int)(r / nch), ch = (int)(r % nch);
+    const int i = ch * MD_BLOCK + threadIdx.x;
+    if (i >= n) continue;
+    const int32_t* ls = reinterpret_cast<const int32_t*>(arena + M.leaf_off);
+    const int lo = ls[leaf], m = ls[leaf + 1] - lo;
+    const uint32_t* cmat = reinterpret_cast<const uint32_t*>(arena + M.cmat_off);
+    const int64_t* so = v.spec_off + M.s0;
+    const int64_t pi = so[i + 1] - so[i];
+    double row, col;
+    dual_leaf_at([&](int j) { return md_dist(cmat[(int64_t)j * n + i], pi, so[j + 1] - so[j]); }, lo, m, i, row,
+                 col);
+    const int32_t node = ls[md_max_leaves(n) + 1 + leaf];
+    double* lsum = reinterpret_cast<double*>(arena + M.lsum_off);
+    lsum[(int64_t)node * n + i] = row;
+    lsum[(int64_t)(2 * M.L - 1 + node) * n + i] = col;
+  }
+}
+
+// Totals = (tree(row leaves) + tree(column leaves)) / n (most_similar_representative.py:98-100):
+// grid-stride over (cluster, 256-wide chunk of i); thread i runs the cluster's
+// post-order program over its node-value slots (coalesced across i).
+__global__ __launch_bounds__(MD_BLOCK) void medoid_combine_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
+                                                                  const int64_t* chunk_base, char* arena,
+                                                                  double* totals_out) {
+  const int32_t nd = *n_deferred;
+  const int64_t total = chunk_base[nd];
+  for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {
+    const int o = md_owner(chunk_base, nd, u);
+    const MedoidMeta M = meta[o];
+    const int n = M.n;
+    const int i = (int)(u - chunk_base[o]) * MD_BLOCK + threadIdx.x;
+    if (i >= n) continue;
+    const int32_t* prog = reinterpret_cast<const int32_t*>(arena + M.leaf_off) + (md_max_leaves(n) + 1) +
+                          md_max_leaves(n);
+    double* row = reinterpret_cast<double*>(arena + M.lsum_off) + i;
+    double* col = row + (int64_t)(2 * M.L - 1) * n;
+    for (int q = 0; q < M.L - 1; ++q) {
+      const int64_t l = prog[3 * q], r = prog[3 * q + 1], out = prog[3 * q + 2];
+      row[out * n] = row[l * n] + row[r * n];
+      col[out * n] = col[l * n] + col[r * n];
+    }
+    const int64_t root = 2 * M.L - 2;
+    const double t = ((0.0 + row[root * n]) + (0.0 + col[root * n])) / (double)n;
+    reinterpret_cast<double*>(arena + M.tot_off)[i] = t;
+    if (totals_out) totals_out[M.s0 + i] = t;
+  }
+}
+
+// Lowest-index argmin of the totals (most_similar_representative.py:103-110), one workgroup per cluster.
+__global__ __launch_bounds__(MD_BLOCK) void medoid_argmin_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
+                                                                 const char* arena, int64_t* rep) {
   __shared__ double bt_sh[MD_BLOCK / kWave];
   __shared__ int bi_sh[MD_BLOCK / kWave];
   const int tid = threadIdx.x;
@@ -514,24 +934,13 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_totals_kernel(CsrView v, cons
   for (int32_t di = blockIdx.x; di < nd; di += gridDim.x) {
     const MedoidMeta M = meta[di];
     if (!M.ok) continue;
-    const int n = M.n;
-    const uint32_t* cmat = reinterpret_cast<const uint32_t*>(scratch + M.cmat_off);
-    const int64_t* so = v.spec_off + M.s0;
+    const double* tot = reinterpret_cast<const double*>(arena + M.tot_off);
     double best_t = __longlong_as_double(0x7ff0000000000000ll);
     int best_i = 0x7fffffff;
-    for (int i = tid; i < n; i += MD_BLOCK) {
-      const int64_t pi = so[i + 1] - so[i];
-      auto drow = [&](int64_t j) {
-        return j >= i ? md_dist(cmat[j * n + i], pi, so[j + 1] - so[j]) : 0.0;
-      };
-      auto dcol = [&](int64_t j) {
-        return j <= i ? md_dist(cmat[j * n + i], pi, so[j + 1] - so[j]) : 0.0;
-      };
-      const double t = (pw_sum(drow, n) + pw_sum(dcol, n)) / (double)n;
-      if (totals_out) totals_out[M.s0 + i] = t;
+    for (int i = tid; i < M.n; i += MD_BLOCK) {
+      const double t = tot[i];
       if (t < best_t) { best_t = t; best_i = i; }
     }
-    // block argmin, lowest index on ties
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
       const double t2 = __shfl_xor(best_t, o, kWave);

@@ -70,6 +70,13 @@ int32_t ablate_mask() {
   return e ? (int32_t)std::atoi(e) : 0;
 }
 
+// Per-cluster bin-mean kernel: 0 = spectrum-serial LDS kernel (default),
+// 1 = per-bin list kernel.  SPX_BIN_KERNEL selects (A/B profiling).
+int bin_kernel_variant() {
+  const char* e = std::getenv("SPX_BIN_KERNEL");
+  return e ? std::atoi(e) : 0;
+}
+
 int32_t bin_words(const spx_bin_params* p) {
   const double nb = std::trunc((p->maximum - p->minimum) / p->binsize) + 1.0;  // binning.py:172
   return (int32_t)((nb + 63.0) / 64.0);
@@ -127,9 +134,15 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
   if (hipMemsetAsync(n_def, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
-  hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                     charge_out, status, def, n_def);
-  if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
+  if (bin_kernel_variant() == 1) {
+    hipLaunchKernelGGL(spx::bin_mean_list_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                       charge_out, status, def, n_def);
+    if (int rc = check_launch("bin_mean_list_kernel")) return rc;
+  } else {
+    hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                       charge_out, status, def, n_def);
+    if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
+  }
   hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)fallback_grid(C)), dim3(spx::BM_BLOCK), 0, s, V, P,
                      O, prec_out, charge_out, status, def, n_def, scratch,
                      spx::bin_mean_slice_bytes(P.n_words, dcap), (int)std::min<int64_t>(dcap, INT32_MAX));
@@ -193,19 +206,22 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
 // ------------------------------------------------------------------- medoid
 size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t C) {
   if (C < 0 || (C > 0 && (!hco || !hso))) return 0;
-  size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) +
-                 align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
-                 align256(sizeof(spx::MedoidMeta) * (size_t)std::max<int64_t>(C, 1)) +
-                 align256(sizeof(int64_t) * (size_t)(C + 1));
+  const size_t Cm = (size_t)std::max<int64_t>(C, 1);
+  size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(sizeof(int32_t) * Cm) +
+                 align256(sizeof(spx::MedoidMeta) * Cm) + 3 * align256(sizeof(int64_t) * (Cm + 1));
   size_t arena = 0, margin = 0;
   for (int64_t c = 0; c < C; ++c) {
     const int64_t n = hco[c + 1] - hco[c];
     const int64_t p = hso[hco[c + 1]] - hso[hco[c]];
     const int64_t K = std::max<int64_t>(p, 1);  // occupied bins <= peaks
-    const int64_t KW = (K + 63) / 64;
-    const int64_t T = (n + spx::MD_TILE - 1) / spx::MD_TILE;
-    const size_t bytes = (size_t)(T * spx::MD_TILE * KW * 8) + align256((size_t)(n * n * 4)) +
-                         align256((size_t)K * 12);  // + level-2 occupancy words
+    const int64_t KW = ((K + 63) / 64 + 7) / 8 * 8;
+    const int64_t T = (n + spx::MD_GT - 1) / spx::MD_GT;
+    const int64_t B1 = std::min<int64_t>(K, 64 * (int64_t)spx::MD_L1WORDS);
+    const int64_t L = spx::md_max_leaves(n);
+    const size_t bytes = (size_t)(spx::md_l1_bytes() + spx::md_align(B1 * 12 + 8) +
+                                  spx::md_align(T * spx::MD_GT * KW * 8) + spx::md_align(n * n * 4) +
+                                  spx::md_align((5 * L + 1) * 4) + spx::md_align(2 * (2 * L) * n * 8) +
+                                  spx::md_align(n * 8));
     if (n > spx::MD_NMAX) arena += bytes;
     else if (n > 1) margin = std::max(margin, bytes);
   }
@@ -228,27 +244,41 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   int32_t* def = w.take<int32_t>((size_t)C);
   spx::MedoidMeta* meta = w.take<spx::MedoidMeta>((size_t)C);
   int64_t* tile_base = w.take<int64_t>((size_t)C + 1);
+  int64_t* unit_base = w.take<int64_t>((size_t)C + 1);
+  int64_t* chunk_base = w.take<int64_t>((size_t)C + 1);
   if (w.used >= workspace_bytes) return fail(SPX_ENOSPACE, "spx_medoid: workspace too small");
   char* arena = w.base + w.used;
   const int64_t arena_bytes = (int64_t)(workspace_bytes - w.used);
   spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance, ablate_mask()};
   const spx::CsrView V = view(csr);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024));
+  const dim3 grid2(spx::MD_GRIDX, g), blk(spx::MD_BLOCK);
 
   if (hipMemsetAsync(n_def, 0, 512, s) != hipSuccess) return check_launch("spx_medoid memset");
-  hipLaunchKernelGGL(spx::medoid_small_kernel, dim3((unsigned)C), dim3(spx::MD_BLOCK), 0, s, V, P, rep, totals, def,
-                     n_def);
+  hipLaunchKernelGGL(spx::medoid_small_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, def, n_def, meta);
   if (int rc = check_launch("medoid_small_kernel")) return rc;
-  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024));
-  hipLaunchKernelGGL(spx::medoid_build_kernel, dim3(g), dim3(spx::MD_BLOCK), 0, s, V, P, def, n_def, meta, arena,
-                     bump, arena_bytes, rep);
-  if (int rc = check_launch("medoid_build_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_tile_scan_kernel, dim3(1), dim3(spx::MD_BLOCK), 0, s, meta, n_def, tile_base);
-  if (int rc = check_launch("medoid_tile_scan_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_gram_kernel, dim3(2048), dim3(spx::MD_BLOCK), 0, s, meta, n_def, tile_base, arena);
-  if (int rc = check_launch("medoid_gram_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_totals_kernel, dim3(g), dim3(spx::MD_BLOCK), 0, s, V, meta, n_def, arena, rep,
-                     totals);
-  return check_launch("medoid_totals_kernel");
+  hipLaunchKernelGGL(spx::medoid_range_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena, bump, arena_bytes);
+  if (int rc = check_launch("medoid_range_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_l1_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena);
+  if (int rc = check_launch("medoid_l1_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_plan1_kernel, dim3(g), blk, 0, s, n_def, meta, arena, bump, arena_bytes, rep);
+  if (int rc = check_launch("medoid_plan1_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_l2_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena);
+  if (int rc = check_launch("medoid_l2_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_plan2_kernel, dim3(g), blk, 0, s, n_def, meta, arena, bump, arena_bytes, rep);
+  if (int rc = check_launch("medoid_plan2_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_scan_kernel, dim3(1), blk, 0, s, meta, n_def, tile_base, unit_base, chunk_base);
+  if (int rc = check_launch("medoid_scan_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_fill_kernel, grid2, blk, 0, s, V, P, meta, n_def, arena);
+  if (int rc = check_launch("medoid_fill_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_gram_mfma_kernel, dim3(2048), blk, 0, s, meta, n_def, tile_base, arena);
+  if (int rc = check_launch("medoid_gram_mfma_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_leaves_kernel, dim3(4096), blk, 0, s, V, meta, n_def, unit_base, arena);
+  if (int rc = check_launch("medoid_leaves_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_combine_kernel, dim3(1024), blk, 0, s, meta, n_def, chunk_base, arena, totals);
+  if (int rc = check_launch("medoid_combine_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_argmin_kernel, dim3(g), blk, 0, s, meta, n_def, arena, rep);
+  return check_launch("medoid_argmin_kernel");
 }
 
 }  // extern "C"

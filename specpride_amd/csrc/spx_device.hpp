@@ -211,10 +211,12 @@ __device__ __forceinline__ double pw_sum_small(const F& f, int64_t n) {
   return 0.0 + pw_leaf(f, 0, n);
 }
 
-// General form: the recursion unrolled onto an explicit stack (depth <= 40).
-template <class F>
-__device__ double pw_sum(const F& f, int64_t n) {
-  if (n <= 128) return 0.0 + pw_leaf(f, 0, n);
+// numpy's recursion over [0, n) unrolled onto an explicit stack (depth <= 40):
+// leaf(lo, m) returns the sum of the leaf segment [lo, lo + m), m <= 128; the
+// leaves are visited left to right.  Returns 0.0 + tree (np.add.reduce).
+template <class L>
+__device__ double pw_tree(const L& leaf, int64_t n) {
+  if (n <= 128) return 0.0 + leaf(0, n);
   int64_t lo[40], len[40];
   double left[40];
   int state[40];
@@ -223,7 +225,7 @@ __device__ double pw_sum(const F& f, int64_t n) {
   for (;;) {
     const int64_t m = len[sp];
     if (m <= 128) {
-      double val = pw_leaf(f, lo[sp], m);
+      double val = leaf(lo[sp], m);
       for (;;) {
         if (sp == 0) return 0.0 + val;
         --sp;
@@ -250,6 +252,12 @@ __device__ double pw_sum(const F& f, int64_t n) {
       ++sp;
     }
   }
+}
+
+// General form of numpy's pairwise sum of f(0..n-1).
+template <class F>
+__device__ double pw_sum(const F& f, int64_t n) {
+  return pw_tree([&](int64_t lo, int64_t m) { return pw_leaf(f, lo, m); }, n);
 }
 
 // Population count below bit `b` of a u64 bitmap with a per-word exclusive

@@ -204,3 +204,40 @@ def test_empty_batch_and_empty_clusters(gpu):
     assert list(rep) == [-1, 1 - 1 + csr.cluster_off[1]]
     r = engine.bin_mean(b).to_host()
     assert r["out_off"][-1] == 0
+
+
+def test_medoid_large_path_skewed_unsorted_and_empty(gpu):
+    """MFMA Gram path: config-4-like skewed sizes (one n = 1500 cluster: 12x12
+    Gram tiles), unsorted peaks, and empty spectra inside a large cluster."""
+    csr = make_clusters_np(400, seed=5, skewed=True, forced_large=1, large_size=1500, n_template=80)
+    csr = _shuffled(csr, seed=11)
+    rng = np.random.default_rng(2)
+    big = [{"m/z array": np.round(rng.uniform(100, 1800, int(k)), 4), "intensity array": np.ones(int(k))}
+           for k in rng.integers(0, 40, 200)]
+    big[0] = {"m/z array": np.zeros(0), "intensity array": np.zeros(0)}
+    big[150] = {"m/z array": np.zeros(0), "intensity array": np.zeros(0)}
+    extra = SpectraCSR.from_clusters([big])
+    both = SpectraCSR(np.concatenate([csr.cluster_off, csr.cluster_off[-1] + extra.cluster_off[1:]]),
+                      np.concatenate([csr.spec_off, csr.spec_off[-1] + extra.spec_off[1:]]),
+                      np.concatenate([csr.mz, extra.mz]), np.concatenate([csr.inten, extra.inten]),
+                      np.concatenate([csr.prec_mz, extra.prec_mz]), np.concatenate([csr.charge, extra.charge]),
+                      np.concatenate([csr.rt, extra.rt]))
+    assert np.diff(both.cluster_off).max() == 1500
+    rep, tot = engine.medoid(engine.DeviceBatch.from_host(both), with_totals=True).to_host()
+    ref_rep, ref_tot = c_oracle.medoid(both, with_totals=True)
+    np.testing.assert_array_equal(rep, ref_rep)
+    np.testing.assert_array_equal(tot, ref_tot)
+
+
+@pytest.mark.parametrize("name", BIN_SETS)
+def test_bin_mean_list_kernel_variant(gpu, synth, monkeypatch, name):
+    """The per-bin list kernel (SPX_BIN_KERNEL=1) meets the same bit-exact bar."""
+    monkeypatch.setenv("SPX_BIN_KERNEL", "1")
+    z, csr = load_golden(f"bin_mean_{name}.npz")
+    ref = dict(status=z["status"], out_off=z["out_off"], out_mz=z["out_mz"], out_int=z["out_int"],
+               prec=z["out_prec"], charge=z["out_charge"])
+    assert_bin_mean_equal(_bin_mean(csr, **bin_params(z)), ref)
+    if name == "synthetic":
+        assert_bin_mean_equal(_bin_mean(synth), c_oracle.bin_mean(synth))
+        sub = _shuffled(synth.select(range(200)))
+        assert_bin_mean_equal(_bin_mean(sub), c_oracle.bin_mean(sub))

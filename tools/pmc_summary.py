@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc counter_collection.csv files: mean counter value
+per dispatch for each kernel, plus per-wave figures (profiling aid).
+
+    python tools/pmc_summary.py gpurun_out/pmc [--json out.json]
+
+FETCH_SIZE / WRITE_SIZE are reported in KB by rocprofv3; `hbm_bytes` converts
+(x1024).  With --json, writes {kernel_short_name: bytes_per_launch} for the
+FETCH_SIZE + WRITE_SIZE pair (profiles/pmc_traffic.json format read by bench.py).
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def short(name):
+    return name.split("(")[0].replace("spx::", "").replace("void ", "")
+
+
+def load(root):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        per = collections.defaultdict(dict)
+        for r in csv.DictReader(open(f)):
+            key = (r["Dispatch_Id"], r["Kernel_Name"])
+            per[key][r["Counter_Name"]] = per[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        for (_d, k), cs in per.items():
+            for c, v in cs.items():
+                acc[short(k)][c].append(v)
+    return acc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    acc = load(a.root)
+    traffic = {}
+    for k, cs in sorted(acc.items()):
+        mean = {c: sum(v) / len(v) for c, v in cs.items()}
+        print(f"== {k}")
+        waves = mean.get("SQ_WAVES")
+        for c in sorted(mean):
+            extra = ""
+            if waves and c.startswith("SQ_INSTS"):
+                extra = f"   ({mean[c] / waves:.1f} / wave)"
+            print(f"   {c:28s} {mean[c]:16.1f}{extra}")
+        if "SQ_WAVE_CYCLES" in mean:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in mean:
+                    print(f"   {c} / WAVE_CYCLES = {mean[c] / mean['SQ_WAVE_CYCLES']:.3f}")
+        if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+            traffic[k] = (mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
+            print(f"   hbm_bytes (fetch+write)      {traffic[k]:16.0f}")
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(traffic, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,9 @@
 """Phase ablation timing of the two headline kernels (profiling aid, not a test).
 
 Times spx_bin_mean and spx_medoid on the bench batch with SPX_ABLATE masks that
-skip phases, so the cost of each phase is the difference.  Prints JSON."""
+skip phases, so the cost of each phase is the difference.  Prints JSON.
+bin-mean: 1 = stop after P3a (bins, slots, spectrum masks), 2 = skip P3d (folds).
+medoid (small kernel): 16 = skip rows on, 64 = skip pairs, 32 = skip totals."""
 import json
 import os
 import sys
@@ -31,7 +33,11 @@ def main():
     bm = engine.bin_mean(b)
     md = engine.medoid(b)
     res = {}
-    for mask in (0, 1, 3):
+    torch.cuda.synchronize()
+    # first int32 of each workspace = clusters deferred to the generic/large path
+    res["bin_mean_deferred"] = int(b._ws["bin_mean"][:4].view(torch.int32).item())
+    res["medoid_deferred"] = int(b._ws["medoid"][:4].view(torch.int32).item())
+    for mask in (0, 1, 2):
         os.environ["SPX_ABLATE"] = str(mask)
         res[f"bin_mean_ablate{mask}_ms"] = timed(lambda: engine.bin_mean(b, out=bm))
     for mask in (0, 16, 64, 32):
