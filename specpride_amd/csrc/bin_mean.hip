@@ -39,15 +39,16 @@ struct BinMeanParams {
   int32_t ablate;   // profiling only (SPX_ABLATE): 1 skip phase 3, 2 skip phase 4
 };
 
-template <class PrefixT>
+template <class PrefixT, class CountT = uint32_t>
 struct BinMeanState {
   unsigned long long* bitmap;
   PrefixT* wprefix;
-  uint32_t* cnt;
+  CountT* cnt;
   float* acc_i;
   float* acc_m;
   uint32_t* owner;
   int32_t* soff;  // LDS copy of the spectrum offsets (nullptr: read spec_off)
+  double* prec;   // LDS copy of the precursor m/z (nullptr: read prec_mz)
   int* votes;
   int32_t* xch;
   int dcap;
@@ -62,10 +63,10 @@ constexpr int BM_NMAX = 128;
 struct BinMeanSmem {
   unsigned long long bitmap[BM_WMAX];
   uint16_t wprefix[BM_WMAX];
-  uint32_t cnt[BM_DCAP];
+  uint16_t cnt[BM_DCAP];       // <= BM_NMAX spectra per slot
   float acc_i[BM_DCAP];
   float acc_m[BM_DCAP];
-  uint32_t owner[BM_DCAP];
+  double prec[BM_NMAX];       // precursor m/z (np.mean at the end, from LDS)
   int32_t soff[BM_NMAX + 1];  // the cluster's spectrum offsets, relative to its first peak
   int votes[2 * (BM_BLOCK / kWave)];
   int32_t xch[2 * (BM_BLOCK / kWave)];  // lane-0 bin key of each wave (fast path neighbour)
@@ -86,6 +87,11 @@ __device__ __forceinline__ int64_t bin_of(double m, const BinMeanParams& P) {
   return trunc_div_exact(m - P.minimum, P.binsize, P.inv_binsize);
 }
 
+// the LDS paths cap the bin count at 64 * BM_WMAX < 2^17: the cheap exact form applies
+__device__ __forceinline__ int32_t bin_small(double m, const BinMeanParams& P) {
+  return trunc_div_small(m - P.minimum, P.binsize, P.inv_binsize);
+}
+
 __device__ __forceinline__ PeakLane load_lane(const CsrView& v, int64_t k, int64_t e) {
   PeakLane L;
   L.active = k < e;
@@ -96,16 +102,16 @@ __device__ __forceinline__ PeakLane load_lane(const CsrView& v, int64_t k, int64
   return L;
 }
 
-template <class PrefixT>
-__device__ __forceinline__ void accumulate(const BinMeanState<PrefixT>& S, int slot, double m, double it) {
-  S.cnt[slot] += 1u;
+template <class PrefixT, class CountT>
+__device__ __forceinline__ void accumulate(const BinMeanState<PrefixT, CountT>& S, int slot, double m, double it) {
+  S.cnt[slot] += (CountT)1;
   S.acc_i[slot] = (float)((double)S.acc_i[slot] + it);
   S.acc_m[slot] = (float)((double)S.acc_m[slot] + m);
 }
 
 // Processes one spectrum chunk lane on the sorted path.
-template <class PrefixT>
-__device__ __forceinline__ void sorted_lane(const BinMeanState<PrefixT>& S, const BinMeanParams& P,
+template <class PrefixT, class CountT>
+__device__ __forceinline__ void sorted_lane(const BinMeanState<PrefixT, CountT>& S, const BinMeanParams& P,
                                             const PeakLane& L) {
   if (!L.active || !in_range(L.m, P)) return;
   const int64_t b = bin_of(L.m, P);
@@ -113,8 +119,8 @@ __device__ __forceinline__ void sorted_lane(const BinMeanState<PrefixT>& S, cons
   accumulate(S, bitmap_rank(S.bitmap, S.wprefix, b), L.m, L.it);
 }
 
-template <bool kSmall, class PrefixT>
-__device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const BinMeanState<PrefixT>& S,
+template <bool kSmall, class PrefixT, class CountT>
+__device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const BinMeanState<PrefixT, CountT>& S,
                                  int64_t c, const PeaksOut& out, double* prec_out, int32_t* charge_out,
                                  int* tmp, int* flag) {
   const int tid = threadIdx.x;
@@ -127,8 +133,10 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   if (n > S.nmax || P.n_words > (kSmall ? BM_WMAX : 0x7fffffff)) return kDeferred;
 
   // spectrum boundaries, from LDS when the cluster is small enough
-  if constexpr (kSmall)
+  if constexpr (kSmall) {
     for (int64_t j = tid; j <= n; j += BM_BLOCK) S.soff[j] = (int32_t)(v.spec_off[s0 + j] - p0);
+    for (int64_t j = tid; j < n; j += BM_BLOCK) S.prec[j] = v.prec_mz[s0 + j];
+  }
   auto spec_a = [&](int64_t s) -> int64_t {
     if constexpr (kSmall) return p0 + S.soff[s - s0];
     else return v.spec_off[s];
@@ -166,7 +174,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
 #pragma unroll
     for (int u = 0; u < U1; ++u) {
       if (k0 + (int64_t)u * BM_BLOCK < p1 && in_range(m[u], P)) {
-        const int64_t b = bin_of(m[u], P);
+        const int64_t b = kSmall ? (int64_t)bin_small(m[u], P) : bin_of(m[u], P);
         atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
       }
     }
@@ -189,78 +197,92 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   // phase 3: ordered accumulation, one spectrum at a time
   int64_t slow_from = (P.ablate & 1) ? s1 : s0;
   if (fast && !(P.ablate & 1)) {
-    // Optimistic fast path (every spectrum <= 256 peaks; lane t holds peak t).
-    // Each lane computes ONE bin key (-1 below min, INT_MAX at/above max) and
-    // takes its neighbour's key by shuffle (lane 63: from the next wave via
-    // LDS).  If keys are non-decreasing inside every spectrum, equal bins are
-    // contiguous and "last peak of its bin" is a neighbour compare.  A key
-    // inversion or a NaN anywhere sets a flag and the whole cluster is redone
-    // on the slow path below, so the fast path never commits a wrong answer.
-    // Slot lookups happen before the barrier; behind it only the slot
-    // read-modify-write, so one barrier per spectrum is the whole serial cost.
+    // Fast path (every spectrum <= 256 peaks; lane t holds peak t of the
+    // spectrum).  Each lane computes ONE bin key (-1 below min, INT_MAX at or
+    // above max) and its slot, and takes its neighbour's key by shuffle; lane
+    // 63's neighbour is the next wave's lane 0, exchanged through LDS.  If keys
+    // are non-decreasing inside every spectrum, equal bins are contiguous and
+    // "last peak of its bin" is a neighbour compare; a key inversion or a NaN
+    // anywhere defers the whole cluster to the generic kernel.
+    // Software-pipelined by one spectrum: iteration j computes spectrum j's
+    // keys and slots (no shared state) while it finishes spectrum j-1 (lane
+    // 63's exchange, then the slot read-modify-write), so the two latency
+    // chains overlap; one LDS-only barrier per spectrum orders the updates.
     if constexpr (kSmall) {
+      struct Pk { double m, it; };
       auto fetch = [&](int64_t j) {
         const int64_t jj = j < n ? j : n - 1;
         const int64_t a = p0 + S.soff[jj], e = p0 + S.soff[jj + 1];
         const int64_t k = a + tid;
-        PeakLane L;
-        L.m = v.mz[k < e ? k : p0];
-        L.it = v.inten[k < e ? k : p0];
-        L.mn = 0.0;
-        L.active = j < n && k < e;
-        L.has_next = j < n && k + 1 < e;
-        return L;
+        Pk q;
+        q.m = v.mz[k < e ? k : p0];
+        q.it = v.inten[k < e ? k : p0];
+        return q;
       };
       const int lane = lane_id(), wid = wave_id();
+      constexpr int NW = BM_BLOCK / kWave;
       int bad = 0;
       constexpr int PF = 8;
-      PeakLane A[PF], B[PF];
+      Pk A[PF], B[PF];
 #pragma unroll
       for (int j = 0; j < PF; ++j) A[j] = fetch(j);
+      // spectrum j - 1 in flight: its slot (or -1), values, and lane 63's pending key
+      int pslot = -1;
+      int32_t pkey = 0;
+      bool pcheck = false;
+      double pm = 0.0, pit = 0.0;
       for (int64_t jb = 0; jb < n; jb += PF) {
 #pragma unroll
         for (int j = 0; j < PF; ++j) B[j] = fetch(jb + PF + j);
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
-          if (jb + j < n) {
-            const PeakLane& L = A[j];
-            const int par = (int)((jb + j) & 1);
-            int32_t key = L.m < P.minimum ? -1 : 0x7fffffff;
-            bad |= L.active && (L.m != L.m);
+          if (jb + j < n) {  // uniform
+            const int64_t js = jb + j;
+            const int par = (int)(js & 1);
+            const int len = S.soff[js + 1] - S.soff[js];
+            const bool active = tid < len, has_next = tid + 1 < len;
+            const Pk& q = A[j];
+            bad |= active && (q.m != q.m);
+            const bool inr = active && in_range(q.m, P);
+            int32_t key = q.m < P.minimum ? -1 : 0x7fffffff;
             int slot = -1;
-            if (L.active && in_range(L.m, P)) {
-              const int64_t b = bin_of(L.m, P);
-              key = (int32_t)b;
-              slot = bitmap_rank(S.bitmap, S.wprefix, b);
+            if (inr) {
+              key = bin_small(q.m, P);
+              slot = bitmap_rank(S.bitmap, S.wprefix, (int64_t)key);
             }
             const int32_t kn = __shfl_down(key, 1, kWave);
-            if (lane == 0) S.xch[par * (BM_BLOCK / kWave) + wid] = key;
-            if (lane < kWave - 1 && L.has_next) bad |= key > kn;
-            bool last = !(lane < kWave - 1 && L.has_next && kn == key);
-            lds_barrier();
-            if (lane == kWave - 1 && L.has_next) {
-              const int32_t kx = S.xch[par * (BM_BLOCK / kWave) + wid + 1];
-              bad |= key > kx;
-              last = kx != key;
+            if (lane == 0) S.xch[par * NW + wid] = key;
+            bool last = true;
+            if (lane < kWave - 1 && has_next) {
+              bad |= key > kn;
+              last = kn != key;
             }
-            if (slot >= 0 && last) accumulate(S, slot, L.m, L.it);
+            // finish spectrum j - 1: lane 63's neighbour key, then its update
+            if (pcheck) {
+              const int32_t kx = S.xch[(par ^ 1) * NW + wid + 1];
+              bad |= pkey > kx;
+              if (kx == pkey) pslot = -1;
+            }
+            if (pslot >= 0) accumulate(S, pslot, pm, pit);
+            lds_barrier();
+            pslot = last ? slot : -1;
+            pkey = key;
+            pcheck = lane == kWave - 1 && has_next;
+            pm = q.m;
+            pit = q.it;
           }
         }
 #pragma unroll
         for (int j = 0; j < PF; ++j) A[j] = B[j];
       }
-      if (block_any<BM_BLOCK, true>(bad, S.votes, 1)) {
-        // redo the cluster on the slow path from a clean slate
-        for (int d = tid; d < D; d += BM_BLOCK) {
-          S.cnt[d] = 0u;
-          S.acc_i[d] = 0.0f;
-          S.acc_m[d] = 0.0f;
-        }
-        __syncthreads();
-        slow_from = s0;
-      } else {
-        slow_from = s1;
+      if (pcheck) {
+        const int32_t kx = S.xch[(int)((n - 1) & 1) * NW + wid + 1];
+        bad |= pkey > kx;
+        if (kx == pkey) pslot = -1;
       }
+      if (pslot >= 0) accumulate(S, pslot, pm, pit);
+      if (block_any<BM_BLOCK, true>(bad, S.votes, 1)) return kDeferred;  // generic kernel redoes it
+      slow_from = s1;
     }
   }
   for (int64_t s = slow_from; s < s1; ++s) {
@@ -276,6 +298,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
     }
     // unsorted spectrum: the highest file position per slot wins (tags grow
     // monotonically through the cluster, so stale tags never win)
+    if (S.owner == nullptr) return kDeferred;  // LDS kernel: no tag array, generic kernel
     if (*flag == 0) {
       for (int d = tid; d < D; d += BM_BLOCK) S.owner[d] = 0u;
       __syncthreads();
@@ -306,7 +329,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   int mine = 0;
   for (int j = 0; j < per; ++j) {
     const int d = d0 + j;
-    if (d < D && S.cnt[d] >= quorum && !isnan((double)S.acc_i[d] / (double)S.cnt[d])) ++mine;
+    if (d < D && S.cnt[d] >= quorum && !isnan(S.acc_i[d])) ++mine;  // cnt >= 1: mean NaN iff sum NaN
   }
   int total;
   int o = block_exclusive_scan<BM_BLOCK>(mine, tmp, total);
@@ -325,7 +348,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
     out.count[c] = total;
     charge_out[c] = z0;
     // np.mean of the precursor list (binning.py:224): pairwise sum / n
-    const double* pr = v.prec_mz + s0;
+    const double* pr = kSmall ? S.prec : v.prec_mz + s0;
     const double sum = kSmall ? pw_sum_small([&](int64_t j) { return pr[j]; }, n)
                               : pw_sum([&](int64_t j) { return pr[j]; }, n);
     prec_out[c] = sum / (double)n;
@@ -339,8 +362,8 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_lds_kernel(CsrView v, BinMe
                                                                 int32_t* n_deferred) {
   __shared__ BinMeanSmem L;
   const int64_t c = blockIdx.x;
-  BinMeanState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, L.owner, L.soff, L.votes, L.xch, BM_DCAP,
-                           BM_NMAX};
+  BinMeanState<uint16_t, uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, nullptr, L.soff, L.prec, L.votes, L.xch,
+                           BM_DCAP, BM_NMAX};
   const int32_t st = bin_mean_body<true>(v, P, S, c, out, prec_out, charge_out, L.tmp, &L.flag);
   if (threadIdx.x == 0) {
     status[c] = st;
@@ -649,6 +672,268 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_list_kernel(CsrView v, BinM
   }
 }
 
+// ------------------------------------------------------------------------
+// bin_mean_fold_kernel (variant 2): bins computed ONCE, spectrum-serial fold
+// with a trivial per-step body.
+//   P1  flat pass over the cluster's peaks (<= 48 per thread, in registers):
+//       exact bin (trunc_div_small), LDS occupancy bitmap, and "last peak of its
+//       bin in its spectrum" from the neighbour's key (shuffle; lane 63 reads
+//       the next wave's lane-0 key after the barrier).  Keys must be
+//       non-decreasing inside every spectrum (else: deferred).
+//   P2  popcount prefix -> compact slots in ascending bin order.
+//   P3a every register entry becomes a u16 code: slot if the peak is the last
+//       of its bin in its spectrum, else NONE.
+//   P3  codes go to LDS (aliasing the dead bitmap) in spectrum-aligned chunks
+//       of <= BF_CODES peaks; the fold walks spectra in file order: lane t
+//       reads its code and, if it owns a slot, does the reference's
+//       cnt += 1; I = f32(f64(I) + it); M = f32(f64(M) + mz) (binning.py:197-199).
+//       m/z and intensity come through an 8-spectrum register prefetch ring; one
+//       LDS-only barrier per spectrum.
+//   P4  quorum filter and ordered output, as the other kernels.
+constexpr int BF_CODES = 7680;  // u16 codes per chunk (= bitmap + prefix bytes)
+constexpr uint16_t BF_NONE = 0xFFFFu;
+constexpr int BF_PB = 8;  // P1 loads in flight per thread
+
+struct BinFoldSmem {
+  union {
+    struct {
+      unsigned long long bitmap[BM_WMAX];
+      uint16_t wprefix[BM_WMAX];
+    } b;                       // P1..P3a
+    uint16_t code[BF_CODES];   // P3 (per chunk)
+  } u;
+  uint32_t cnt[BM_DCAP];
+  float acc_i[BM_DCAP];
+  float acc_m[BM_DCAP];
+  int32_t soff[BL_NMAX + 1];
+  unsigned long long sbits[BL_SW];
+  int32_t xch[BL_UMAX * (BM_BLOCK / kWave)];
+  int votes[2 * (BM_BLOCK / kWave)];
+  int tmp[BM_BLOCK / kWave + 1];
+};
+
+__global__ __launch_bounds__(BM_BLOCK, 4) void bin_mean_fold_kernel(CsrView v, BinMeanParams P, PeaksOut out,
+                                                                 double* prec_out, int32_t* charge_out,
+                                                                 int32_t* status, int32_t* deferred,
+                                                                 int32_t* n_deferred) {
+  static_assert(sizeof(BinFoldSmem::u) >= BF_CODES * 2, "codes alias the bitmap");
+  __shared__ BinFoldSmem L;
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  constexpr int NW = BM_BLOCK / kWave;
+  const int64_t c = blockIdx.x;
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+  const int n = (int)(s1 - s0);
+  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
+  const int np = (int)(p1 - p0);
+  auto defer = [&]() {
+    if (tid == 0) {
+      status[c] = kDeferred;
+      deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    }
+  };
+  if (n == 0) {
+    if (tid == 0) { bl_finish_empty(out, prec_out, charge_out, c); status[c] = kEmpty; }
+    return;
+  }
+  if (n > BL_NMAX || p1 - p0 > BL_PCAP || P.n_words > BM_WMAX) { defer(); return; }
+
+  // P0: charge check (binning.py:205-206), spectrum offsets and starts, zeroing
+  const int32_t z0 = v.charge[s0];
+  int mixed = 0, longspec = 0;
+  if (tid <= n) L.soff[tid] = (int32_t)(v.spec_off[s0 + tid] - p0);
+  if (tid < n) mixed = v.charge[s0 + tid] != z0;
+  const int nsw = (np + 63) / 64;
+  for (int w = tid; w < P.n_words; w += BM_BLOCK) L.u.b.bitmap[w] = 0ull;
+  for (int w = tid; w < nsw; w += BM_BLOCK) L.sbits[w] = 0ull;
+  if (block_any<BM_BLOCK, true>(mixed, L.votes, 0)) {
+    if (tid == 0) { bl_finish_empty(out, prec_out, charge_out, c); status[c] = kMixedCharge; }
+    return;
+  }
+  if (tid >= 1 && tid < n) {
+    const int r = L.soff[tid];
+    if (r < np) atomicOr(&L.sbits[r >> 6], 1ull << (r & 63));  // empty spectra share a bit: harmless here
+  }
+  if (tid < n) longspec = L.soff[tid + 1] - L.soff[tid] > BF_CODES;
+  if (block_any<BM_BLOCK, true>(longspec, L.votes, 1)) { defer(); return; }
+
+  // P1
+  uint32_t ent[BL_UMAX];
+  int bad = 0;
+#pragma unroll
+  for (int u = 0; u < BL_UMAX; ++u) ent[u] = 0u;
+#pragma unroll
+  for (int u0 = 0; u0 < BL_UMAX; u0 += BF_PB) {
+    if (u0 * BM_BLOCK < np) {  // uniform
+      double mb[BF_PB];
+#pragma unroll
+      for (int q = 0; q < BF_PB; ++q) {
+        const int r = (u0 + q) * BM_BLOCK + tid;
+        mb[q] = v.mz[p0 + (r < np ? r : 0)];
+      }
+#pragma unroll
+      for (int q = 0; q < BF_PB; ++q) {
+        const int u = u0 + q;
+        if (u * BM_BLOCK < np) {  // uniform
+          const int r = u * BM_BLOCK + tid;
+          const bool valid = r < np;
+          const double m = mb[q];
+          bad |= valid && (m != m);
+          const bool inr = valid && in_range(m, P);
+          int32_t key = m < P.minimum ? -1 : 0x7fffffff;
+          if (inr) {
+            key = trunc_div_small(m - P.minimum, P.binsize, P.inv_binsize);
+            atomicOr(&L.u.b.bitmap[key >> 6], 1ull << (key & 63));
+          }
+          const int32_t kn = __shfl_down(key, 1, kWave);
+          if (lane == 0) L.xch[u * NW + wid] = key;
+          const int rn = r + 1;
+          const bool same = valid && rn < np && !((L.sbits[rn >> 6] >> (rn & 63)) & 1ull);
+          uint32_t e = inr ? (BL_IN | (uint32_t)key) : (key == 0x7fffffff ? BL_HI : 0u);
+          if (lane < kWave - 1) {
+            bad |= same && key > kn;
+            if (!(same && kn == key)) e |= BL_LAST;
+          } else if (same) {
+            e |= BL_NXT;
+          } else {
+            e |= BL_LAST;
+          }
+          ent[u] = e;
+        }
+      }
+    }
+  }
+  if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) { defer(); return; }
+
+  // P2
+  const int D = bitmap_prefix<BM_BLOCK>(L.u.b.bitmap, L.u.b.wprefix, P.n_words, L.tmp);
+  if (D > BM_DCAP) { defer(); return; }
+  for (int d = tid; d < D; d += BM_BLOCK) {
+    L.cnt[d] = 0u;
+    L.acc_i[d] = 0.0f;
+    L.acc_m[d] = 0.0f;
+  }
+
+  // P3a: entry -> code (slot of a last peak, else BF_NONE), two u16 codes per register
+  uint32_t pk[BL_UMAX / 2];
+#pragma unroll
+  for (int u = 0; u < BL_UMAX; ++u) {
+    uint32_t cd = BF_NONE;
+    if (u * BM_BLOCK < np) {
+      uint32_t e = ent[u];
+      if (e & BL_NXT) {
+        const int32_t kx = wid < NW - 1 ? L.xch[u * NW + wid + 1] : L.xch[(u + 1) * NW];
+        const int32_t key = (e & BL_IN) ? (int32_t)(e & BL_VAL) : ((e & BL_HI) ? 0x7fffffff : -1);
+        bad |= key > kx;
+        if (kx != key) e |= BL_LAST;
+      }
+      if ((e & BL_IN) && (e & BL_LAST))
+        cd = (uint32_t)bitmap_rank(L.u.b.bitmap, L.u.b.wprefix, (int64_t)(e & BL_VAL));
+    }
+    if (u & 1) pk[u >> 1] |= cd << 16;
+    else pk[u >> 1] = cd;
+  }
+  if (block_any<BM_BLOCK, true>(bad, L.votes, 1)) { defer(); return; }
+  if (P.ablate & 1) {
+    if (tid == 0) { out.count[c] = 0; status[c] = kOk; }
+    return;
+  }
+
+  // P3: chunks of whole spectra, codes to LDS, spectrum-serial fold
+  constexpr int PF = 4;
+  auto fetch = [&](int j, double& m, double& it) {
+    const int jj = j < n ? j : n - 1;
+    const int a = L.soff[jj], e = L.soff[jj + 1];
+    const int k = a + tid < e ? a + tid : 0;
+    m = v.mz[p0 + k];
+    it = v.inten[p0 + k];
+  };
+  double Am[PF], Ai[PF], Bm[PF], Bi[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) fetch(j, Am[j], Ai[j]);
+  int sa = 0;
+  while (sa < n) {  // uniform
+    int sb = sa + 1;
+    while (sb < n && L.soff[sb + 1] - L.soff[sa] <= BF_CODES) ++sb;
+    const int ka = L.soff[sa], kb = L.soff[sb];
+#pragma unroll
+    for (int u = 0; u < BL_UMAX; ++u) {
+      const int r = u * BM_BLOCK + tid;
+      if (u * BM_BLOCK < np && r >= ka && r < kb) L.u.code[r - ka] = (uint16_t)(pk[u >> 1] >> (16 * (u & 1)));
+    }
+    lds_barrier();
+    for (int jb = sa; jb < sb; ++jb) {
+      // ring: Am/Ai hold spectra [jr, jr + PF) where jr = jb - (jb % PF) relative to 0
+      const int q = jb % PF;
+      if (q == 0) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) fetch(jb + PF + j, Bm[j], Bi[j]);
+      }
+      double m = 0.0, it = 0.0;
+#pragma unroll
+      for (int j = 0; j < PF; ++j)
+        if (j == q) { m = Am[j]; it = Ai[j]; }
+      const int a = L.soff[jb], e = L.soff[jb + 1];
+      if (a + tid < e) {
+        const uint16_t cd = L.u.code[a - ka + tid];
+        if (cd != BF_NONE) {
+          L.cnt[cd] += 1u;
+          L.acc_i[cd] = (float)((double)L.acc_i[cd] + it);
+          L.acc_m[cd] = (float)((double)L.acc_m[cd] + m);
+        }
+      }
+      for (int k = a + BM_BLOCK + tid; k < e; k += BM_BLOCK) {  // spectra longer than the block
+        const uint16_t cd = L.u.code[k - ka];
+        if (cd != BF_NONE) {
+          L.cnt[cd] += 1u;
+          L.acc_i[cd] = (float)((double)L.acc_i[cd] + v.inten[p0 + k]);
+          L.acc_m[cd] = (float)((double)L.acc_m[cd] + v.mz[p0 + k]);
+        }
+      }
+      if (q == PF - 1) {
+#pragma unroll
+        for (int j = 0; j < PF; ++j) { Am[j] = Bm[j]; Ai[j] = Bi[j]; }
+      }
+      lds_barrier();
+    }
+    sa = sb;
+  }
+  __syncthreads();
+
+  if (P.ablate & 2) {
+    if (tid == 0) { out.count[c] = 0; status[c] = kOk; }
+    return;
+  }
+  // P4: quorum filter and ordered output (binning.py:181-183, 209-222)
+  const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
+  const int per = (D + BM_BLOCK - 1) / BM_BLOCK;
+  const int d0 = tid * per;
+  int mine = 0;
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d < D && L.cnt[d] >= quorum && !isnan(L.acc_i[d])) ++mine;
+  }
+  int total;
+  int o = block_exclusive_scan<BM_BLOCK>(mine, L.tmp, total);
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d < D && L.cnt[d] >= quorum) {
+      const double cn = (double)L.cnt[d];
+      const double mi = (double)L.acc_i[d] / cn;
+      if (isnan(mi)) continue;
+      out.inten[p0 + o] = mi;
+      out.mz[p0 + o] = L.acc_m[d] == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)L.acc_m[d] / cn;
+      ++o;
+    }
+  }
+  if (tid == 0) {
+    out.count[c] = total;
+    charge_out[c] = z0;
+    const double* pr = v.prec_mz + s0;
+    prec_out[c] = pw_sum_small([&](int64_t j) { return pr[j]; }, n) / (double)n;  // np.mean, n <= 64
+    status[c] = kOk;
+  }
+}
+
 // Scratch slice of the deferred path, every array 256-B aligned.
 struct BinSliceLayout {
   int64_t bitmap, wprefix, cnt, acc_i, acc_m, owner, total;
@@ -678,7 +963,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, Bi
   __shared__ int flag;
   char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
   const BinSliceLayout Lo = bin_slice_layout(P.n_words, dcap);
-  BinMeanState<uint32_t> S;
+  BinMeanState<uint32_t, uint32_t> S;
   S.bitmap = reinterpret_cast<unsigned long long*>(base + Lo.bitmap);
   S.wprefix = reinterpret_cast<uint32_t*>(base + Lo.wprefix);
   S.cnt = reinterpret_cast<uint32_t*>(base + Lo.cnt);
@@ -686,6 +971,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_global_kernel(CsrView v, Bi
   S.acc_m = reinterpret_cast<float*>(base + Lo.acc_m);
   S.owner = reinterpret_cast<uint32_t*>(base + Lo.owner);
   S.soff = nullptr;
+  S.prec = nullptr;
   S.votes = votes;
   S.xch = nullptr;
   S.dcap = dcap;

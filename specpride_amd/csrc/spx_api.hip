@@ -71,7 +71,7 @@ int32_t ablate_mask() {
 }
 
 // Per-cluster bin-mean kernel: 0 = spectrum-serial LDS kernel (default),
-// 1 = per-bin list kernel.  SPX_BIN_KERNEL selects (A/B profiling).
+// 1 = per-bin list kernel, 2 = fold kernel.  SPX_BIN_KERNEL selects (A/B profiling).
 int bin_kernel_variant() {
   const char* e = std::getenv("SPX_BIN_KERNEL");
   return e ? std::atoi(e) : 0;
@@ -134,7 +134,11 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
   if (hipMemsetAsync(n_def, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
-  if (bin_kernel_variant() == 1) {
+  if (bin_kernel_variant() == 2) {
+    hipLaunchKernelGGL(spx::bin_mean_fold_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                       charge_out, status, def, n_def);
+    if (int rc = check_launch("bin_mean_fold_kernel")) return rc;
+  } else if (bin_kernel_variant() == 1) {
     hipLaunchKernelGGL(spx::bin_mean_list_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                        charge_out, status, def, n_def);
     if (int rc = check_launch("bin_mean_list_kernel")) return rc;

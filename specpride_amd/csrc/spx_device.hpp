@@ -140,33 +140,46 @@ __device__ __forceinline__ int block_any(int pred, int* votes, int parity) {
 // ------------------------------------------------------ exact bin indexing
 // trunc(fl((m - lo) / w)) and ceil(fl(m / w)) exactly as numpy / OpenMS compute
 // them (IEEE subtract + correctly rounded divide), without paying a f64 divide
-// per peak: q = x * (1/w) is within ~2 ulp of the exact quotient, so whenever q
-// is further than 2^-44 (relative) from an integer, the rounded quotient lies
-// on the same side and trunc/ceil agree.  Near an integer the exact divide runs.
+// per peak.  Exact trunc/floor/ceil of fl(x / w) via the reciprocal product q = x * (1/w):
+// for |q| < 2^24, q is within 2^-27 of fl(x / w), so outside a 2^-24 band
+// around an integer q's integer part is the answer (32-bit conversion); inside
+// the band, or for larger quotients, the correctly rounded division decides.
+constexpr double kDivFastLimit = 0x1p24;
+constexpr double kDivBand = 0x1p-24;
+
 __device__ __forceinline__ int64_t trunc_div_exact(double x, double w, double inv_w) {
-  double q = x * inv_w;
-  double t = trunc(q);
-  double f = q - t;
-  double eps = fabs(q) * 0x1p-44;
-  if (f > eps && f < 1.0 - eps) return (int64_t)t;
+  const double q = x * inv_w;
+  const double t = trunc(q);
+  const double f = fabs(q - t);
+  if (fabs(q) < kDivFastLimit && f > kDivBand && f < 1.0 - kDivBand) return (int64_t)(int32_t)t;
   return (int64_t)trunc(x / w);
 }
 
+// trunc(fl(x / w)) for 0 <= x / w < 2^17 (the LDS bin-mean paths).  There the
+// reciprocal product q is within 2^-34 of fl(x / w), so outside a 2^-30 band
+// around an integer its integer part is the answer; inside the band (1 peak in
+// ~10^8 for arbitrary m/z) the correctly rounded division decides.
+__device__ __forceinline__ int32_t trunc_div_small(double x, double w, double inv_w) {
+  const double q = x * inv_w;
+  const double t = trunc(q);
+  const double f = q - t;
+  if (f > 0x1p-30 && f < 1.0 - 0x1p-30) return (int32_t)t;
+  return (int32_t)trunc(x / w);
+}
+
 __device__ __forceinline__ int64_t floor_div_exact(double x, double w, double inv_w) {
-  double q = x * inv_w;
-  double t = floor(q);
-  double f = q - t;
-  double eps = fabs(q) * 0x1p-44;
-  if (f > eps && f < 1.0 - eps) return (int64_t)t;
+  const double q = x * inv_w;
+  const double t = floor(q);
+  const double f = q - t;
+  if (fabs(q) < kDivFastLimit && f > kDivBand && f < 1.0 - kDivBand) return (int64_t)(int32_t)t;
   return (int64_t)floor(x / w);
 }
 
 __device__ __forceinline__ int64_t ceil_div_exact(double x, double w, double inv_w) {
-  double q = x * inv_w;
-  double t = ceil(q);
-  double f = t - q;
-  double eps = fabs(q) * 0x1p-44;
-  if (f > eps && f < 1.0 - eps) return (int64_t)t;
+  const double q = x * inv_w;
+  const double t = ceil(q);
+  const double f = t - q;
+  if (fabs(q) < kDivFastLimit && f > kDivBand && f < 1.0 - kDivBand) return (int64_t)(int32_t)t;
   return (int64_t)ceil(x / w);
 }
 

@@ -229,10 +229,12 @@ def test_medoid_large_path_skewed_unsorted_and_empty(gpu):
     np.testing.assert_array_equal(tot, ref_tot)
 
 
+@pytest.mark.parametrize("variant", ["1", "2"])
 @pytest.mark.parametrize("name", BIN_SETS)
-def test_bin_mean_list_kernel_variant(gpu, synth, monkeypatch, name):
-    """The per-bin list kernel (SPX_BIN_KERNEL=1) meets the same bit-exact bar."""
-    monkeypatch.setenv("SPX_BIN_KERNEL", "1")
+def test_bin_mean_kernel_variants(gpu, synth, monkeypatch, name, variant):
+    """The per-bin list kernel (SPX_BIN_KERNEL=1) and the fold kernel (=2) meet
+    the same bit-exact bar as the default kernel."""
+    monkeypatch.setenv("SPX_BIN_KERNEL", variant)
     z, csr = load_golden(f"bin_mean_{name}.npz")
     ref = dict(status=z["status"], out_off=z["out_off"], out_mz=z["out_mz"], out_int=z["out_int"],
                prec=z["out_prec"], charge=z["out_charge"])

@@ -37,9 +37,18 @@ def main():
     # first int32 of each workspace = clusters deferred to the generic/large path
     res["bin_mean_deferred"] = int(b._ws["bin_mean"][:4].view(torch.int32).item())
     res["medoid_deferred"] = int(b._ws["medoid"][:4].view(torch.int32).item())
-    for mask in (0, 1, 2):
-        os.environ["SPX_ABLATE"] = str(mask)
-        res[f"bin_mean_ablate{mask}_ms"] = timed(lambda: engine.bin_mean(b, out=bm))
+    for var in ("0", "1", "2"):
+        os.environ["SPX_BIN_KERNEL"] = var
+        for mask in (0, 1, 2):
+            os.environ["SPX_ABLATE"] = str(mask)
+            res[f"bin_mean_v{var}_ablate{mask}_ms"] = timed(lambda: engine.bin_mean(b, out=bm))
+        os.environ["SPX_ABLATE"] = "0"
+        torch.cuda.synchronize()
+        b._ws["bin_mean"][:4].zero_()
+        engine.bin_mean(b, out=bm)
+        torch.cuda.synchronize()
+        res[f"bin_mean_v{var}_deferred"] = int(b._ws["bin_mean"][:4].view(torch.int32).item())
+    os.environ["SPX_BIN_KERNEL"] = "0"
     for mask in (0, 16, 64, 32):
         os.environ["SPX_ABLATE"] = str(mask)
         res[f"medoid_ablate{mask}_ms"] = timed(lambda: engine.medoid(b, out=md))
