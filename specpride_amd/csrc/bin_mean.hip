@@ -934,6 +934,312 @@ __global__ __launch_bounds__(BM_BLOCK, 4) void bin_mean_fold_kernel(CsrView v, B
   }
 }
 
+// ------------------------------------------------------------------------
+// bin_mean_hash_kernel (variant 3): ONE pass over the cluster's peaks.
+//
+// The two-pass LDS kernels first stream every m/z to build the occupied-bin
+// bitmap (slot = rank of the bin), then stream m/z and intensity again for the
+// ordered fold: 24 B of loads per peak.  Here the per-cluster accumulators live
+// in an LDS hash table keyed by bin, so the fold starts with the first spectrum
+// and every peak is loaded exactly once (16 B per peak, the algorithmic minimum).
+//   * spectra in file order through a BH_PF-deep register prefetch ring.  Wave w
+//     takes peaks 63w .. 63w+63 of a 252-peak chunk: lane 63 duplicates the next
+//     wave's lane 0, so every participating lane finds its successor's key in its
+//     own wave (one DPP move) -- no cross-wave exchange; lane 63 never updates.
+//   * key = exact trunc(fl((mz - min)/binsize)) (spx_device.hpp); the last peak of
+//     each run of equal keys in a spectrum is the one numpy's fancy-index "+="
+//     keeps (binning.py:197-199)
+//   * table: H bins in groups of 4 (one ds_read_b128 per probe), hashed home
+//     group, double-hashed probing over groups; a new bin is claimed by LDS
+//     compare-and-swap.  Groups fill left to right, so the first word of a group
+//     that is the bin OR empty ends a search.  Counts (u16) and float32
+//     accumulators (I, M) in parallel arrays.
+//   * update: count += 1; I = f32(f64(I) + it); M = f32(f64(M) + mz) -- the
+//     reference's float32 accumulation in spectrum order (one LDS-only barrier
+//     per spectrum; bins are unique inside a step, so updates never collide)
+//   * end: kept slots (count >= int(0.25 n)+1, mean not NaN) go to an occupancy
+//     bitmap (aliasing the accumulators) whose popcount prefix gives each its
+//     output position in ascending bin order (binning.py:209-222)
+// Deferred to bin_mean_global_kernel: > BM_NMAX spectra, > BM_WMAX bitmap
+// words, a key inversion inside a spectrum (unsorted; NaN next to in-range
+// peaks), a full table.
+constexpr uint32_t BH_EMPTY = 0xFFFFFFFFu;  // never a bin (< 2^17)
+constexpr int BH_PF = 8;                    // spectra in flight per lane
+constexpr int BH_CHUNK = 4 * (kWave - 1);   // peaks per block step (252)
+constexpr int BH_MAXITER = 64;              // probe iterations before a cluster is deferred (table full)
+
+template <int H>
+struct BinHashSmem {
+  uint32_t key[H];      // bin, or BH_EMPTY
+  uint32_t cnt2[H / 2];  // u16 counts, two per word (ds_add_u32 on the right half)
+  union {
+    float2 acc[H];  // (I, M) float32 running sums
+    struct {
+      unsigned long long bitmap[BM_WMAX];
+      uint16_t wprefix[BM_WMAX];
+    } b;  // output ordering (after the fold)
+  } u;
+  double prec[BM_NMAX];
+  int32_t soff[BM_NMAX + 1 + 2 * BH_PF];  // spectrum offsets relative to the cluster's first peak (+ end pad)
+  int votes[2 * (BM_BLOCK / kWave)];
+  int tmp[BM_BLOCK / kWave + 1];
+};
+
+// home group and probe stride (odd: the sequence visits every group) of a bin.
+// Adjacent bins (a jittered peak straddling a bin edge) land far apart.
+template <int H>
+__device__ __forceinline__ uint32_t bh_home(uint32_t key) {
+  constexpr int LG = __builtin_ctz(H / 4);
+  return __umul24(key, 0x9E3779u) >> (24 - LG) & (H / 4 - 1);
+}
+__device__ __forceinline__ uint32_t bh_stride(uint32_t key) { return (__umul24(key, 0x85EBCAu) >> 12) | 1u; }
+
+// lane i receives lane i+1's value (DPP wave_shl:1); lane 63 receives `old`
+__device__ __forceinline__ int32_t wave_next(int32_t x, int32_t old) {
+  return __builtin_amdgcn_update_dpp(old, x, 0x130, 0xF, 0xF, false);
+}
+
+// First word of a group that is `key` or empty (-1: neither; the group is full
+// of other bins).  Sets hit when it is `key`.
+__device__ __forceinline__ int bh_find4(const uint4& k, uint32_t key, bool& hit) {
+  const bool m0 = k.x == key, m1 = k.y == key, m2 = k.z == key, m3 = k.w == key;
+  const bool s0 = m0 | (k.x == BH_EMPTY), s1 = m1 | (k.y == BH_EMPTY), s2 = m2 | (k.z == BH_EMPTY),
+             s3 = m3 | (k.w == BH_EMPTY);
+  hit = m0 | m1 | m2 | m3;
+  return s0 ? 0 : s1 ? 1 : s2 ? 2 : s3 ? 3 : -1;
+}
+
+template <int H>
+__device__ __forceinline__ void bh_count_add(BinHashSmem<H>& L, int slot) {
+  atomicAdd(&L.cnt2[slot >> 1], 1u << (16 * (slot & 1)));  // ds_add_u32, no return
+}
+template <int H>
+__device__ __forceinline__ void bh_count_set1(BinHashSmem<H>& L, int slot) {
+  reinterpret_cast<uint16_t*>(L.cnt2)[slot] = 1;
+}
+template <int H>
+__device__ __forceinline__ uint32_t bh_count(const BinHashSmem<H>& L, int slot) {
+  return reinterpret_cast<const uint16_t*>(L.cnt2)[slot];
+}
+
+// Slow path of one update: the bin's home group is full of other bins, or
+// another lane of this step claimed the empty word first.  Continue the probe
+// sequence; returns false if the table is full.
+template <int H>
+__device__ __forceinline__ bool bh_slow_update(BinHashSmem<H>& L, uint32_t key, uint32_t g, double m, double it) {
+  constexpr uint32_t G = H / 4;
+  const uint32_t stride = bh_stride(key);
+#pragma unroll 1
+  for (int iter = 0; iter < BH_MAXITER; ++iter) {
+    const uint4 k4 = *reinterpret_cast<const uint4*>(&L.key[g * 4]);
+    bool hit;
+    const int e = bh_find4(k4, key, hit);
+    if (e < 0) {
+      g = (g + stride) & (G - 1);
+      continue;
+    }
+    const int slot = (int)g * 4 + e;
+    if (hit) {
+      const float2 a = L.u.acc[slot];
+      bh_count_add(L, slot);
+      L.u.acc[slot] = make_float2((float)((double)a.x + it), (float)((double)a.y + m));
+      return true;
+    }
+    if (atomicCAS(&L.key[slot], BH_EMPTY, key) == BH_EMPTY) {
+      bh_count_set1(L, slot);
+      L.u.acc[slot] = make_float2((float)(0.0 + it), (float)(0.0 + m));
+      return true;
+    }
+    // lost the claim: re-read the same group
+  }
+  return false;
+}
+
+template <int H>
+__global__ __launch_bounds__(BM_BLOCK) void bin_mean_hash_kernel(CsrView v, BinMeanParams P, PeaksOut out,
+                                                                 double* prec_out, int32_t* charge_out,
+                                                                 int32_t* status, int32_t* deferred,
+                                                                 int32_t* n_deferred) {
+  static_assert(sizeof(float2) * H >= sizeof(unsigned long long) * BM_WMAX + sizeof(uint16_t) * BM_WMAX,
+                "the ordering bitmap aliases the accumulators");
+  constexpr int SPT = H / BM_BLOCK;  // table slots per thread at the end
+  static_assert(SPT % 4 == 0, "whole key groups per thread");
+  static_assert(BH_PF + 1 <= kWave, "one lane per ring offset");
+  __shared__ BinHashSmem<H> L;
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const int64_t c = blockIdx.x;
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+  const int n = (int)(s1 - s0);
+  auto defer = [&]() {
+    if (tid == 0) {
+      status[c] = kDeferred;
+      deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    }
+  };
+  if (n == 0) {
+    if (tid == 0) { bl_finish_empty(out, prec_out, charge_out, c); status[c] = kEmpty; }
+    return;
+  }
+  if (n > BM_NMAX || P.n_words > BM_WMAX) { defer(); return; }
+  const int64_t p0 = v.spec_off[s0];
+  const double* __restrict__ mzc = v.mz + p0;
+  const double* __restrict__ itc = v.inten + p0;
+
+  // P0: offsets (padded with the end offset) and precursors to LDS, charge
+  // check (binning.py:205-206), empty table
+  const int32_t z0 = v.charge[s0];
+  int mixed = 0, longspec = 0;
+  // padded with the end offset up to n + 2 BH_PF: the ring reads the offsets of the turn after the last
+  for (int j = tid; j <= n + 2 * BH_PF; j += BM_BLOCK) L.soff[j] = (int32_t)(v.spec_off[s0 + (j < n ? j : n)] - p0);
+  for (int j = tid; j < n; j += BM_BLOCK) {
+    L.prec[j] = v.prec_mz[s0 + j];
+    mixed |= v.charge[s0 + j] != z0;
+    longspec |= v.spec_off[s0 + j + 1] - v.spec_off[s0 + j] > BH_CHUNK;
+  }
+#pragma unroll
+  for (int q = 0; q < SPT / 4; ++q)
+    reinterpret_cast<uint4*>(L.key)[tid + q * BM_BLOCK] = make_uint4(BH_EMPTY, BH_EMPTY, BH_EMPTY, BH_EMPTY);
+  if (block_any<BM_BLOCK, true>(mixed, L.votes, 0)) {
+    if (tid == 0) { bl_finish_empty(out, prec_out, charge_out, c); status[c] = kMixedCharge; }
+    return;
+  }
+  longspec = block_any<BM_BLOCK, true>(longspec, L.votes, 1);  // also: offsets and empty table visible
+
+  // P1: the ordered fold, one spectrum per step
+  const int t0 = (kWave - 1) * wid + lane;  // this lane's peak in a chunk
+  // a peak by cluster-relative index: 32-bit byte offsets from a scalar base
+  auto ld = [&](const double* base, int k) __attribute__((always_inline)) {
+    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + (uint32_t)k * 8u);
+  };
+  uint64_t badm = 0;  // lanes that saw a key inversion (wave mask)
+  // One lane's peak t of a spectrum of `len` peaks.  A NaN m/z gets key -1:
+  // excluded, as numpy's (mz >= min) & (mz < max) excludes it (binning.py:191-192);
+  // next to in-range peaks it reads as an inversion and defers the cluster.
+  auto peak = [&](int t, int len, double m, double it) __attribute__((always_inline)) {
+    const int32_t b = bin_small(m, P);
+    const int32_t key = !(m >= P.minimum) ? -1 : (m < P.maximum ? b : 0x7fffffff);
+    const int32_t kn = wave_next(key, 0x7fffffff);
+    const bool active = (t < len) & (lane < kWave - 1), has_next = t + 1 < len;
+    badm |= __ballot(active & has_next & (key > kn));
+    const bool part = active & !(has_next & (kn == key)) & ((uint32_t)key < 0x7fffffffu) & !(P.ablate & 16);
+    // probe the home group (every lane: harmless for non-participants)
+    const uint32_t uk = (uint32_t)key & 0x1FFFFu;
+    const uint32_t g = bh_home<H>(uk);
+    const uint4 k4 = *reinterpret_cast<const uint4*>(&L.key[g * 4]);
+    bool hit;
+    const int e = bh_find4(k4, uk, hit);
+    // one more round trip: the accumulators of the found slot and, for a new
+    // bin, the claim of the group's first empty word, in flight together
+    const int slot = (int)g * 4 + (e < 0 ? 0 : e);
+    const float2 a = L.u.acc[slot];  // speculative for non-hits
+    const bool ins = part & !hit & (e >= 0) & !(P.ablate & 4);
+    uint32_t old = 0u;
+    if (ins) old = atomicCAS(&L.key[slot], BH_EMPTY, uk);
+    const bool upd = part & hit & !(P.ablate & 8);
+    const bool fresh = ins & (old == BH_EMPTY);
+    if (upd) bh_count_add(L, slot);
+    if (fresh) bh_count_set1(L, slot);
+    if (upd | fresh) {
+      const float ax = fresh ? 0.0f : a.x, ay = fresh ? 0.0f : a.y;
+      L.u.acc[slot] = make_float2((float)((double)ax + it), (float)((double)ay + m));
+    }
+    if (part & !hit & !fresh & !(P.ablate & 4)) {
+      if (!bh_slow_update<H>(L, uk, g, m, it)) badm |= 1ull << lane;
+    }
+  };
+  const bool any_peaks = v.spec_off[s1] > p0;  // else nothing to fold (and no peak to clamp loads to)
+  if (!any_peaks) {
+  } else if (longspec) {
+    // a spectrum longer than a chunk: no ring (the extra chunks of a step
+    // would sit between the ring's loads and their uses)
+    for (int j = 0; j < n; ++j) {
+      const int a = __builtin_amdgcn_readfirstlane(L.soff[j]);
+      const int len = __builtin_amdgcn_readfirstlane(L.soff[j + 1]) - a;
+      for (int tb = 0; tb < len; tb += BH_CHUNK) {
+        const int t = tb + t0;
+        const int k = a + (t < len ? t : 0);
+        peak(t, len, ld(mzc, k), ld(itc, k));
+      }
+      lds_barrier();
+    }
+  } else {
+    // The ring.  Every refill is unconditional (past the last spectrum it
+    // reads one line), so no ring register is ever a merge of a load and
+    // another value: the compiler waits with a counted vmcnt and BH_PF
+    // spectra stay in flight across the LDS-only barriers.  The offsets of a
+    // ring turn are read once (lane i: offset jb + i) and handed out by readlane.
+    // The ring registers are defined in ONE place (the loop body; the first
+    // turn, jb = -BH_PF, only fills), so the allocator keeps each in one
+    // register pair with no copies at the loop header.
+    double Rm[BH_PF], Ri[BH_PF];
+    int Rl[BH_PF];
+    for (int jb = -BH_PF; jb < n; jb += BH_PF) {
+      const int offs = L.soff[jb + BH_PF + (lane < BH_PF + 1 ? lane : 0)];  // next turn's offsets (padded)
+#pragma unroll
+      for (int q = 0; q < BH_PF; ++q) {
+        const bool live = jb >= 0 && jb + q < n;  // uniform
+        if (live) peak(t0, Rl[q], Rm[q], Ri[q]);
+        const int a = __builtin_amdgcn_readlane(offs, q);
+        const int len = __builtin_amdgcn_readlane(offs, q + 1) - a;
+        const int k = len ? a + (t0 < len ? t0 : 0) : 0;
+        Rm[q] = ld(mzc, k);
+        Ri[q] = ld(itc, k);
+        Rl[q] = len;
+        if (live) lds_barrier();
+      }
+    }
+  }
+  if (block_any<BM_BLOCK, true>(badm != 0, L.votes, 0)) { defer(); return; }
+  if (P.ablate & 2) {
+    if (tid == 0) { out.count[c] = 0; status[c] = kOk; }
+    return;
+  }
+
+  // P2: kept slots (binning.py:209-222) into registers; thread owns SPT slots
+  const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
+  int32_t kk[SPT];
+  float ka[SPT], kb[SPT];
+  uint32_t kn[SPT];
+#pragma unroll
+  for (int q = 0; q < SPT; ++q) {
+    const int s = tid * SPT + q;
+    const uint32_t w = L.key[s];
+    const uint32_t cn = bh_count(L, s);
+    const float2 a = L.u.acc[s];
+    // cnt >= 1, so the mean is NaN iff the float32 sum is
+    const bool keep = w != BH_EMPTY && cn >= quorum && !isnan(a.x);
+    kk[q] = keep ? (int32_t)w : -1;
+    ka[q] = a.x;
+    kb[q] = a.y;
+    kn[q] = cn;
+  }
+  lds_barrier();  // accumulators dead: the bitmap takes their place
+  for (int w = tid; w < P.n_words; w += BM_BLOCK) L.u.b.bitmap[w] = 0ull;
+  lds_barrier();
+#pragma unroll
+  for (int q = 0; q < SPT; ++q)
+    if (kk[q] >= 0) atomicOr(&L.u.b.bitmap[kk[q] >> 6], 1ull << (kk[q] & 63));
+  lds_barrier();
+  const int K = bitmap_prefix<BM_BLOCK>(L.u.b.bitmap, L.u.b.wprefix, P.n_words, L.tmp);
+  if (!(P.ablate & 32)) {
+#pragma unroll
+    for (int q = 0; q < SPT; ++q) {
+      if (kk[q] >= 0) {
+        const int o = bitmap_rank(L.u.b.bitmap, L.u.b.wprefix, (int64_t)kk[q]);
+        const double cnd = (double)kn[q];
+        out.inten[p0 + o] = (double)ka[q] / cnd;
+        out.mz[p0 + o] = kb[q] == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)kb[q] / cnd;
+      }
+    }
+  }
+  if (tid == 0) {
+    out.count[c] = K;
+    charge_out[c] = z0;
+    prec_out[c] = pw_sum_small([&](int64_t j) { return L.prec[j]; }, n) / (double)n;  // np.mean (binning.py:224)
+    status[c] = kOk;
+  }
+}
+
 // Scratch slice of the deferred path, every array 256-B aligned.
 struct BinSliceLayout {
   int64_t bitmap, wprefix, cnt, acc_i, acc_m, owner, total;

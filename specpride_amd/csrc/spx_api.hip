@@ -134,7 +134,15 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
   if (hipMemsetAsync(n_def, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
-  if (bin_kernel_variant() == 2) {
+  if (bin_kernel_variant() == 3 || bin_kernel_variant() == 4) {
+    if (bin_kernel_variant() == 3)
+      hipLaunchKernelGGL(spx::bin_mean_hash_kernel<2048>, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O,
+                         prec_out, charge_out, status, def, n_def);
+    else
+      hipLaunchKernelGGL(spx::bin_mean_hash_kernel<4096>, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O,
+                         prec_out, charge_out, status, def, n_def);
+    if (int rc = check_launch("bin_mean_hash_kernel")) return rc;
+  } else if (bin_kernel_variant() == 2) {
     hipLaunchKernelGGL(spx::bin_mean_fold_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                        charge_out, status, def, n_def);
     if (int rc = check_launch("bin_mean_fold_kernel")) return rc;

@@ -229,7 +229,7 @@ def test_medoid_large_path_skewed_unsorted_and_empty(gpu):
     np.testing.assert_array_equal(tot, ref_tot)
 
 
-@pytest.mark.parametrize("variant", ["1", "2"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_bin_mean_kernel_variants(gpu, synth, monkeypatch, name, variant):
     """The per-bin list kernel (SPX_BIN_KERNEL=1) and the fold kernel (=2) meet

@@ -37,9 +37,10 @@ def main():
     # first int32 of each workspace = clusters deferred to the generic/large path
     res["bin_mean_deferred"] = int(b._ws["bin_mean"][:4].view(torch.int32).item())
     res["medoid_deferred"] = int(b._ws["medoid"][:4].view(torch.int32).item())
-    for var in ("0", "1", "2"):
+    for var in os.environ.get("SPX_VARIANTS", "0,1,2").split(","):
         os.environ["SPX_BIN_KERNEL"] = var
-        for mask in (0, 1, 2):
+        masks = (0, 1, 2) if var in ("0", "1", "2") else (0, 2, 4, 8, 12, 16)
+        for mask in masks:
             os.environ["SPX_ABLATE"] = str(mask)
             res[f"bin_mean_v{var}_ablate{mask}_ms"] = timed(lambda: engine.bin_mean(b, out=bm))
         os.environ["SPX_ABLATE"] = "0"
