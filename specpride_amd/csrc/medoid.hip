@@ -21,6 +21,8 @@
 // Large clusters (n > 64, or an LDS overflow) go to a deferred list and run
 // through medoid_build -> medoid_tile_scan -> medoid_gram -> medoid_totals with
 // state in a bump-allocated global scratch.
+#include <type_traits>
+
 #include "spx_device.hpp"
 
 namespace spx {
@@ -329,6 +331,328 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
     for (int i = 1; i < n; ++i)
       if (L.totals[i] < bt) { bt = L.totals[i]; best = i; }
     rep[c] = s0 + best;
+  }
+}
+
+// ------------------------------------------------- small clusters, v2 (default)
+// medoid_reg_kernel: the same algorithm as medoid_small_kernel with every m/z
+// read from HBM exactly ONCE (8 B per peak, the algorithmic minimum) and the
+// per-peak LDS traffic cut to two operations:
+//   P1  flat coalesced pass over the cluster's peaks (peak r = u*256 + tid,
+//       8 loads in flight per thread): absolute bin ceil(mz/tol) < 65,536, kept
+//       in registers as packed u16 (<= MR_UMAX per thread), union bitmap in LDS
+//       (32-bit LDS atomics).  The xcorr is a set intersection: no range pass,
+//       and unsorted spectra need no special path.
+//   P2  popcount prefix -> K compact columns; bitmap word and prefix share one
+//       16-byte record, so a rank is one ds_read_b128
+//   P3  bit-packed rows from the register bins: column = rank (one LDS read),
+//       spectrum = the wave's start-bit word and its prefix, handed out by
+//       readlane (a wave's 64 peaks of a slice are one start-bit word); rows
+//       are set by 32-bit LDS atomics (neighbouring peaks share a row word)
+//   P4  one thread per pair i <= j: c_ij = popcount(row_i & row_j) into
+//       registers, then d_ij = 1 - c_ij/min(p_i, p_j) (one IEEE divide per pair)
+//       into the reference's n x n matrix (upper triangle incl. the diagonal,
+//       zeros below: most_similar_representative.py:91-93), aliasing the dead
+//       bitmap and rows
+//   P5  totals with numpy's pairwise tree (:98-100): 16 lanes per spectrum --
+//       8 accumulators of row i, 8 of column i -- combined
+//       ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) by shuffles, sequential tail,
+//       total = (row + col)/n
+//   P6  lowest index of the minimum (:103-110), one wave
+// Deferred to the large path: n > 64, > MR_UMAX*256 peaks, a bin outside
+// [0, 65,536), > 1,984 distinct bins.
+constexpr int MR_UMAX = 48;                  // peaks per thread (12,288 per cluster)
+constexpr int MR_PMAX = MR_UMAX * MD_BLOCK;
+constexpr int MR_MS = MD_NMAX + 1;           // max row stride of the distance matrix (odd)
+
+struct MrRec {
+  unsigned long long bits;
+  uint32_t pre, pad;
+};
+
+struct MedoidRegSmem {
+  union {
+    struct {
+      MrRec rec[MD_WMAX];                        // occupancy word + exclusive popcount prefix
+      unsigned long long rows[MD_NMAX * MD_KWMAX];
+      unsigned long long sbits[MR_PMAX / 64];    // bit r: peak r starts spectrum >= 1
+      uint8_t spre[MR_PMAX / 64];                // spectra started before word w
+    } a;                                         // P0..P4a
+    double d[MD_NMAX * MR_MS];                   // P4b..P5
+  } u;
+  int32_t soff[MD_NMAX + 1];
+  double totals[MD_NMAX];
+  int tmp[MD_BLOCK / kWave + 1];
+  long long red[4];
+};
+
+__global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
+                                                              double* totals_out, int32_t* deferred,
+                                                              int32_t* n_deferred, MedoidMeta* meta) {
+  __shared__ MedoidRegSmem L;
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const int64_t c = blockIdx.x;
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+  const int n = (int)(s1 - s0);
+  if (s1 - s0 > MD_NMAX) {
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
+    return;
+  }
+  if (n <= 1) {
+    if (tid == 0) {
+      rep[c] = n == 1 ? s0 : -1;
+      if (totals_out && n == 1) totals_out[s0] = 0.0;
+    }
+    return;
+  }
+  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
+  const int np = (int)(p1 - p0);
+  if (p1 - p0 > MR_PMAX) {
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
+    return;
+  }
+  const double* __restrict__ mzc = v.mz + p0;
+
+  // P0: offsets, spectrum start bits, empty bitmap.  Bins are absolute
+  // ceil(mz/tol) in [0, 65,536) (m/z < 6,553.6 at tol 0.1): the xcorr is a set
+  // intersection, so neither a range pass nor sorted spectra are needed.
+  const int nsw = (np + 63) / 64;
+  for (int w = tid; w < nsw; w += MD_BLOCK) L.u.a.sbits[w] = 0ull;
+  if (tid <= n) L.soff[tid] = (int32_t)(v.spec_off[s0 + tid] - p0);
+  for (int w = tid; w < MD_WMAX; w += MD_BLOCK) L.u.a.rec[w].bits = 0ull;
+  if (tid == 0) L.red[0] = 0;
+  __syncthreads();
+  if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
+    const bool empty_spec = tid < n && L.soff[tid + 1] == L.soff[tid];
+    if (tid == 0) L.red[1] = __ballot(empty_spec) != 0ull;
+  }
+  for (int j = 1 + tid; j < n; j += MD_BLOCK) {
+    const int r = L.soff[j];
+    if (r < np) atomicOr(&L.u.a.sbits[r >> 6], 1ull << (r & 63));
+  }
+  __syncthreads();
+  const bool has_empty = L.red[1] != 0;
+  if (tid < kWave) {  // prefix of start bits (<= 192 words, one wave)
+    int carry = 0;
+    for (int w0 = 0; w0 < nsw; w0 += kWave) {
+      const int w = w0 + tid;
+      const int c1 = w < nsw ? __popcll(L.u.a.sbits[w]) : 0;
+      const int inc = wave_inclusive_sum(c1);
+      if (w < nsw) L.u.a.spre[w] = (uint8_t)(carry + inc - c1);
+      carry += __shfl(inc, kWave - 1, kWave);
+    }
+  }
+
+  if (P.ablate & 1024) { if (tid == 0) rep[c] = s0; return; }  // profiling: P0 only
+  // P1: one read of every m/z; bins packed two per register.  Batches of 8
+  // loads per thread, double-buffered (batch b+1 in flight while b is binned).
+  // The batch count is a compile-time constant per size class, so every load
+  // is unconditional: no ring register is ever a merge of a load and another
+  // value, and the compiler waits with counted vmcnt.
+  uint32_t bins[MR_UMAX / 2];
+  int outside = 0;
+  uint32_t bmax = 0u;
+  constexpr uint32_t kBins = (uint32_t)MD_WMAX * 64u;
+  constexpr int NB = MR_UMAX / 8;
+  auto pass1 = [&](auto nbt_c) __attribute__((always_inline)) {
+    constexpr int NBT = decltype(nbt_c)::value;
+    double mb[2][8];
+#pragma unroll
+    for (int bt = 0; bt <= NBT; ++bt) {
+      if (bt < NBT) {  // issue batch bt
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = (bt * 8 + q) * MD_BLOCK + tid;
+          mb[bt & 1][q] = mzc[r < np ? r : 0];
+        }
+      }
+      if (bt > 0) {  // bin batch bt - 1
+        const int pb = bt - 1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int u = pb * 8 + q;
+          const int r = u * MD_BLOCK + tid;
+          uint32_t b = 0u;
+          if (r < np) {
+            const int64_t bb = md_bin(mb[pb & 1][q], P);
+            if (bb < 0 || bb >= (int64_t)kBins) {
+              outside = 1;
+            } else {
+              b = (uint32_t)bb;
+              bmax = b > bmax ? b : bmax;
+              // 32-bit half of the occupancy word (same-address LDS atomics serialise)
+              if (!(P.ablate & 2048))
+                atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rec[b >> 6].bits) + ((b >> 5) & 1), 1u << (b & 31));
+            }
+          }
+          if (u & 1) bins[u >> 1] |= b << 16;
+          else bins[u >> 1] = b;
+        }
+      }
+    }
+  };
+  switch ((np + 8 * MD_BLOCK - 1) / (8 * MD_BLOCK)) {  // uniform size class
+    case 0: break;
+    case 1: pass1(std::integral_constant<int, 1>{}); break;
+    case 2: pass1(std::integral_constant<int, 2>{}); break;
+    case 3: pass1(std::integral_constant<int, 3>{}); break;
+    case 4: pass1(std::integral_constant<int, 4>{}); break;
+    case 5: pass1(std::integral_constant<int, 5>{}); break;
+    default: pass1(std::integral_constant<int, NB>{}); break;
+  }
+  static_assert(NB == 6, "size classes above cover MR_UMAX = 48");
+  if (bmax) atomicMax(reinterpret_cast<int*>(&L.red[0]), (int)bmax);
+  if (__syncthreads_or(outside)) {  // m/z out of the LDS bitmap's range: general path
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
+    return;
+  }
+  const int nw = np > 0 ? (int)(L.red[0] >> 6) + 1 : 0;
+  if (P.ablate & 4096) { if (tid == 0) rep[c] = s0 + (bins[0] & 1); return; }  // profiling: P0 + P1
+  // P2: compact columns (exclusive popcount prefix into the records)
+  int K;
+  {
+    const int per = (nw + MD_BLOCK - 1) / MD_BLOCK, w0 = tid * per;
+    int local = 0;
+    for (int k = 0; k < per; ++k)
+      if (w0 + k < nw) local += __popcll(L.u.a.rec[w0 + k].bits);
+    int base = block_exclusive_scan<MD_BLOCK>(local, L.tmp, K);
+    for (int k = 0; k < per; ++k) {
+      if (w0 + k < nw) {
+        L.u.a.rec[w0 + k].pre = (uint32_t)base;
+        base += __popcll(L.u.a.rec[w0 + k].bits);
+      }
+    }
+  }
+  // row stride KW is odd: lanes reading rows j, j+1, ... at one word hit
+  // different LDS banks (an even stride of u64s would fold them together)
+  const int KW = ((K + 63) / 64) | 1;
+  if (KW > MD_KWMAX) {
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
+    return;
+  }
+  // P3: bit-packed rows from the register bins
+  for (int w = tid; w < n * KW; w += MD_BLOCK) L.u.a.rows[w] = 0ull;
+  // start-bit word 4u + wid and its prefix for slice u, lane u holds them
+  unsigned long long my_sw = 0ull;
+  int my_sp = 0;
+  {
+    const int w = 4 * lane + wid;
+    if (lane < MR_UMAX && w < nsw) { my_sw = L.u.a.sbits[w]; my_sp = L.u.a.spre[w]; }
+  }
+  __syncthreads();
+  if (P.ablate & 16) { if (tid == 0) rep[c] = s0; return; }
+  const unsigned long long upto = (2ull << lane) - 1ull;  // bits 0..lane
+#pragma unroll
+  for (int u = 0; u < MR_UMAX; ++u) {
+    if (u * MD_BLOCK < np) {  // uniform
+      const int r = u * MD_BLOCK + tid;
+      const uint32_t swlo = __builtin_amdgcn_readlane((uint32_t)my_sw, u);
+      const uint32_t swhi = __builtin_amdgcn_readlane((uint32_t)(my_sw >> 32), u);
+      const int spw = __builtin_amdgcn_readlane(my_sp, u);
+      if (r < np) {
+        const uint32_t b = (bins[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+        const MrRec R = L.u.a.rec[b >> 6];
+        const int col = (int)R.pre + __popcll(R.bits & ((1ull << (b & 63)) - 1ull));
+        // empty spectra share a start bit: then the binary search
+        const unsigned long long sw = ((unsigned long long)swhi << 32) | swlo;
+        const int sp = has_empty ? spectrum_of(L.soff, n, r) : spw + __popcll(sw & upto);
+        if (P.ablate & 128) {  // profiling: no row update
+          if (col < 0) L.u.a.rows[0] = 1ull;
+        } else if (P.ablate & 256) {  // profiling: conflict-free addresses
+          atomicOr(&L.u.a.rows[(tid + (sp * KW + (col >> 6)) * 0) % (n * KW)], 1ull << (col & 63));
+        } else {
+          // 32-bit halves: consecutive peaks of a spectrum share a row word, and
+          // same-address LDS atomics serialise -- half as many per address
+          atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[sp * KW]) + (col >> 5), 1u << (col & 31));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (P.ablate & 64) { if (tid == 0) rep[c] = s0; return; }
+
+  // P4: every pair i <= j of the row-major upper triangle (row i starts at
+  // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
+  // registers until the rows are dead
+  constexpr int PPT = (MD_NMAX * (MD_NMAX + 1) / 2 + MD_BLOCK - 1) / MD_BLOCK;  // pairs per thread (9)
+  const int NP = n * (n + 1) / 2;
+  auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
+  uint32_t pc[PPT];
+  int pij[PPT];
+#pragma unroll
+  for (int q = 0; q < PPT; ++q) {
+    const int p = tid + q * MD_BLOCK;
+    pc[q] = 0u;
+    pij[q] = -1;
+    if (p < NP) {
+      const float b2 = 2.0f * n + 1.0f;
+      int i = (int)((b2 - sqrtf(b2 * b2 - 8.0f * (float)p)) * 0.5f);
+      i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+      while (i > 0 && row_start(i) > p) --i;
+      while (i + 1 < n && row_start(i + 1) <= p) ++i;
+      const int j = i + (p - row_start(i));
+      uint32_t cnt = 0;
+      for (int w = 0; w < KW; ++w) cnt += (uint32_t)__popcll(L.u.a.rows[i * KW + w] & L.u.a.rows[j * KW + w]);
+      pc[q] = cnt;
+      pij[q] = i << 8 | j;
+    }
+  }
+  __syncthreads();  // rows dead: the distance matrix takes their place
+  const int ms = n | 1;  // odd row stride (conflict-free column reads)
+#pragma unroll
+  for (int q = 0; q < PPT; ++q) {
+    if (pij[q] >= 0) {
+      const int i = pij[q] >> 8, j = pij[q] & 0xff;
+      L.u.d[i * ms + j] = md_dist(pc[q], L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
+      if (j != i) L.u.d[j * ms + i] = 0.0;  // the reference's lower triangle stays 0
+    }
+  }
+  __syncthreads();
+  if (P.ablate & 32) { if (tid == 0) rep[c] = s0; return; }
+
+  // P5: totals, 16 lanes per spectrum (8 row accumulators, 8 column ones)
+  const int k = lane & 7;
+  const bool colside = (lane & 8) != 0;
+  const int lim = n - (n % 8);
+  for (int i0 = 0; i0 < n; i0 += MD_BLOCK / 16) {  // uniform
+    const int i = i0 + tid / 16;
+    const bool valid = i < n;
+    const int ii = valid ? i : 0;
+    // row ii (stride 1 from ii*ms) or column ii (stride ms from ii)
+    const double* e = L.u.d + (colside ? ii : ii * ms);
+    const int st = colside ? ms : 1;
+    double s = 0.0;
+    if (n >= 8) {
+      double r = e[k * st];
+      for (int j = 8 + k; j < lim; j += 8) r += e[j * st];
+      r += __shfl_xor(r, 1, kWave);
+      r += __shfl_xor(r, 2, kWave);
+      r += __shfl_xor(r, 4, kWave);  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+      s = r;
+      for (int j = lim; j < n; ++j) s += e[j * st];  // the sequential tail
+    } else {
+      for (int j = 0; j < n; ++j) s += e[j * st];  // 0.0 + a0 + a1 + ...
+    }
+    s = 0.0 + s;
+    const double other = __shfl_xor(s, 8, kWave);
+    if (valid && (lane & 15) == 0) {
+      const double t = (s + other) / (double)n;  // (row + col) / n
+      L.totals[i] = t;
+      if (totals_out) totals_out[s0 + i] = t;
+    }
+  }
+  __syncthreads();
+  // P6: first index of the minimum (:103-110)
+  if (tid < kWave) {
+    double t = tid < n ? L.totals[tid] : __longlong_as_double(0x7ff0000000000000ll);
+    int idx = tid < n ? tid : 0x7fffffff;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const double t2 = __shfl_xor(t, o, kWave);
+      const int i2 = __shfl_xor(idx, o, kWave);
+      if (t2 < t || (t2 == t && i2 < idx)) { t = t2; idx = i2; }
+    }
+    if (tid == 0) rep[c] = s0 + idx;
   }
 }
 

@@ -77,6 +77,13 @@ int bin_kernel_variant() {
   return e ? std::atoi(e) : 0;
 }
 
+// Small-cluster medoid kernel: 0 = medoid_reg_kernel (one m/z read, default),
+// 1 = medoid_small_kernel (two reads).  SPX_MEDOID_KERNEL selects (A/B profiling).
+int medoid_kernel_variant() {
+  const char* e = std::getenv("SPX_MEDOID_KERNEL");
+  return e ? std::atoi(e) : 0;
+}
+
 int32_t bin_words(const spx_bin_params* p) {
   const double nb = std::trunc((p->maximum - p->minimum) / p->binsize) + 1.0;  // binning.py:172
   return (int32_t)((nb + 63.0) / 64.0);
@@ -264,11 +271,16 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance, ablate_mask()};
   const spx::CsrView V = view(csr);
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024));
-  const dim3 grid2(spx::MD_GRIDX, g), blk(spx::MD_BLOCK);
+  // grid-stride passes: 32 deferred clusters at a time x 64 blocks fills the chip,
+  // and an empty deferred list (the common case) costs a small launch
+  const dim3 grid2(spx::MD_GRIDX, std::min<unsigned>(g, 32u)), blk(spx::MD_BLOCK);
 
   if (hipMemsetAsync(n_def, 0, 512, s) != hipSuccess) return check_launch("spx_medoid memset");
-  hipLaunchKernelGGL(spx::medoid_small_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, def, n_def, meta);
-  if (int rc = check_launch("medoid_small_kernel")) return rc;
+  if (medoid_kernel_variant() == 1)
+    hipLaunchKernelGGL(spx::medoid_small_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, def, n_def, meta);
+  else
+    hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, def, n_def, meta);
+  if (int rc = check_launch("medoid small-cluster kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_range_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena, bump, arena_bytes);
   if (int rc = check_launch("medoid_range_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_l1_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena);

@@ -126,7 +126,10 @@ def test_gap_average_synthetic_vs_oracle(gpu, synth):
     assert_gap_close(got, np_oracle.gap_average(sub), 1000.0)
 
 
-def test_medoid_synthetic_vs_oracle(gpu, synth):
+@pytest.mark.parametrize("variant", ["0", "1"])
+def test_medoid_synthetic_vs_oracle(gpu, synth, monkeypatch, variant):
+    """Default single-read kernel (SPX_MEDOID_KERNEL=0) and the two-read v1 kernel (=1)."""
+    monkeypatch.setenv("SPX_MEDOID_KERNEL", variant)
     rep, tot = engine.medoid(engine.DeviceBatch.from_host(synth), with_totals=True).to_host()
     ref_rep, ref_tot = c_oracle.medoid(synth, with_totals=True)
     np.testing.assert_array_equal(rep, ref_rep)

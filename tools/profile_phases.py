@@ -50,7 +50,7 @@ def main():
         torch.cuda.synchronize()
         res[f"bin_mean_v{var}_deferred"] = int(b._ws["bin_mean"][:4].view(torch.int32).item())
     os.environ["SPX_BIN_KERNEL"] = "0"
-    for mask in (0, 16, 64, 32):
+    for mask in (0, 16, 64, 32, 64 | 128, 64 | 256, 1024, 4096, 4096 | 2048):
         os.environ["SPX_ABLATE"] = str(mask)
         res[f"medoid_ablate{mask}_ms"] = timed(lambda: engine.medoid(b, out=md))
     os.environ["SPX_ABLATE"] = "0"
