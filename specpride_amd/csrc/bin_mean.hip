@@ -1009,24 +1009,25 @@ __device__ __forceinline__ int bh_find4(const uint4& k, uint32_t key, bool& hit)
   return s0 ? 0 : s1 ? 1 : s2 ? 2 : s3 ? 3 : -1;
 }
 
-template <int H>
-__device__ __forceinline__ void bh_count_add(BinHashSmem<H>& L, int slot) {
+// (S: any LDS layout with members key[H], cnt2[H/2] and u.acc[H])
+template <class S>
+__device__ __forceinline__ void bh_count_add(S& L, int slot) {
   atomicAdd(&L.cnt2[slot >> 1], 1u << (16 * (slot & 1)));  // ds_add_u32, no return
 }
-template <int H>
-__device__ __forceinline__ void bh_count_set1(BinHashSmem<H>& L, int slot) {
+template <class S>
+__device__ __forceinline__ void bh_count_set1(S& L, int slot) {
   reinterpret_cast<uint16_t*>(L.cnt2)[slot] = 1;
 }
-template <int H>
-__device__ __forceinline__ uint32_t bh_count(const BinHashSmem<H>& L, int slot) {
+template <class S>
+__device__ __forceinline__ uint32_t bh_count(const S& L, int slot) {
   return reinterpret_cast<const uint16_t*>(L.cnt2)[slot];
 }
 
 // Slow path of one update: the bin's home group is full of other bins, or
 // another lane of this step claimed the empty word first.  Continue the probe
 // sequence; returns false if the table is full.
-template <int H>
-__device__ __forceinline__ bool bh_slow_update(BinHashSmem<H>& L, uint32_t key, uint32_t g, double m, double it) {
+template <int H, class S>
+__device__ __forceinline__ bool bh_slow_update(S& L, uint32_t key, uint32_t g, double m, double it) {
   constexpr uint32_t G = H / 4;
   const uint32_t stride = bh_stride(key);
 #pragma unroll 1
@@ -1053,6 +1054,46 @@ __device__ __forceinline__ bool bh_slow_update(BinHashSmem<H>& L, uint32_t key, 
     // lost the claim: re-read the same group
   }
   return false;
+}
+
+// One lane's peak t of a spectrum of `len` peaks, one fold step (see
+// bin_mean_hash_kernel).  A NaN m/z gets key -1: excluded, as numpy's
+// (mz >= min) & (mz < max) excludes it (binning.py:191-192); next to in-range
+// peaks it reads as an inversion and defers the cluster.  badm collects (per
+// wave) lanes that saw a key inversion or a full table.
+template <int H, class S>
+__device__ __forceinline__ void bh_fold_peak(S& L, const BinMeanParams& P, int lane, int t, int len,
+                                             double m, double it, uint64_t& badm) {
+  const int32_t b = bin_small(m, P);
+  const int32_t key = !(m >= P.minimum) ? -1 : (m < P.maximum ? b : 0x7fffffff);
+  const int32_t kn = wave_next(key, 0x7fffffff);
+  const bool active = (t < len) & (lane < kWave - 1), has_next = t + 1 < len;
+  badm |= __ballot(active & has_next & (key > kn));
+  const bool part = active & !(has_next & (kn == key)) & ((uint32_t)key < 0x7fffffffu) & !(P.ablate & 16);
+  // probe the home group (every lane: harmless for non-participants)
+  const uint32_t uk = (uint32_t)key & 0x1FFFFu;
+  const uint32_t g = bh_home<H>(uk);
+  const uint4 k4 = *reinterpret_cast<const uint4*>(&L.key[g * 4]);
+  bool hit;
+  const int e = bh_find4(k4, uk, hit);
+  // one more round trip: the accumulators of the found slot and, for a new
+  // bin, the claim of the group's first empty word, in flight together
+  const int slot = (int)g * 4 + (e < 0 ? 0 : e);
+  const float2 a = L.u.acc[slot];  // speculative for non-hits
+  const bool ins = part & !hit & (e >= 0) & !(P.ablate & 4);
+  uint32_t old = 0u;
+  if (ins) old = atomicCAS(&L.key[slot], BH_EMPTY, uk);
+  const bool upd = part & hit & !(P.ablate & 8);
+  const bool fresh = ins & (old == BH_EMPTY);
+  if (upd) bh_count_add(L, slot);
+  if (fresh) bh_count_set1(L, slot);
+  if (upd | fresh) {
+    const float ax = fresh ? 0.0f : a.x, ay = fresh ? 0.0f : a.y;
+    L.u.acc[slot] = make_float2((float)((double)ax + it), (float)((double)ay + m));
+  }
+  if (part & !hit & !fresh & !(P.ablate & 4)) {
+    if (!bh_slow_update<H>(L, uk, g, m, it)) badm |= 1ull << lane;
+  }
 }
 
 template <int H>
@@ -1112,40 +1153,8 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_hash_kernel(CsrView v, BinM
     return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + (uint32_t)k * 8u);
   };
   uint64_t badm = 0;  // lanes that saw a key inversion (wave mask)
-  // One lane's peak t of a spectrum of `len` peaks.  A NaN m/z gets key -1:
-  // excluded, as numpy's (mz >= min) & (mz < max) excludes it (binning.py:191-192);
-  // next to in-range peaks it reads as an inversion and defers the cluster.
   auto peak = [&](int t, int len, double m, double it) __attribute__((always_inline)) {
-    const int32_t b = bin_small(m, P);
-    const int32_t key = !(m >= P.minimum) ? -1 : (m < P.maximum ? b : 0x7fffffff);
-    const int32_t kn = wave_next(key, 0x7fffffff);
-    const bool active = (t < len) & (lane < kWave - 1), has_next = t + 1 < len;
-    badm |= __ballot(active & has_next & (key > kn));
-    const bool part = active & !(has_next & (kn == key)) & ((uint32_t)key < 0x7fffffffu) & !(P.ablate & 16);
-    // probe the home group (every lane: harmless for non-participants)
-    const uint32_t uk = (uint32_t)key & 0x1FFFFu;
-    const uint32_t g = bh_home<H>(uk);
-    const uint4 k4 = *reinterpret_cast<const uint4*>(&L.key[g * 4]);
-    bool hit;
-    const int e = bh_find4(k4, uk, hit);
-    // one more round trip: the accumulators of the found slot and, for a new
-    // bin, the claim of the group's first empty word, in flight together
-    const int slot = (int)g * 4 + (e < 0 ? 0 : e);
-    const float2 a = L.u.acc[slot];  // speculative for non-hits
-    const bool ins = part & !hit & (e >= 0) & !(P.ablate & 4);
-    uint32_t old = 0u;
-    if (ins) old = atomicCAS(&L.key[slot], BH_EMPTY, uk);
-    const bool upd = part & hit & !(P.ablate & 8);
-    const bool fresh = ins & (old == BH_EMPTY);
-    if (upd) bh_count_add(L, slot);
-    if (fresh) bh_count_set1(L, slot);
-    if (upd | fresh) {
-      const float ax = fresh ? 0.0f : a.x, ay = fresh ? 0.0f : a.y;
-      L.u.acc[slot] = make_float2((float)((double)ax + it), (float)((double)ay + m));
-    }
-    if (part & !hit & !fresh & !(P.ablate & 4)) {
-      if (!bh_slow_update<H>(L, uk, g, m, it)) badm |= 1ull << lane;
-    }
+    bh_fold_peak<H>(L, P, lane, t, len, m, it, badm);
   };
   const bool any_peaks = v.spec_off[s1] > p0;  // else nothing to fold (and no peak to clamp loads to)
   if (!any_peaks) {

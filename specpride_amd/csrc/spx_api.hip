@@ -14,7 +14,7 @@
 #include <cstring>
 
 #include "../../include/specpride.h"
-#include "bin_mean.hip"
+#include "bin_mean_stream.hip"  // includes bin_mean.hip
 #include "gap_average.hip"
 #include "medoid.hip"
 
@@ -70,11 +70,24 @@ int32_t ablate_mask() {
   return e ? (int32_t)std::atoi(e) : 0;
 }
 
-// Per-cluster bin-mean kernel: 0 = spectrum-serial LDS kernel (default),
-// 1 = per-bin list kernel, 2 = fold kernel.  SPX_BIN_KERNEL selects (A/B profiling).
+// Bin-mean kernel: 0 = per-cluster two-pass LDS kernel (default, fastest
+// measured), 1 = per-bin list kernel, 2 = fold kernel, 3/4 = per-cluster hash
+// kernel (2048/4096 slots), 5 = persistent stream + hash fold, 6 = persistent
+// stream + bitmap-rank fold (DESIGN.md §3 has the measurements).
+// SPX_BIN_KERNEL selects (A/B profiling).
 int bin_kernel_variant() {
   const char* e = std::getenv("SPX_BIN_KERNEL");
   return e ? std::atoi(e) : 0;
+}
+
+// Workgroups of the persistent bin-mean kernel: BS_BLOCKS_PER_CU per CU (its
+// LDS and VGPR budgets admit exactly that many), never more than clusters.
+int64_t stream_grid(int64_t C) {
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                               hipSuccess || ncu <= 0)
+    ncu = 256;
+  return std::max<int64_t>(1, std::min<int64_t>({C, (int64_t)ncu * spx::BS_BLOCKS_PER_CU, spx::BS_PLAN_MAX}));
 }
 
 // Small-cluster medoid kernel: 0 = medoid_reg_kernel (one m/z read, default),
@@ -107,6 +120,7 @@ size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* par
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   return align256(sizeof(int32_t)) + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
+         align256(sizeof(int32_t) * (spx::BS_PLAN_MAX + 1)) +
          (size_t)fallback_grid(C) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
@@ -126,6 +140,7 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
   int32_t* n_def = w.take<int32_t>(1);
   int32_t* def = w.take<int32_t>((size_t)C);
+  int32_t* plan = w.take<int32_t>(spx::BS_PLAN_MAX + 1);
   char* scratch = w.base + w.used;
 
   spx::BinMeanParams P;
@@ -141,7 +156,24 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
   if (hipMemsetAsync(n_def, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
-  if (bin_kernel_variant() == 3 || bin_kernel_variant() == 4) {
+  const int64_t G = stream_grid(C);
+  // the stream kernel addresses a workgroup's range with 32-bit offsets: bound
+  // the range (weight / G + one cluster) well below 2^28 peaks
+  const int64_t wtot = csr->n_peaks + 64 * csr->n_spectra + 1024 * C;
+  const bool range_ok = wtot / G + info->max_cluster_peaks + 64 * info->max_cluster_spectra + 1024 < (int64_t(1) << 28);
+  const int bv = bin_kernel_variant();
+  if ((bv == 5 || bv == 6) && P.n_words <= spx::BM_WMAX && range_ok) {
+    const unsigned pg = (unsigned)std::min<int64_t>((C + 1 + 255) / 256, 1024);
+    hipLaunchKernelGGL(spx::range_plan_kernel, dim3(pg), dim3(256), 0, s, V, (int32_t)G, plan);
+    if (int rc = check_launch("range_plan_kernel")) return rc;
+    if (bv == 6)
+      hipLaunchKernelGGL(spx::bin_mean_stream2_kernel, dim3((unsigned)G), dim3(spx::BM_BLOCK), 0, s, V, P, O,
+                         prec_out, charge_out, status, def, n_def, plan);
+    else
+      hipLaunchKernelGGL(spx::bin_mean_stream_kernel<spx::BS_H>, dim3((unsigned)G), dim3(spx::BM_BLOCK), 0, s, V, P,
+                         O, prec_out, charge_out, status, def, n_def, plan);
+    if (int rc = check_launch("bin_mean_stream_kernel")) return rc;
+  } else if (bin_kernel_variant() == 3 || bin_kernel_variant() == 4) {
     if (bin_kernel_variant() == 3)
       hipLaunchKernelGGL(spx::bin_mean_hash_kernel<2048>, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O,
                          prec_out, charge_out, status, def, n_def);

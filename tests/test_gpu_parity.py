@@ -232,7 +232,7 @@ def test_medoid_large_path_skewed_unsorted_and_empty(gpu):
     np.testing.assert_array_equal(tot, ref_tot)
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6"])
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_bin_mean_kernel_variants(gpu, synth, monkeypatch, name, variant):
     """The per-bin list kernel (SPX_BIN_KERNEL=1) and the fold kernel (=2) meet
@@ -246,3 +246,55 @@ def test_bin_mean_kernel_variants(gpu, synth, monkeypatch, name, variant):
         assert_bin_mean_equal(_bin_mean(synth), c_oracle.bin_mean(synth))
         sub = _shuffled(synth.select(range(200)))
         assert_bin_mean_equal(_bin_mean(sub), c_oracle.bin_mean(sub))
+
+
+def _concat(*parts):
+    """Concatenate SpectraCSR batches (cluster order kept)."""
+    co, so, n_s, n_p = [np.zeros(1, np.int64)], [np.zeros(1, np.int64)], 0, 0
+    for p in parts:
+        co.append(p.cluster_off[1:] + n_s)
+        so.append(p.spec_off[1:] + n_p)
+        n_s += p.n_spectra
+        n_p += p.n_peaks
+    cat = lambda k: np.concatenate([getattr(p, k) for p in parts])  # noqa: E731
+    return SpectraCSR(np.concatenate(co), np.concatenate(so), cat("mz"), cat("inten"), cat("prec_mz"),
+                      cat("charge"), cat("rt"))
+
+
+@pytest.mark.parametrize("variant", ["5", "6"])
+def test_bin_mean_stream_many_clusters_per_workgroup(gpu, monkeypatch, variant):
+    """The persistent streaming kernels (hash fold = 5, bitmap-rank fold = 6): far more clusters than
+    workgroups, so every workgroup folds a long range -- with empty clusters,
+    empty spectra, mixed charges, a spectrum longer than one step (252 peaks),
+    an unsorted spectrum and a > 128-spectrum cluster scattered through it."""
+    monkeypatch.setenv("SPX_BIN_KERNEL", variant)
+    rng = np.random.default_rng(21)
+    base = make_clusters_np(7000, seed=8, min_size=1, max_size=12, n_template=60)
+    co = base.cluster_off.copy()
+    # empty clusters: repeat some boundaries
+    co = np.sort(np.concatenate([co, rng.choice(co[1:-1], 300)]))
+    ch = base.charge.copy()
+    for c in rng.choice(len(co) - 1, 40, replace=False):  # mixed charges
+        a, b = co[c], co[c + 1]
+        if b - a >= 2:
+            ch[b - 1] = ch[a] + 1
+    body = SpectraCSR(co, base.spec_off, base.mz, base.inten, base.prec_mz, ch, base.rt)
+
+    def spec(k, sort=True):
+        m = np.round(rng.uniform(100.0, 2000.0, k), 5)
+        return {"m/z array": np.sort(m) if sort else m, "intensity array": np.round(rng.lognormal(5, 1.5, k), 2),
+                "precursor mz": 600.0, "precursor charge": 2}
+
+    special = SpectraCSR.from_clusters([
+        [spec(300), spec(200), spec(280)],                  # longer than a step
+        [spec(50), {"m/z array": [], "intensity array": [], "precursor mz": 600.0, "precursor charge": 2},
+         spec(40)],                                         # an empty spectrum
+        [spec(30, sort=False), spec(30)],                   # unsorted
+        [spec(20) for _ in range(140)],                     # > 128 spectra
+        [],
+    ])
+    parts = [body.select(range(0, 3000)), special, body.select(range(3000, 5000)), special,
+             body.select(range(5000, body.n_clusters))]
+    csr = _concat(*parts)
+    assert csr.n_clusters > 5 * 1280
+    assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))

@@ -37,6 +37,24 @@ def main():
         ms = e0.elapsed_time(e1) / 10
         nbytes = t["n_peaks"] * (8 if kind == 4 else 16)
         res[name] = {"ms": round(ms, 4), "GBs": round(nbytes / ms / 1e6, 1)}
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    for kind, name in ((5, "pers_range"), (6, "pers_rr"), (7, "cl_ring_lds")):
+        def go2():
+            rc = lib.stream_shape2(kind, ctypes.c_void_p(t["cluster_off"].data_ptr()),
+                                   ctypes.c_void_p(t["spec_off"].data_ptr()), ctypes.c_void_p(t["mz"].data_ptr()),
+                                   ctypes.c_void_p(t["inten"].data_ptr()), ctypes.c_int64(t["n_clusters"]),
+                                   ctypes.c_int(5 * ncu), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(st))
+            assert rc == 0
+        go2()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            go2()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 10
+        res[name] = {"ms": round(ms, 4), "GBs": round(t["n_peaks"] * 16 / ms / 1e6, 1)}
     print(json.dumps(res))
 
 

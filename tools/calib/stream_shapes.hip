@@ -108,3 +108,86 @@ extern "C" int stream_shape(int kind, const void* coff, const void* soff, const 
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// ---- persistent shapes (the stream kernel's access pattern, no fold) ----
+//   5 pers_range   workgroup b reads clusters [b*C/G, (b+1)*C/G) as one spectrum stream
+//   6 pers_rr      workgroup b reads clusters b, b+G, b+2G, ...
+//   7 cl_ring_lds  as 2, but 30 KB of LDS per workgroup (5 per CU, like the fold)
+// All with a 7-deep ring and an LDS-only barrier per spectrum; G = 5 per CU.
+template <int PF>
+__device__ __forceinline__ unsigned long long ring_clusters(const int64_t* __restrict__ coff,
+                                                            const int64_t* __restrict__ soff,
+                                                            const double* __restrict__ mz,
+                                                            const double* __restrict__ it, int64_t cfirst,
+                                                            int64_t ccount, int64_t cstride) {
+  // flat list of the spectra of the given clusters, in order; ring over it
+  unsigned long long s = 0;
+  double M[PF], X[PF];
+  auto spec_at = [&](int64_t j, int64_t& sidx) {
+    // j-th spectrum of the stream: walk clusters (uniform)
+    return j;
+  };
+  (void)spec_at;
+  for (int64_t k = 0; k < ccount; ++k) {
+    const int64_t c = cfirst + k * cstride;
+    const int64_t s0 = coff[c], s1 = coff[c + 1];
+    const int n = (int)(s1 - s0);
+    auto fetch = [&](int j, double& m, double& x) {
+      const int64_t a = soff[s0 + (j < n ? j : n - 1)], e = soff[s0 + (j < n ? j : n - 1) + 1];
+      const int64_t q = a + (int64_t)threadIdx.x < e ? a + threadIdx.x : a;
+      m = mz[q];
+      x = it[q];
+    };
+#pragma unroll
+    for (int q = 0; q < PF; ++q) fetch(q, M[q], X[q]);
+    for (int jb = 0; jb < n; jb += PF) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        if (jb + q < n) {
+          s ^= bits(M[q]) + bits(X[q]);
+          fetch(jb + q + PF, M[q], X[q]);
+          lds_barrier();
+        }
+      }
+    }
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_pers(const int64_t* __restrict__ coff, const int64_t* __restrict__ soff,
+                                              const double* __restrict__ mz, const double* __restrict__ it,
+                                              int64_t C, int rr, unsigned long long* out) {
+  __shared__ double pad[3800];  // ~30 KB: 5 workgroups per CU
+  const int64_t G = gridDim.x, b = blockIdx.x;
+  unsigned long long s;
+  if (rr) s = ring_clusters<7>(coff, soff, mz, it, b, (C - b + G - 1) / G, G);
+  else s = ring_clusters<7>(coff, soff, mz, it, b * C / G, (b + 1) * C / G - b * C / G, 1);
+  if (s == 0x123456789ull) { pad[threadIdx.x] = 1.0; out[b] = s + (unsigned long long)pad[threadIdx.x ^ 1]; }
+}
+
+__global__ __launch_bounds__(256) void k_cl_ring_lds(const int64_t* __restrict__ coff, const int64_t* __restrict__ soff,
+                                                     const double* __restrict__ mz, const double* __restrict__ it,
+                                                     unsigned long long* out) {
+  __shared__ double pad[3800];
+  const unsigned long long s = ring_clusters<7>(coff, soff, mz, it, blockIdx.x, 1, 1);
+  if (s == 0x123456789ull) { pad[threadIdx.x] = 1.0; out[blockIdx.x] = s + (unsigned long long)pad[threadIdx.x ^ 1]; }
+}
+
+extern "C" int stream_shape2(int kind, const void* coff, const void* soff, const void* mz, const void* it,
+                             int64_t n_clusters, int grid, void* out, void* stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (kind) {
+    case 5:
+    case 6:
+      hipLaunchKernelGGL(k_pers, dim3(grid), dim3(256), 0, s, (const int64_t*)coff, (const int64_t*)soff,
+                         (const double*)mz, (const double*)it, n_clusters, kind == 6 ? 1 : 0,
+                         (unsigned long long*)out);
+      break;
+    case 7:
+      hipLaunchKernelGGL(k_cl_ring_lds, dim3((unsigned)n_clusters), dim3(256), 0, s, (const int64_t*)coff,
+                         (const int64_t*)soff, (const double*)mz, (const double*)it, (unsigned long long*)out);
+      break;
+    default: return -2;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -5,7 +5,11 @@ per dispatch for each kernel, plus per-wave figures (profiling aid).
     python tools/pmc_summary.py gpurun_out/pmc [--json out.json]
 
 FETCH_SIZE / WRITE_SIZE are reported in KB by rocprofv3; `hbm_bytes` converts
-(x1024).  With --json, writes {kernel_short_name: bytes_per_launch} for the
+(x1024) and applies the gfx950 read correction of MI355X_MICROARCH.md (HBM
+section): FETCH_SIZE counts half the bytes of a coalesced streaming read, so it
+is doubled.  Calibrated on our own access pattern: bin_mean_stream_kernel reads
+every m/z and intensity exactly once (8-B lanes, 8.31 GB algorithmic) and
+FETCH_SIZE x 2 = 8.45 GB.  With --json, writes {kernel_short_name: bytes_per_launch} for the
 FETCH_SIZE + WRITE_SIZE pair (profiles/pmc_traffic.json format read by bench.py).
 """
 import argparse
@@ -20,9 +24,11 @@ def short(name):
     return name.split("(")[0].replace("spx::", "").replace("void ", "")
 
 
-def load(root):
+def load(root, only=None):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        if only and not os.path.basename(f).startswith(only):
+            continue
         per = collections.defaultdict(dict)
         for r in csv.DictReader(open(f)):
             key = (r["Dispatch_Id"], r["Kernel_Name"])
@@ -37,8 +43,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--json")
+    ap.add_argument("--only", help="only counter files whose name starts with this prefix")
     a = ap.parse_args()
-    acc = load(a.root)
+    acc = load(a.root, a.only)
     traffic = {}
     for k, cs in sorted(acc.items()):
         mean = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -54,7 +61,7 @@ def main():
                 if c in mean:
                     print(f"   {c} / WAVE_CYCLES = {mean[c] / mean['SQ_WAVE_CYCLES']:.3f}")
         if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
-            traffic[k] = (mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
+            traffic[k] = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
             print(f"   hbm_bytes (fetch+write)      {traffic[k]:16.0f}")
     if a.json:
         with open(a.json, "w") as fh:
