@@ -81,14 +81,6 @@ __device__ __forceinline__ T block_exclusive_scan_lds(T v, T* tmp, T& total) {
   return base + inc - v;
 }
 
-__device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)x >> 32), l);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ double readlane_f64(double x, int l) {
-  return __longlong_as_double(readlane64(__double_as_longlong(x), l));
-}
 
 // Lane-distributed look-ahead of one turn, ONE register: lane i of lanes 0..15
 // holds the low word of spectrum (j0 + i)'s start offset (relative to the

@@ -38,11 +38,14 @@ struct GapParams {
   double bucket_w, inv_bucket_w;  // mz_accuracy (LDS path) or mz_accuracy/2 (global path)
   int32_t pepmass_mode;  // 0 lower_median, 1 naive_average, 2 neutral_average
   int32_t rt_mode;       // 0 median, 1 mass_lower_median
+  int32_t ablate;        // profiling only (SPX_ABLATE): stop after phase 1/2/3/4/5 (bits 1..16), 32 no precursor
 };
 
 enum : int32_t { kNonFinite = 4 };
 
-constexpr int GA_BLOCK = 256;
+constexpr int GA_BLOCK = 512;  // 2 workgroups per CU (LDS): 16 waves
+constexpr int GA_NW = GA_BLOCK / kWave;
+constexpr int GA_U = 12;  // peaks per thread held in registers (8,192 per cluster)
 constexpr int GA_WMAX = 3584;  // 229,376 buckets (2,293 Da at 0.01)
 constexpr int GA_DCAP = 1536;  // occupied buckets per cluster
 
@@ -79,9 +82,91 @@ struct PrecSummary {
 // numpy-compatible "less" for argsort/median ranks: NaN sorts last.
 __device__ __forceinline__ bool lt_nan_last(double a, double b) { return a < b || (!isnan(a) && isnan(b)); }
 
+// Clusters of <= 64 spectra (every config's common case): lane i holds
+// spectrum i's charge, neutral mass and RT, loaded once; ranks and sums walk
+// the other lanes' values by readlane (uniform index) -- no memory traffic in
+// the O(n^2) rank loops.  Same arithmetic and order as the general path below.
+// Lane i's spectrum fields (one load each).
+struct PrecLanes {
+  int32_t z;
+  double pm, rt;
+};
+__device__ __forceinline__ PrecLanes prec_lanes(const CsrView& v, int64_t s0, int64_t n) {
+  const int lane = lane_id();
+  const bool valid = lane < n;
+  return PrecLanes{valid ? v.charge[s0 + lane] : 0, valid ? v.prec_mz[s0 + lane] : 0.0, valid ? v.rt[s0 + lane] : 0.0};
+}
+
+__device__ PrecSummary precursor_summary_wave(const PrecLanes& pl, int n, const GapParams& P) {
+  PrecSummary R;
+  const int lane = lane_id();
+  const double H = P.proton;
+  const bool valid = lane < n;
+  const int32_t zi = pl.z;
+  const double z = (double)zi;
+  const double pm = pl.pm;
+  const double mi = pm * z - z * H;  // (m*c - c*H), no contraction
+  const double ri = pl.rt;
+  // lower-median index of the neutral masses: rank == (n-1)//2
+  const int want = (n - 1) / 2;
+  int rank = 0;
+  for (int j = 0; j < n; ++j) {
+    const double mj = readlane_f64(mi, j);
+    rank += lt_nan_last(mj, mi) || (!lt_nan_last(mi, mj) && j < lane);
+  }
+  const unsigned long long hit = __ballot(valid && rank == want);
+  const int lm = hit ? __ffsll((long long)hit) - 1 : 0;
+  double rt_lo = 0.0, rt_hi = 0.0;
+  if (P.rt_mode == 0) {  // np.median
+    int rr = 0;
+    for (int j = 0; j < n; ++j) {
+      const double rj = readlane_f64(ri, j);
+      rr += lt_nan_last(rj, ri) || (!lt_nan_last(ri, rj) && j < lane);
+    }
+    const unsigned long long h1 = __ballot(valid && rr == (n - 1) / 2), h2 = __ballot(valid && rr == n / 2);
+    rt_lo = readlane_f64(ri, __ffsll((long long)h1) - 1);
+    rt_hi = readlane_f64(ri, __ffsll((long long)h2) - 1);
+  }
+  R.status = kOk;
+  if (P.pepmass_mode == 0) {
+    const int32_t zl = __builtin_amdgcn_readlane(zi, lm);
+    R.pepmass = (readlane_f64(mi, lm) + (double)zl * H) / (double)zl;
+    R.charge = zl;
+  } else if (P.pepmass_mode == 1) {
+    double s = 0.0;
+    int mixed = 0;
+    const int32_t z0 = __builtin_amdgcn_readlane(zi, 0);
+    for (int i = 0; i < n; ++i) {
+      s += readlane_f64(pm, i);
+      mixed |= __builtin_amdgcn_readlane(zi, i) != z0;
+    }
+    R.pepmass = s / (double)n;
+    R.charge = z0;
+    if (mixed) R.status = kMixedCharge;
+  } else {
+    double sm = 0.0;
+    int64_t sz = 0;
+    for (int i = 0; i < n; ++i) {
+      sm += readlane_f64(mi, i);
+      sz += __builtin_amdgcn_readlane(zi, i);
+    }
+    const int32_t zz = (int32_t)rint((double)sz / (double)n);
+    R.pepmass = (sm / (double)n + (double)zz * H) / (double)zz;
+    R.charge = zz;
+  }
+  if (P.rt_mode == 1) {
+    R.rt = readlane_f64(ri, lm);
+  } else {
+    R.rt = (n & 1) ? rt_lo : (0.0 + rt_lo + rt_hi) / 2.0;
+    if (isnan(rt_lo) || isnan(rt_hi)) R.rt = nan_d();
+  }
+  return R;
+}
+
 // Run by one whole wave.  Ranks are stable (ties by index), which is what
 // numpy's argsort returns for n <= 16 and for tie-free input.
 __device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n, const GapParams& P) {
+  if (n <= kWave) return precursor_summary_wave(prec_lanes(v, s0, n), (int)n, P);
   PrecSummary R;
   const int lane = lane_id();
   const double H = P.proton;
@@ -162,6 +247,29 @@ __device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n
   return R;
 }
 
+// Every peak of [p0, p1) once, GA_BATCH loads in flight per thread (indices
+// clamped, so each load is unconditional): f(k, mz[k], inten[k]).  kInten
+// false skips the intensity loads (f sees 0.0).
+constexpr int GA_BATCH = 8;
+template <bool kInten, class F>
+__device__ __forceinline__ void gap_peaks(const CsrView& v, int64_t p0, int64_t p1, F f) {
+  for (int64_t k0 = p0 + threadIdx.x; k0 < p1; k0 += GA_BATCH * GA_BLOCK) {
+    double m[GA_BATCH], it[GA_BATCH];
+#pragma unroll
+    for (int u = 0; u < GA_BATCH; ++u) {
+      const int64_t k = k0 + (int64_t)u * GA_BLOCK;
+      const int64_t kk = k < p1 ? k : p0;
+      m[u] = v.mz[kk];
+      it[u] = kInten ? v.inten[kk] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < GA_BATCH; ++u) {
+      const int64_t k = k0 + (int64_t)u * GA_BLOCK;
+      if (k < p1) f(k, m[u], it[u]);
+    }
+  }
+}
+
 // --------------------------------------------------------------- the body
 template <class PrefixT>
 __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState<PrefixT>& S, int64_t c,
@@ -171,17 +279,52 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1], N = p1 - p0;
   if (n == 0) return kNoGap;
 
+  // The cluster's peaks are read from HBM ONCE into registers when they fit
+  // (<= GA_U per thread: every config's U{2..50} clusters); the passes below
+  // then run from registers.  Larger clusters re-read them per pass.
+  const bool inreg = N <= (int64_t)GA_U * GA_BLOCK;  // uniform
+  double rm[GA_U], ri[GA_U];
+  if (inreg) {
+#pragma unroll
+    for (int u = 0; u < GA_U; ++u) {
+      const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
+      const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
+      if (N > 0) {
+        rm[u] = v.mz[kk];
+        ri[u] = v.inten[kk];
+      } else {
+        rm[u] = ri[u] = 0.0;
+      }
+    }
+  }
+  // f(m, it, tag): tag is scratch the callee may ignore
+  auto peaks = [&](auto f) __attribute__((always_inline)) {
+    if (inreg) {
+#pragma unroll
+      for (int u = 0; u < GA_U; ++u) {
+        const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
+        int32_t tag = 0;
+        if (k < p1) f(rm[u], ri[u], tag);
+      }
+    } else {
+      gap_peaks<true>(v, p0, p1, [&](int64_t, double m, double it) {
+        int32_t tag = 0;
+        f(m, it, tag);
+      });
+    }
+  };
+
   // 1: extrema and finiteness
   double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
   int bad = 0;
-  for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
-    const double m = v.mz[k], it = v.inten[k];
+  peaks([&](double m, double it, int32_t& tag) {
     bad |= !isfinite(m) || !isfinite(it);
     lo = fmin(lo, m);
     hi = fmax(hi, m);
     imax = fmax(imax, fabs(it));
-  }
+  });
   if (__syncthreads_or(bad)) return kNonFinite;
+  if (P.ablate & 1) return kEmpty;
 
   if (n == 1) {
     // passthrough + dynamic-range filter on the raw spectrum (:88-98)
@@ -215,14 +358,15 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   lo = wave_min_d(lo);
   hi = -wave_min_d(-hi);
   imax = -wave_min_d(-imax);
-  if (lane == 0) { red[wid] = lo; red[4 + wid] = hi; red[8 + wid] = imax; }
+  if (lane == 0) { red[wid] = lo; red[GA_NW + wid] = hi; red[2 * GA_NW + wid] = imax; }
   __syncthreads();
   for (int w = 0; w < GA_BLOCK / kWave; ++w) {
     lo = fmin(lo, red[w]);
-    hi = fmax(hi, red[4 + w]);
-    imax = fmax(imax, red[8 + w]);
+    hi = fmax(hi, red[GA_NW + w]);
+    imax = fmax(imax, red[2 * GA_NW + w]);
   }
   const int64_t kb = floor_div_exact(lo, P.bucket_w, P.inv_bucket_w);
+  constexpr bool tagged = false;  // (no per-peak bucket cache: the registers go to the peaks)
   const int64_t ke = floor_div_exact(hi, P.bucket_w, P.inv_bucket_w);
   const int64_t nw = (ke - kb) / 64 + 1;
   if (nw > S.wcap) return kDeferred;
@@ -230,14 +374,15 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   // 2: occupied buckets
   for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
   __syncthreads();
-  for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
-    const int64_t b = floor_div_exact(v.mz[k], P.bucket_w, P.inv_bucket_w) - kb;
+  peaks([&](double m, double, int32_t& tag) {
+    const int64_t b = (tagged ? (int64_t)tag : floor_div_exact(m, P.bucket_w, P.inv_bucket_w)) - kb;
     SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
     atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
-  }
+  });
   __syncthreads();
   const int D = bitmap_prefix<GA_BLOCK>(S.bitmap, S.wprefix, (int)nw, tmp);
   if (D > S.dcap) return kDeferred;
+  if (P.ablate & 2) return kEmpty;
   for (int d = tid; d < D; d += GA_BLOCK) {
     S.cnt[d] = 0u;
     S.gcnt[d] = 0u;
@@ -247,17 +392,19 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   __syncthreads();
 
   // 3: per-slot count and m/z extent
-  for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
-    const double m = v.mz[k];
-    const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
+  peaks([&](double m, double, int32_t& tag) {
+    const int slot =
+        bitmap_rank(S.bitmap, S.wprefix, (tagged ? (int64_t)tag : floor_div_exact(m, P.bucket_w, P.inv_bucket_w)) - kb);
+    tag = slot;
     const uint64_t key = f64_order_key(m);
     SPX_GUARD(slot >= 0 && slot < D, "gap slot c=%ld slot=%d D=%d\n", (long)c, slot, D)
     atomicAdd(&S.cnt[slot], 1u);
     atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)key);
     atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)key);
-  }
+  });
   __syncthreads();
 
+  if (P.ablate & 4) return kEmpty;
   // 4: gaps between consecutive occupied buckets -> emitted group per slot
   const int per = (D + GA_BLOCK - 1) / GA_BLOCK;
   const int d0 = tid * per;
@@ -288,21 +435,23 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
   __syncthreads();
 
+  if (P.ablate & 8) return kEmpty;
   // 5: fixed-point group sums (exact integer adds: order-independent)
   int ex_m, ex_i;
   frexp(fmax(fabs(lo), fabs(hi)) * (double)N, &ex_m);
   frexp(imax * (double)N, &ex_i);
   const int sc_m = 61 - ex_m, sc_i = 61 - ex_i;
-  for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
-    const double m = v.mz[k], it = v.inten[k];
-    const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
+  peaks([&](double m, double it, int32_t& tag) {
+    const int slot =
+        tagged ? tag : bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
     const uint32_t eg = S.cnt[slot];
     SPX_GUARD(slot >= 0 && slot < D && (int)eg < E, "gap eg c=%ld slot=%d eg=%u E=%d\n", (long)c, slot, eg, E)
     atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), (unsigned long long)__double2ll_rn(ldexp(m, sc_m)));
     atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[eg]), (unsigned long long)__double2ll_rn(ldexp(it, sc_i)));
-  }
+  });
   __syncthreads();
 
+  if (P.ablate & 16) return kEmpty;
   // 6: min_fraction filter, dynamic range, ordered output
   const double min_len = P.min_fraction * (double)n;
   const int gper = (E + GA_BLOCK - 1) / GA_BLOCK;
@@ -345,12 +494,16 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 template <class PrefixT>
 __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P, int64_t c, int32_t st,
                                            const PeaksOut& out, double* prec_out, int32_t* charge_out,
-                                           double* rt_out, int32_t* status) {
+                                           double* rt_out, int32_t* status, const PrecLanes* pl = nullptr) {
   const int64_t s0 = v.cluster_off[c], n = v.cluster_off[c + 1] - s0;
   if (st == kDeferred) return;
+  if (P.ablate & 32) {
+    if (threadIdx.x == 0) status[c] = st;
+    return;
+  }
   if (wave_id() == 0) {
     PrecSummary R{nan_d(), nan_d(), 0, kOk};
-    if (n > 0) R = precursor_summary(v, s0, n, P);
+    if (n > 0) R = (pl && n <= kWave) ? precursor_summary_wave(*pl, (int)n, P) : precursor_summary(v, s0, n, P);
     if (lane_id() == 0) {
       // the reference computes the precursor first (:161-163): its error wins
       const int32_t fin = R.status != kOk ? R.status : st;
@@ -363,7 +516,7 @@ __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P,
   }
 }
 
-__global__ __launch_bounds__(GA_BLOCK) void gap_average_lds_kernel(CsrView v, GapParams P, PeaksOut out,
+__global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v, GapParams P, PeaksOut out,
                                                                    double* prec_out, int32_t* charge_out,
                                                                    double* rt_out, int32_t* status,
                                                                    int32_t* deferred, int32_t* n_deferred) {

@@ -236,6 +236,7 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   P.rt_mode = params->rt_mode;
   P.bucket_w = params->mz_accuracy;
   P.inv_bucket_w = 1.0 / params->mz_accuracy;
+  P.ablate = ablate_mask();
   spx::PeaksOut O{out->mz, out->inten, out->count};
   const spx::CsrView V = view(csr);
   const int wcap = gap_wcap(params, info);

@@ -83,6 +83,16 @@ __device__ __forceinline__ double wave_min_d(double x) {
   return x;
 }
 
+// lane l's value, broadcast (l uniform: v_readlane into scalar registers)
+__device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)x >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  return __longlong_as_double(readlane64(__double_as_longlong(x), l));
+}
+
 // Block exclusive scan of one int per thread.  `tmp` holds BLOCK/64 + 1 ints
 // in LDS.  Returns the exclusive prefix; `total` receives the block sum.
 template <int BLOCK, class T>
