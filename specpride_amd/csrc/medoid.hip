@@ -363,7 +363,8 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
 // [0, 65,536), > 1,984 distinct bins.
 constexpr int MR_UMAX = 48;                  // peaks per thread (12,288 per cluster)
 constexpr int MR_PMAX = MR_UMAX * MD_BLOCK;
-constexpr int MR_MS = MD_NMAX + 1;           // max row stride of the distance matrix (odd)
+constexpr int MR_WMAX = 512;                 // union-bitmap words: bins < 32,768 (m/z < 3,276.8 at 0.1)
+constexpr int MR_TRI = MD_NMAX * (MD_NMAX + 1) / 2;  // packed upper triangle of the distance matrix
 
 struct MrRec {
   unsigned long long bits;
@@ -373,12 +374,12 @@ struct MrRec {
 struct MedoidRegSmem {
   union {
     struct {
-      MrRec rec[MD_WMAX];                        // occupancy word + exclusive popcount prefix
+      MrRec rec[MR_WMAX];                        // occupancy word + exclusive popcount prefix
       unsigned long long rows[MD_NMAX * MD_KWMAX];
       unsigned long long sbits[MR_PMAX / 64];    // bit r: peak r starts spectrum >= 1
       uint8_t spre[MR_PMAX / 64];                // spectra started before word w
     } a;                                         // P0..P4a
-    double d[MD_NMAX * MR_MS];                   // P4b..P5
+    double d[MR_TRI];                            // P4b..P5: d(i, j), j >= i, row-major packed
   } u;
   int32_t soff[MD_NMAX + 1];
   double totals[MD_NMAX];
@@ -419,7 +420,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   const int nsw = (np + 63) / 64;
   for (int w = tid; w < nsw; w += MD_BLOCK) L.u.a.sbits[w] = 0ull;
   if (tid <= n) L.soff[tid] = (int32_t)(v.spec_off[s0 + tid] - p0);
-  for (int w = tid; w < MD_WMAX; w += MD_BLOCK) L.u.a.rec[w].bits = 0ull;
+  for (int w = tid; w < MR_WMAX; w += MD_BLOCK) L.u.a.rec[w].bits = 0ull;
   if (tid == 0) L.red[0] = 0;
   __syncthreads();
   if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
@@ -452,7 +453,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   uint32_t bins[MR_UMAX / 2];
   int outside = 0;
   uint32_t bmax = 0u;
-  constexpr uint32_t kBins = (uint32_t)MD_WMAX * 64u;
+  constexpr uint32_t kBins = (uint32_t)MR_WMAX * 64u;
   constexpr int NB = MR_UMAX / 8;
   auto pass1 = [&](auto nbt_c) __attribute__((always_inline)) {
     constexpr int NBT = decltype(nbt_c)::value;
@@ -598,16 +599,17 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     }
   }
   __syncthreads();  // rows dead: the distance matrix takes their place
-  const int ms = n | 1;  // odd row stride (conflict-free column reads)
 #pragma unroll
   for (int q = 0; q < PPT; ++q) {
     if (pij[q] >= 0) {
       const int i = pij[q] >> 8, j = pij[q] & 0xff;
-      L.u.d[i * ms + j] = md_dist(pc[q], L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
-      if (j != i) L.u.d[j * ms + i] = 0.0;  // the reference's lower triangle stays 0
+      L.u.d[row_start(i) + j - i] = md_dist(pc[q], L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
     }
   }
   __syncthreads();
+  // D(a, b) of the reference's dense matrix: the upper triangle incl. the
+  // diagonal, zeros below (most_similar_representative.py:91-93)
+  auto dval = [&](int a, int b) -> double { return b >= a ? L.u.d[row_start(a) + b - a] : 0.0; };
   if (P.ablate & 32) { if (tid == 0) rep[c] = s0; return; }
 
   // P5: totals, 16 lanes per spectrum (8 row accumulators, 8 column ones)
@@ -618,20 +620,19 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     const int i = i0 + tid / 16;
     const bool valid = i < n;
     const int ii = valid ? i : 0;
-    // row ii (stride 1 from ii*ms) or column ii (stride ms from ii)
-    const double* e = L.u.d + (colside ? ii : ii * ms);
-    const int st = colside ? ms : 1;
+    // row ii or column ii of D
+    auto e = [&](int j) { return colside ? dval(j, ii) : dval(ii, j); };
     double s = 0.0;
     if (n >= 8) {
-      double r = e[k * st];
-      for (int j = 8 + k; j < lim; j += 8) r += e[j * st];
+      double r = e(k);
+      for (int j = 8 + k; j < lim; j += 8) r += e(j);
       r += __shfl_xor(r, 1, kWave);
       r += __shfl_xor(r, 2, kWave);
       r += __shfl_xor(r, 4, kWave);  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
       s = r;
-      for (int j = lim; j < n; ++j) s += e[j * st];  // the sequential tail
+      for (int j = lim; j < n; ++j) s += e(j);  // the sequential tail
     } else {
-      for (int j = 0; j < n; ++j) s += e[j * st];  // 0.0 + a0 + a1 + ...
+      for (int j = 0; j < n; ++j) s += e(j);  // 0.0 + a0 + a1 + ...
     }
     s = 0.0 + s;
     const double other = __shfl_xor(s, 8, kWave);
