@@ -14,6 +14,8 @@
  *   spx_medoid       <- src/most_similar_representative.py:13-19 distance() and the
  *                       per-cluster medoid loop :60-111
  *   spx_xcorr_distance <- src/most_similar_representative.py:13-19 distance() per pair
+ *   spx_binned_cosine  <- src/benchmark.py:10-38  bin_proc / cos_dist / average_cos_dist
+ *                       (representative vs its cluster members)
  *   spx_compact_peaks   (packing helper for the shims' output writers)
  *
  * Conventions
@@ -138,6 +140,23 @@ int spx_medoid(const spx_csr *csr, const spx_medoid_params *params, int64_t *rep
  * behind most_similar_representative.distance (:13-19); not the batched path. */
 int spx_xcorr_distance(const spx_csr *csr, const spx_medoid_params *params, const int64_t *pairs,
                        int64_t n_pairs, double *out, void *stream);
+
+/* ---- binned cosine: benchmark.cos_dist(representative, member) for every member of
+ *      every cluster + average_cos_dist per cluster (benchmark.py:10-38) ---- */
+typedef struct spx_cosine_params {
+  double mz_space; /* benchmark.py:7-8: 1.000508 * .005 */
+} spx_cosine_params;
+
+/* Cluster c's representative is the peak list [rep_off[c], rep_off[c+1]) of
+ * rep_mz / rep_inten (device arrays; e.g. the compacted bin-mean output); its
+ * members are the cluster's spectra in csr.  cos_out [n_spectra] = cos_dist per
+ * member, avg_out [n_clusters] = average_cos_dist (0.0 for no members).
+ * status[c]: SPX_EMPTY if the representative or a member has no peaks (the
+ * reference's mz[-1] raises IndexError; NaN outputs), SPX_UNRESOLVED if the
+ * representative has more than 1,024 peaks. */
+int spx_binned_cosine(const spx_csr *csr, const int64_t *rep_off, const double *rep_mz, const double *rep_inten,
+                      const spx_cosine_params *params, double *cos_out, double *avg_out, int32_t *status,
+                      void *stream);
 
 /* Pack the per-cluster outputs densely: dst[out_off[c] + k] = src[spec_off[cluster_off[c]] + k]
  * for k < count[c]; out_off is the exclusive prefix sum of count (device array [C+1]). */

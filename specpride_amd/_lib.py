@@ -59,10 +59,14 @@ class SpxMedoidParams(ctypes.Structure):
     _fields_ = [("tolerance", _dbl)]
 
 
+class SpxCosineParams(ctypes.Structure):
+    _fields_ = [("mz_space", _dbl)]
+
+
 # every symbol include/specpride.h declares (checked by tests/test_host.py)
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_gap_average_workspace_size", "spx_gap_average",
-            "spx_medoid_workspace_size", "spx_medoid", "spx_xcorr_distance", "spx_compact_peaks", "spx_abi_version",
-            "spx_last_error"]
+            "spx_medoid_workspace_size", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine", "spx_compact_peaks",
+            "spx_abi_version", "spx_last_error"]
 
 SPX_ABI_VERSION = 1
 _lib = None
@@ -129,6 +133,7 @@ def lib():
     L.spx_medoid.argtypes = [_p, _p, _p, _p, _p, _sz, _p]
     L.spx_compact_peaks.argtypes = [_p, _p, _p, _p, _p, _p]
     L.spx_xcorr_distance.argtypes = [_p, _p, _p, _i64, _p, _p]
+    L.spx_binned_cosine.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _p]
     if L.spx_abi_version() != SPX_ABI_VERSION:
         raise RuntimeError(f"libspecpride_hip ABI {L.spx_abi_version()} != {SPX_ABI_VERSION}")
     _lib = L

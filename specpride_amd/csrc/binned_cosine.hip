@@ -1,0 +1,309 @@
+// Binned-cosine evaluation of a representative against its cluster members
+// (reference: src/benchmark.py:10-38, bin_proc / cos_dist / average_cos_dist;
+// restated in oracle/np_oracle.py and pinned by tests/golden/binned_cosine.npz).
+//
+// The reference densifies both spectra on the edges
+//   np.arange(-s/2, max_mz, s), s = 1.000508 * 0.005, max_mz = max(last m/z of the pair)
+// (~400k bins), sums intensities per bin (scipy binned_statistic: np.digitize,
+// a value "on" the rightmost edge -- x >= e_last and np.around(x, 8) ==
+// np.around(e_last, 8) -- shifted into the last bin, outliers dropped), and
+// takes cos = A.B / sqrt(A.A * B.B) (0 if either is all zero).  Only bins a
+// spectrum occupies contribute, so everything here is sparse:
+//   * edges exactly as numpy's DOUBLE_fill writes them: e0 = start,
+//     e1 = start + s, e_i = start + i * (e1 - e0); a peak's bin k is the exact
+//     #edges <= x minus 1 (a divide for the estimate, then edge compares)
+//   * the representative (<= CS_RCAP peaks) is stable-rank-sorted by bin in LDS,
+//     its runs summed in input order (np.bincount's order), and the prefix of
+//     A_b^2 over runs kept, so each pair's cut (bins <= L-2, L = len(edges))
+//     gives A.A with one binary search
+//   * one wave per member: each peak's bin (cut and on-edge rule of this pair),
+//     A.B = sum_q I_q * A'_{bin(q)} by binary search over the runs, B.B from the
+//     member's own runs of equal bins (sums in input order; an unsorted member
+//     takes an O(m^2) pass instead)
+//   * average_cos_dist = the sequential mean over the members in order.
+// Dot products are summed in a different order than BLAS's ddot: values agree
+// with the reference to ~1e-15 relative (the north star asks 1e-5).
+#include "spx_device.hpp"
+
+namespace spx {
+
+struct CosParams {
+  double s, start, e1, d;  // np.arange(start, stop, s) = start, e1, start + i * d
+  double p10;              // 10**decimals of scipy's on-edge rounding
+};
+
+constexpr int CS_BLOCK = 256;
+constexpr int CS_RCAP = 1024;  // representative peaks held in LDS
+constexpr int CS_NW = CS_BLOCK / kWave;
+
+struct CosSmem {
+  int32_t sk[CS_RCAP];       // representative peak bins, input order (rank sort input)
+  int32_t pk[CS_RCAP];       // ... sorted by (bin, index)
+  double pI[CS_RCAP];        //     their intensities
+  int16_t pidx[CS_RCAP];     //     their input index
+  int32_t rb[CS_RCAP];       // runs of equal bins: bin,
+  int16_t rs[CS_RCAP + 1];   //   first sorted position,
+  double rA[CS_RCAP];        //   A_b (summed in input order),
+  double rA2[CS_RCAP + 1];   //   exclusive prefix of A_b^2
+  int32_t wk[CS_NW][kWave];  // per-wave member scratch: bins,
+  double wI[CS_NW][kWave];   //   intensities
+  double tmpd[CS_NW + 1];
+  int tmp[CS_NW + 1];
+  int nruns;
+};
+
+__device__ __forceinline__ double cs_edge(const CosParams& P, int64_t i) {
+  return i == 0 ? P.start : (i == 1 ? P.e1 : P.start + (double)i * P.d);
+}
+
+// k with e_k <= x < e_{k+1} over the unbounded edge sequence; -1 below e_0 or NaN
+__device__ __forceinline__ int64_t cs_bin(const CosParams& P, double x) {
+  if (!(x >= P.start)) return -1;
+  int64_t k = (int64_t)((x - P.start) / P.d);
+  if (k > 0 && cs_edge(P, k) > x) --k;
+  if (k > 0 && cs_edge(P, k) > x) --k;
+  while (cs_edge(P, k + 1) <= x) ++k;
+  return k;
+}
+
+// np.around(x, decimals) for decimals > 0: rint(x * 10**d) / 10**d
+__device__ __forceinline__ double np_around(double x, double p10) { return rint(x * p10) / p10; }
+
+// first run index with a bin > b (runs sorted by bin), over [0, nr)
+__device__ __forceinline__ int runs_upper(const int32_t* rb, int nr, int64_t b) {
+  int lo = 0, hi = nr;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)rb[mid] <= b) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+__global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosParams P, const int64_t* rep_off,
+                                                                 const double* rep_mz, const double* rep_int,
+                                                                 double* cos_out, double* avg_out, int32_t* status) {
+  __shared__ CosSmem L;
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const int64_t c = blockIdx.x;
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+  const int n = (int)(s1 - s0);
+  const int64_t r0 = rep_off[c];
+  const int R = (int)(rep_off[c + 1] - r0);
+  const double nan = __longlong_as_double(0x7ff8000000000000ll);
+  if (n == 0) {  // average_cos_dist of no members (benchmark.py:36-38)
+    if (tid == 0) { avg_out[c] = 0.0; status[c] = kOk; }
+    return;
+  }
+  // an empty spectrum: the reference's mz[-1] raises IndexError (benchmark.py:20)
+  int empty = R == 0;
+  for (int j = tid; j < n; j += CS_BLOCK) empty |= v.spec_off[s0 + j + 1] == v.spec_off[s0 + j];
+  const bool any_empty = __syncthreads_or(empty);
+  if (any_empty || R > CS_RCAP) {
+    for (int j = tid; j < n; j += CS_BLOCK) cos_out[s0 + j] = nan;
+    if (tid == 0) { avg_out[c] = nan; status[c] = any_empty ? kEmpty : kDeferred; }
+    return;
+  }
+
+  // representative: bins, stable rank sort by (bin, index), runs, prefix of A^2
+  for (int i = tid; i < R; i += CS_BLOCK) {
+    const int64_t k = cs_bin(P, rep_mz[r0 + i]);
+    L.sk[i] = k > 0x7ffffffe ? 0x7ffffffe : (int32_t)k;
+  }
+  __syncthreads();
+  for (int i = tid; i < R; i += CS_BLOCK) {
+    const int32_t k = L.sk[i];
+    int rank = 0;
+    for (int j = 0; j < R; ++j) {
+      const int32_t kj = L.sk[j];
+      rank += kj < k || (kj == k && j < i);
+    }
+    L.pk[rank] = k;
+    L.pI[rank] = rep_int[r0 + i];
+    L.pidx[rank] = (int16_t)i;
+  }
+  __syncthreads();
+  {
+    constexpr int PER = CS_RCAP / CS_BLOCK;
+    int heads = 0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int r = PER * tid + u;
+      heads += r < R && (r == 0 || L.pk[r] != L.pk[r - 1]);
+    }
+    int nr;
+    int id = block_exclusive_scan<CS_BLOCK>(heads, L.tmp, nr);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int r = PER * tid + u;
+      if (r < R && (r == 0 || L.pk[r] != L.pk[r - 1])) {
+        double A = 0.0;  // np.bincount: out[bin] = 0.0, then += w in input order
+        for (int q = r; q < R && L.pk[q] == L.pk[r]; ++q) A += L.pI[q];
+        L.rb[id] = L.pk[r];
+        L.rs[id] = (int16_t)r;
+        L.rA[id] = A;
+        ++id;
+      }
+    }
+    if (tid == 0) { L.nruns = nr; L.rs[nr] = (int16_t)R; }
+    __syncthreads();
+    double sq = 0.0;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int r = PER * tid + u;
+      if (r < nr && L.rb[r] >= 0) sq += L.rA[r] * L.rA[r];
+    }
+    double tot;
+    double pre = block_exclusive_scan<CS_BLOCK>(sq, L.tmpd, tot);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int r = PER * tid + u;
+      if (r < nr) {
+        L.rA2[r] = pre;
+        if (L.rb[r] >= 0) pre += L.rA[r] * L.rA[r];
+      }
+    }
+    if (tid == 0) L.rA2[nr] = tot;
+    __syncthreads();
+  }
+  const int NR = L.nruns;
+  const double rep_last = rep_mz[r0 + R - 1];  // rep.mz[-1] (benchmark.py:20)
+
+  // members: one wave each
+  for (int j = wid; j < n; j += CS_NW) {
+    const int64_t a = v.spec_off[s0 + j], e = v.spec_off[s0 + j + 1];
+    const double mem_last = v.mz[e - 1];
+    const double max_mz = mem_last > rep_last ? mem_last : rep_last;  // max(rep.mz[-1], member.mz[-1])
+    const int64_t Lc = (int64_t)ceil((max_mz - P.start) / P.s);      // len(np.arange(...))
+    const int64_t kc = Lc - 2;                                          // the last bin
+    const double e_last = cs_edge(P, Lc - 1), rl = np_around(e_last, P.p10);
+    // representative under this pair's cut: A.A and the on-edge extra of bin kc
+    const int ic = runs_upper(L.rb, NR, kc);  // runs with a bin <= kc
+    double extra = 0.0;
+    bool has_extra = false;
+    if (ic < NR && (int64_t)L.rb[ic] == kc + 1) {
+      for (int q = L.rs[ic]; q < L.rs[ic + 1]; ++q) {
+        const double x = rep_mz[r0 + L.pidx[q]];
+        if (x >= e_last && np_around(x, P.p10) == rl) {
+          extra += L.pI[q];
+          has_extra = true;
+        }
+      }
+    }
+    const bool kc_run = ic > 0 && (int64_t)L.rb[ic - 1] == kc;
+    const double A_kc = (kc_run ? L.rA[ic - 1] : 0.0) + extra;  // A'_{kc}
+    double aa = L.rA2[ic];
+    if (has_extra) aa = L.rA2[kc_run ? ic - 1 : ic] + A_kc * A_kc;
+    auto lookup = [&](int64_t b) -> double {
+      if (b == kc) return A_kc;
+      const int u = runs_upper(L.rb, NR, b);
+      return (u > 0 && (int64_t)L.rb[u - 1] == b) ? L.rA[u - 1] : 0.0;
+    };
+    auto mem_bin = [&](double x) -> int64_t {
+      const int64_t k = cs_bin(P, x);
+      if (k >= 0 && k <= kc) return k;
+      if (k > kc && x >= e_last && np_around(x, P.p10) == rl) return kc;  // on the rightmost edge
+      return -1;
+    };
+    const int m = (int)(e - a);
+    double ab = 0.0, bb = 0.0;
+    int64_t carry_b = -1, lastb = -1, last_raw = -1;
+    double carry_s = 0.0;
+    bool unsorted = false;
+    for (int ch = 0; ch < m; ch += kWave) {
+      const int q = ch + lane;
+      const bool in = q < m;
+      const double x = in ? v.mz[a + q] : 0.0, I = in ? v.inten[a + q] : 0.0;
+      const int64_t bm = in ? mem_bin(x) : -1;
+      if (bm >= 0) ab += I * lookup(bm);
+      // runs need every valid bin >= the previous valid one, and a repeated bin
+      // right after its predecessor (an invalid peak between two equal bins
+      // would split np.bincount's single sum)
+      int64_t pm = bm;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int64_t t = __shfl_up(pm, o, kWave);
+        if (lane >= o) pm = pm > t ? pm : t;
+      }
+      int64_t prev = __shfl_up(pm, 1, kWave);
+      int64_t raw_before = __shfl_up(bm, 1, kWave);
+      if (lane == 0) { prev = -1; raw_before = last_raw; }
+      prev = prev > lastb ? prev : lastb;
+      unsorted |= __ballot(bm >= 0 && (bm < prev || (bm == prev && raw_before != bm))) != 0ull;
+      const int64_t cmax = __shfl(pm, kWave - 1, kWave);
+      lastb = cmax > lastb ? cmax : lastb;
+      last_raw = __shfl(bm, kWave - 1, kWave);
+      if (unsorted) continue;  // (uniform) B.B by the O(m^2) pass below
+      // runs of equal bins, summed in input order; the last one may continue
+      L.wk[wid][lane] = (int32_t)bm;
+      L.wI[wid][lane] = I;
+      wave_lds_sync();
+      const int64_t before = lane == 0 ? carry_b : (int64_t)L.wk[wid][lane - 1];
+      const bool head = bm >= 0 && bm != before;
+      const bool cont = lane == 0 && bm >= 0 && bm == carry_b;  // continues the open run
+      int64_t new_carry_b = -1;
+      double new_carry_s = 0.0;
+      if (carry_b >= 0 && !(__ballot(cont) & 1ull) && lane == 0) bb += carry_s * carry_s;  // open run closed
+      if (head || cont) {
+        double s = cont ? carry_s : 0.0;
+        int qq = lane;
+        while (qq < kWave && L.wk[wid][qq] == (int32_t)bm) s += L.wI[wid][qq++];
+        if (qq == kWave && ch + kWave < m) {
+          new_carry_b = bm;
+          new_carry_s = s;
+        } else {
+          bb += s * s;
+        }
+      }
+      const unsigned long long cm = __ballot(new_carry_b >= 0);
+      if (cm) {
+        const int cl = __ffsll((long long)cm) - 1;
+        carry_b = readlane64(new_carry_b, cl);
+        carry_s = readlane_f64(new_carry_s, cl);
+      } else {
+        carry_b = -1;
+        carry_s = 0.0;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (unsorted) {  // B.B = sum_q I_q * (sum of I over the member's peaks in q's bin)
+      bb = 0.0;
+      for (int ch = 0; ch < m; ch += kWave) {
+        const int q = ch + lane;
+        const double I = q < m ? v.inten[a + q] : 0.0;
+        const int64_t bm = q < m ? mem_bin(v.mz[a + q]) : -1;
+        double sb = 0.0;
+        for (int ch2 = 0; ch2 < m; ch2 += kWave) {
+          const int q2 = ch2 + lane;
+          L.wk[wid][lane] = q2 < m ? (int32_t)mem_bin(v.mz[a + q2]) : -1;
+          L.wI[wid][lane] = q2 < m ? v.inten[a + q2] : 0.0;
+          wave_lds_sync();
+          for (int t = 0; t < kWave; ++t)
+            if (bm >= 0 && L.wk[wid][t] == (int32_t)bm) sb += L.wI[wid][t];
+          __builtin_amdgcn_wave_barrier();
+        }
+        if (bm >= 0) bb += I * sb;
+      }
+    } else if (carry_b >= 0 && lane == 0) {
+      bb += carry_s * carry_s;
+    }
+    ab = wave_sum(ab);
+    bb = wave_sum(bb);
+    if (lane == 0) cos_out[s0 + j] = (aa == 0.0 || bb == 0.0) ? 0.0 : ab / sqrt(aa * bb);
+  }
+  __syncthreads();
+  if (tid == 0) {  // average_cos_dist: sequential sum in member order (benchmark.py:33-36)
+    double sum = 0.0;
+    for (int j = 0; j < n; ++j) sum += cos_out[s0 + j];
+    avg_out[c] = sum / (double)n;
+    status[c] = kOk;
+  }
+}
+
+}  // namespace spx

@@ -15,6 +15,7 @@
 
 #include "../../include/specpride.h"
 #include "bin_mean_stream.hip"  // includes bin_mean.hip
+#include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
 
@@ -350,6 +351,30 @@ extern "C" int spx_xcorr_distance(const spx_csr* csr, const spx_medoid_params* p
   hipLaunchKernelGGL(spx::xcorr_pairs_kernel, dim3((unsigned)((n_pairs + 3) / 4)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), view(csr), P, pairs, n_pairs, out);
   return check_launch("xcorr_pairs_kernel");
+}
+
+// ------------------------------------------------------------ binned cosine
+extern "C" int spx_binned_cosine(const spx_csr* csr, const int64_t* rep_off, const double* rep_mz,
+                                 const double* rep_inten, const spx_cosine_params* params, double* cos_out,
+                                 double* avg_out, int32_t* status, void* stream) {
+  if (!csr_ok(csr) || !rep_off || !params || !avg_out || !status || (csr->n_spectra && !cos_out))
+    return fail(SPX_EINVAL, "spx_binned_cosine: null argument");
+  if (!(params->mz_space > 0)) return fail(SPX_EINVAL, "spx_binned_cosine: mz_space must be > 0");
+  const int64_t C = csr->n_clusters;
+  if (C == 0) return SPX_SUCCESS;
+  // np.arange(-s/2, stop, s): e0 = start, e1 = start + s, e_i = start + i * (e1 - e0)
+  // (numpy DOUBLE_fill); scipy's on-edge rounding keeps int(-log10(min edge gap)) + 6 decimals
+  spx::CosParams P;
+  P.s = params->mz_space;
+  P.start = -params->mz_space / 2.0;
+  P.e1 = P.start + P.s;
+  P.d = P.e1 - P.start;
+  const int dec = (int)(-std::log10(std::min(P.d, P.s))) + 6;
+  P.p10 = std::pow(10.0, (double)dec);
+  hipLaunchKernelGGL(spx::binned_cosine_kernel, dim3((unsigned)C), dim3(spx::CS_BLOCK), 0,
+                     reinterpret_cast<hipStream_t>(stream), view(csr), P, rep_off, rep_mz, rep_inten, cos_out, avg_out,
+                     status);
+  return check_launch("binned_cosine_kernel");
 }
 
 // ---------------------------------------------------------------- compaction

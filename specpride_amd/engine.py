@@ -223,3 +223,35 @@ def xcorr_distance(batch: DeviceBatch, pairs, tolerance=0.1, stream=None):
     _lib.check(_lib.lib().spx_xcorr_distance(ctypes.byref(batch.csr), ctypes.byref(prm), _ptr(pairs_t),
                                              len(pairs_t), _ptr(out), _stream_handle(stream)), "spx_xcorr_distance")
     return out[:len(pairs_t)]
+
+
+MZ_SPACE = 1.000508 * .005  # benchmark.py:7-8 (mz_unit * .005)
+
+
+@dataclass
+class CosineResult:
+    cos: object     # [S] f64: cos_dist(representative, member) per member spectrum
+    avg: object     # [C] f64: average_cos_dist per cluster
+    status: object  # [C] i32 (STATUS_EMPTY: an empty spectrum; STATUS_UNRESOLVED: > 1,024 representative peaks)
+
+    def to_host(self):
+        return self.cos.cpu().numpy(), self.avg.cpu().numpy(), self.status.cpu().numpy()
+
+
+def binned_cosine(batch: DeviceBatch, rep_off, rep_mz, rep_int, mz_space=MZ_SPACE,
+                  out: Optional[CosineResult] = None, stream=None) -> CosineResult:
+    """cos_dist / average_cos_dist (benchmark.py:19-38) for every cluster of the
+    batch: cluster c's representative is the device peak list
+    [rep_off[c], rep_off[c+1]) of rep_mz / rep_int, its members are its spectra."""
+    import torch
+
+    dev = batch.device
+    if out is None:
+        out = CosineResult(torch.empty(max(batch.n_spectra, 1), dtype=torch.float64, device=dev),
+                           torch.empty(max(batch.n_clusters, 1), dtype=torch.float64, device=dev),
+                           torch.empty(max(batch.n_clusters, 1), dtype=torch.int32, device=dev))
+    prm = _lib.SpxCosineParams(float(mz_space))
+    _lib.check(_lib.lib().spx_binned_cosine(ctypes.byref(batch.csr), _ptr(rep_off), _ptr(rep_mz), _ptr(rep_int),
+                                            ctypes.byref(prm), _ptr(out.cos), _ptr(out.avg), _ptr(out.status),
+                                            _stream_handle(stream)), "spx_binned_cosine")
+    return out

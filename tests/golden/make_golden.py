@@ -18,6 +18,7 @@ Fixtures:
   precursor_helpers.npz     lower_median_mass & co (average_spectrum_clustering.py:106-148)
   medoid_<set>.npz          most_similar_representative.main() reps (most_similar_representative.py:22-115)
   pairwise_sum.npz          numpy pairwise summation (the reduction pandas .sum() runs)
+  binned_cosine.npz         cos_dist / average_cos_dist per cluster (benchmark.py:10-38)
 """
 from __future__ import annotations
 
@@ -408,6 +409,87 @@ def gen_pairwise():
     print("pairwise_sum: ok")
 
 
+def binned_cosine_cases(rng):
+    """Representative + members per cluster: synthetic clusters with a member
+    or a jittered copy as the representative, plus the binning edge cases."""
+    import importlib
+    bench = importlib.import_module("benchmark")
+    s = bench.mz_space
+    start = -s / 2.
+    clusters, reps = [], []
+    csr = make_clusters_np(40, seed=31, n_template=120)
+    for c in range(csr.n_clusters):
+        spectra = []
+        for k in range(csr.cluster_off[c], csr.cluster_off[c + 1]):
+            a, b = csr.spec_off[k], csr.spec_off[k + 1]
+            spectra.append((csr.mz[a:b].copy(), csr.inten[a:b].copy()))
+        clusters.append(spectra)
+        if c % 3 == 0:
+            reps.append(spectra[0])
+        else:  # a consensus-like representative: jittered, re-sorted
+            mz = np.sort(np.round(spectra[-1][0] + rng.normal(0, 0.002, len(spectra[-1][0])), 5))
+            reps.append((mz, np.round(rng.lognormal(5, 1, len(mz)), 2)))
+
+    def edge(i):  # np.arange's i-th value (numpy DOUBLE_fill)
+        return start if i == 0 else (start + s if i == 1 else start + i * ((start + s) - start))
+
+    # on the rightmost edge: the pair's max m/z puts a member peak within 1e-9 of the last edge
+    M = 1500.0
+    L = int(np.ceil((M - start) / s))
+    e_last = edge(L - 1)
+    rep = (np.array([100.0, 700.5, 1200.25, M]), np.array([10.0, 20.0, 30.0, 40.0]))
+    mem = (np.array([100.001, 700.501, e_last, e_last + 3e-9, e_last + 2e-7]), np.array([1.0, 2.0, 3.0, 4.0, 5.0]))
+    clusters.append([mem, rep])
+    reps.append(rep)
+    # peaks sharing bins (sum order), a peak at 0.0 and one below the first edge
+    clusters.append([(np.array([-0.01, 0.0, 0.001, 0.002, 500.0, 500.001]), np.array([1., 2., 3., 4., 5., 6.])),
+                     (np.array([0.0005, 500.0004]), np.array([7., 8.]))])
+    reps.append((np.array([0.0, 0.0015, 500.0, 800.0]), np.array([2.0, 3.0, 5.0, 1.0])))
+    # no shared bin (0.0), zero intensities (a == 0 -> 0.0), identical spectra (1.0)
+    clusters.append([(np.array([300.0, 400.0]), np.array([1.0, 1.0])),
+                     (np.array([200.0, 250.0]), np.array([0.0, 0.0])),
+                     (np.array([200.0, 250.0, 900.0]), np.array([3.0, 4.0, 5.0]))])
+    reps.append((np.array([200.0, 250.0, 900.0]), np.array([3.0, 4.0, 5.0])))
+    # unsorted member and unsorted representative
+    clusters.append([(np.array([900.0, 200.0, 250.0, 200.001]), np.array([5.0, 3.0, 4.0, 1.0]))])
+    reps.append((np.array([250.0, 200.0, 900.0, 200.002]), np.array([4.0, 3.0, 5.0, 2.0])))
+    # no members (average 0.0), an empty member (IndexError)
+    clusters.append([])
+    reps.append((np.array([100.0]), np.array([1.0])))
+    clusters.append([(np.array([100.0]), np.array([1.0])), (np.zeros(0), np.zeros(0))])
+    reps.append((np.array([100.0]), np.array([1.0])))
+    return bench, clusters, reps
+
+
+def gen_binned_cosine():
+    from types import SimpleNamespace
+
+    rng = np.random.default_rng(17)
+    bench, clusters, reps = binned_cosine_cases(rng)
+    cos, avg, status = [], [], []
+    for spectra, (rm, ri) in zip(clusters, reps):
+        rep = SimpleNamespace(mz=rm, intensity=ri)
+        members = [SimpleNamespace(mz=m, intensity=i) for m, i in spectra]
+        try:
+            cs = [bench.cos_dist(rep, mem) for mem in members]
+            avg.append(bench.average_cos_dist(rep, members))
+            cos.extend(cs)
+            status.append(STATUS_OK)
+        except IndexError:  # mz[-1] of an empty spectrum (benchmark.py:20)
+            cos.extend([np.nan] * len(spectra))
+            avg.append(np.nan)
+            status.append(STATUS_EMPTY)
+    csr = SpectraCSR.from_clusters([[{"m/z array": m, "intensity array": i} for m, i in sp] for sp in clusters])
+    rep_off = np.zeros(len(reps) + 1, np.int64)
+    np.cumsum([len(r[0]) for r in reps], out=rep_off[1:])
+    np.savez_compressed(os.path.join(HERE, "binned_cosine.npz"), **_csr_arrays(csr),
+                        rep_off=rep_off, rep_mz=np.concatenate([r[0] for r in reps]),
+                        rep_int=np.concatenate([r[1] for r in reps]), mz_space=np.float64(bench.mz_space),
+                        cos=np.array(cos, np.float64), avg=np.array(avg, np.float64),
+                        status=np.array(status, np.int32))
+    print(f"binned_cosine: {len(clusters)} clusters, {len(cos)} members")
+
+
 def main():
     if not os.path.isdir(REF_SRC):
         raise SystemExit("reference not present; fixtures are committed under tests/golden/")
@@ -418,6 +500,7 @@ def main():
     gen_precursor_helpers(asc)
     gen_pairwise()
     gen_medoid(msr)
+    gen_binned_cosine()
 
 
 if __name__ == "__main__":

@@ -86,3 +86,15 @@ def test_medoid_oracle_matches_reference(impl):
     else:
         rep = c_oracle.medoid(csr, dense_tables=(impl == "c_dense"))
     np.testing.assert_array_equal(rep, z["rep_index"])
+
+
+def test_binned_cosine_oracle_matches_reference():
+    """benchmark.py cos_dist / average_cos_dist, run by the reference itself
+    (scipy binned_statistic) vs the numpy restatement: identical values."""
+    z, csr = load_golden("binned_cosine.npz")
+    cos, avg, status = np_oracle.binned_cosine(csr, z["rep_off"], z["rep_mz"], z["rep_int"], float(z["mz_space"]))
+    np.testing.assert_array_equal(status, z["status"])
+    np.testing.assert_array_equal(cos, z["cos"])
+    np.testing.assert_array_equal(avg, z["avg"])
+    # the golden holds the edge cases it claims: an on-edge member peak, cos 0 and 1, no members
+    assert np.any(z["cos"] == 0.0) and np.any(np.isclose(z["cos"], 1.0)) and np.any(z["avg"] == 0.0)
