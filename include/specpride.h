@@ -16,6 +16,8 @@
  *   spx_xcorr_distance <- src/most_similar_representative.py:13-19 distance() per pair
  *   spx_binned_cosine  <- src/benchmark.py:10-38  bin_proc / cos_dist / average_cos_dist
  *                       (representative vs its cluster members)
+ *   spx_best_score   <- src/best_spectrum.py:67-100  get_best_representative
+ *                       (called per cluster from best_spectrum():170-174)
  *   spx_compact_peaks   (packing helper for the shims' output writers)
  *
  * Conventions
@@ -157,6 +159,20 @@ typedef struct spx_cosine_params {
 int spx_binned_cosine(const spx_csr *csr, const int64_t *rep_off, const double *rep_mz, const double *rep_inten,
                       const spx_cosine_params *params, double *cos_out, double *avg_out, int32_t *status,
                       void *stream);
+
+/* ---- best spectrum: best_spectrum.get_best_representative(cluster, scores) for every
+ *      cluster: scores.idxmax() over the cluster's members (best_spectrum.py:97-100) ---- */
+
+/* Only csr->n_clusters / n_spectra / cluster_off are read (no peaks).  Per spectrum
+ * (device arrays [n_spectra]): score = the max non-NaN PSM score of its USI (NaN if
+ * every PSM score is NaN), rank = the USI's position among the sorted distinct score
+ * USIs (the order of get_scores()' sort_index, best_spectrum.py:64), -1 = no PSM.
+ * best[c] = global index of the member with the highest score, ties to the lowest
+ * rank (idxmax = first maximum in sorted-USI order); -1 if none.  status[c]:
+ * SPX_EMPTY if no member has a PSM (the reference's ValueError, :98-99), SPX_NON_FINITE
+ * if every matching score is NaN (pandas' idxmax returns NaN -> KeyError). */
+int spx_best_score(const spx_csr *csr, const double *score, const int64_t *rank, int64_t *best, int32_t *status,
+                   void *stream);
 
 /* Pack the per-cluster outputs densely: dst[out_off[c] + k] = src[spec_off[cluster_off[c]] + k]
  * for k < count[c]; out_off is the exclusive prefix sum of count (device array [C+1]). */

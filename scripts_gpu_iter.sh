@@ -1,20 +1,14 @@
 #!/bin/bash
-# Iteration loop: parity tests -> bench -> phase ablation -> per-kernel stats.
+# Iteration loop: GPU parity tests, then the bench and a bin-mean variant/phase timing.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
-echo "pytest rc=$?" >> gpurun_out/gpu_tests.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?
 tail -3 gpurun_out/gpu_tests.log
-grep -q "pytest rc=0" gpurun_out/gpu_tests.log || { grep -E "^(FAILED|E  )" gpurun_out/gpu_tests.log | head -30; exit 1; }
+[ $rc -eq 0 ] || { grep -E "^(FAILED|E  )" gpurun_out/gpu_tests.log | head -30; exit 1; }
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
-tail -1 gpurun_out/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['kernels'], d['roofline']['frac'])"
-timeout -k 10 300 python tools/profile_phases.py > gpurun_out/phases.json 2>gpurun_out/phases.err || { tail -5 gpurun_out/phases.err; exit 1; }
+tail -1 gpurun_out/bench.log
+SPX_VARIANTS=${SPX_VARIANTS:-7,0} timeout -k 10 300 python tools/profile_phases.py > gpurun_out/phases.json 2>gpurun_out/phases.err || { tail -5 gpurun_out/phases.err; exit 1; }
 cat gpurun_out/phases.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_plain -o run -- python3 tools/profile_phases.py plain > gpurun_out/prof_plain.log 2>&1 || { tail -5 gpurun_out/prof_plain.log; exit 1; }
-timeout -k 10 400 python tools/bench_medoid_large.py --check > gpurun_out/medoid_large.log 2>&1 || { tail -5 gpurun_out/medoid_large.log; exit 1; }
-tail -1 gpurun_out/medoid_large.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_md -o run -- python3 tools/bench_medoid_large.py > gpurun_out/prof_md.log 2>&1 || { tail -5 gpurun_out/prof_md.log; exit 1; }
-echo done

@@ -28,6 +28,7 @@
 //
 // HBM traffic per cluster: mz + inten once from HBM (16 B/peak; phase 3 re-reads
 // the m/z that phase 1 pulled into L2/MALL), 16 B per output peak, offsets.
+#pragma once
 #include "spx_device.hpp"
 
 namespace spx {
@@ -54,6 +55,10 @@ struct BinMeanState {
   int dcap;
   int nmax;  // clusters with more spectra are deferred (leaf-only pairwise mean)
 };
+
+#ifndef SPX_BM_PF
+#define SPX_BM_PF 12  // spectra in flight per thread in the fast path's register ring
+#endif
 
 constexpr int BM_BLOCK = 256;
 constexpr int BM_WMAX = 1536;  // 98,304 bins
@@ -222,10 +227,14 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
       const int lane = lane_id(), wid = wave_id();
       constexpr int NW = BM_BLOCK / kWave;
       int bad = 0;
-      constexpr int PF = 8;
-      Pk A[PF], B[PF];
+      // Rolling register ring: slot j holds spectrum jb + j and is refilled with
+      // spectrum jb + j + PF right after it is read, so every load has PF steps
+      // to land.  (A double buffer copied at the end of each batch would make
+      // the copy wait for the whole next batch's loads: s_waitcnt vmcnt(0).)
+      constexpr int PF = SPX_BM_PF;
+      Pk R[PF];
 #pragma unroll
-      for (int j = 0; j < PF; ++j) A[j] = fetch(j);
+      for (int j = 0; j < PF; ++j) R[j] = fetch(j);
       // spectrum j - 1 in flight: its slot (or -1), values, and lane 63's pending key
       int pslot = -1;
       int32_t pkey = 0;
@@ -233,15 +242,14 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
       double pm = 0.0, pit = 0.0;
       for (int64_t jb = 0; jb < n; jb += PF) {
 #pragma unroll
-        for (int j = 0; j < PF; ++j) B[j] = fetch(jb + PF + j);
-#pragma unroll
         for (int j = 0; j < PF; ++j) {
           if (jb + j < n) {  // uniform
             const int64_t js = jb + j;
             const int par = (int)(js & 1);
             const int len = S.soff[js + 1] - S.soff[js];
             const bool active = tid < len, has_next = tid + 1 < len;
-            const Pk& q = A[j];
+            const Pk q = R[j];
+            R[j] = fetch(js + PF);
             bad |= active && (q.m != q.m);
             const bool inr = active && in_range(q.m, P);
             int32_t key = q.m < P.minimum ? -1 : 0x7fffffff;
@@ -272,8 +280,6 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
             pit = q.it;
           }
         }
-#pragma unroll
-        for (int j = 0; j < PF; ++j) A[j] = B[j];
       }
       if (pcheck) {
         const int32_t kx = S.xch[(int)((n - 1) & 1) * NW + wid + 1];

@@ -41,7 +41,6 @@ struct GapParams {
   int32_t ablate;        // profiling only (SPX_ABLATE): stop after phase 1/2/3/4/5 (bits 1..16), 32 no precursor
 };
 
-enum : int32_t { kNonFinite = 4 };
 
 constexpr int GA_BLOCK = 512;  // 2 workgroups per CU (LDS): 16 waves
 constexpr int GA_NW = GA_BLOCK / kWave;

@@ -14,7 +14,10 @@
 #include <cstring>
 
 #include "../../include/specpride.h"
+#include "best_score.hip"
 #include "bin_mean_stream.hip"  // includes bin_mean.hip
+#include "bin_mean_wave.hip"
+#include "bin_mean_fast.hip"
 #include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
@@ -71,14 +74,21 @@ int32_t ablate_mask() {
   return e ? (int32_t)std::atoi(e) : 0;
 }
 
-// Bin-mean kernel: 0 = per-cluster two-pass LDS kernel (default, fastest
-// measured), 1 = per-bin list kernel, 2 = fold kernel, 3/4 = per-cluster hash
-// kernel (2048/4096 slots), 5 = persistent stream + hash fold, 6 = persistent
-// stream + bitmap-rank fold (DESIGN.md §3 has the measurements).
-// SPX_BIN_KERNEL selects (A/B profiling).
-int bin_kernel_variant() {
+// Bin-mean kernel: 0 = per-cluster two-pass LDS kernel (default: fastest
+// measured), 7 = wave-private bin ranges with no per-spectrum barrier,
+// 8 = buffer-load / float2 variant of 0 (7 and 8 derive counts from the m/z
+// sums, so they run only where bin_counts_derivable holds), 1 = per-bin list
+// kernel, 2 = fold kernel, 3/4 = per-cluster hash kernel (2048/4096 slots),
+// 5 = persistent stream + hash fold, 6 = persistent stream + bitmap-rank fold
+// (DESIGN.md §3 has the measurements).  SPX_BIN_KERNEL selects (A/B profiling).
+bool bin_counts_derivable(const spx_bin_params* p) {
+  return p->minimum > 0.0 && 128.0 * (p->binsize / p->minimum) + 128.0 * 128.0 * 0x1p-23 < 0.45;
+}
+
+int bin_kernel_variant(const spx_bin_params* p) {
   const char* e = std::getenv("SPX_BIN_KERNEL");
-  return e ? std::atoi(e) : 0;
+  const int v = e ? std::atoi(e) : 0;
+  return ((v == 7 || v == 8) && !bin_counts_derivable(p)) ? 0 : v;
 }
 
 // Workgroups of the persistent bin-mean kernel: BS_BLOCKS_PER_CU per CU (its
@@ -162,7 +172,7 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   // the range (weight / G + one cluster) well below 2^28 peaks
   const int64_t wtot = csr->n_peaks + 64 * csr->n_spectra + 1024 * C;
   const bool range_ok = wtot / G + info->max_cluster_peaks + 64 * info->max_cluster_spectra + 1024 < (int64_t(1) << 28);
-  const int bv = bin_kernel_variant();
+  const int bv = bin_kernel_variant(params);
   if ((bv == 5 || bv == 6) && P.n_words <= spx::BM_WMAX && range_ok) {
     const unsigned pg = (unsigned)std::min<int64_t>((C + 1 + 255) / 256, 1024);
     hipLaunchKernelGGL(spx::range_plan_kernel, dim3(pg), dim3(256), 0, s, V, (int32_t)G, plan);
@@ -174,19 +184,27 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
       hipLaunchKernelGGL(spx::bin_mean_stream_kernel<spx::BS_H>, dim3((unsigned)G), dim3(spx::BM_BLOCK), 0, s, V, P,
                          O, prec_out, charge_out, status, def, n_def, plan);
     if (int rc = check_launch("bin_mean_stream_kernel")) return rc;
-  } else if (bin_kernel_variant() == 3 || bin_kernel_variant() == 4) {
-    if (bin_kernel_variant() == 3)
+  } else if (bv == 8) {
+    hipLaunchKernelGGL(spx::bin_mean_fast_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                       charge_out, status, def, n_def);
+    if (int rc = check_launch("bin_mean_fast_kernel")) return rc;
+  } else if (bv == 7) {
+    hipLaunchKernelGGL(spx::bin_mean_wave_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                       charge_out, status, def, n_def);
+    if (int rc = check_launch("bin_mean_wave_kernel")) return rc;
+  } else if (bv == 3 || bv == 4) {
+    if (bv == 3)
       hipLaunchKernelGGL(spx::bin_mean_hash_kernel<2048>, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O,
                          prec_out, charge_out, status, def, n_def);
     else
       hipLaunchKernelGGL(spx::bin_mean_hash_kernel<4096>, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O,
                          prec_out, charge_out, status, def, n_def);
     if (int rc = check_launch("bin_mean_hash_kernel")) return rc;
-  } else if (bin_kernel_variant() == 2) {
+  } else if (bv == 2) {
     hipLaunchKernelGGL(spx::bin_mean_fold_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                        charge_out, status, def, n_def);
     if (int rc = check_launch("bin_mean_fold_kernel")) return rc;
-  } else if (bin_kernel_variant() == 1) {
+  } else if (bv == 1) {
     hipLaunchKernelGGL(spx::bin_mean_list_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                        charge_out, status, def, n_def);
     if (int rc = check_launch("bin_mean_list_kernel")) return rc;
@@ -375,6 +393,21 @@ extern "C" int spx_binned_cosine(const spx_csr* csr, const int64_t* rep_off, con
                      reinterpret_cast<hipStream_t>(stream), view(csr), P, rep_off, rep_mz, rep_inten, cos_out, avg_out,
                      status);
   return check_launch("binned_cosine_kernel");
+}
+
+// --------------------------------------------------------- best spectrum
+extern "C" int spx_best_score(const spx_csr* csr, const double* score, const int64_t* rank, int64_t* best,
+                              int32_t* status, void* stream) {
+  if (!csr || csr->n_clusters < 0 || !csr->cluster_off || !best || !status ||
+      (csr->n_spectra > 0 && (!score || !rank)))
+    return fail(SPX_EINVAL, "spx_best_score: null argument");
+  const int64_t C = csr->n_clusters;
+  if (C == 0) return SPX_SUCCESS;
+  const int64_t blocks = (C + spx::BEST_WAVES - 1) / spx::BEST_WAVES;
+  if (blocks > INT32_MAX) return fail(SPX_EINVAL, "spx_best_score: too many clusters");
+  hipLaunchKernelGGL(spx::best_score_kernel, dim3((unsigned)blocks), dim3(spx::BEST_WAVES * spx::kWave), 0,
+                     reinterpret_cast<hipStream_t>(stream), C, csr->cluster_off, score, rank, best, status);
+  return check_launch("best_score_kernel");
 }
 
 // ---------------------------------------------------------------- compaction

@@ -45,7 +45,7 @@ struct PeaksOut {
   int64_t* __restrict__ count;
 };
 
-enum : int32_t { kOk = 0, kMixedCharge = 1, kNoGap = 2, kEmpty = 3, kDeferred = 100 };
+enum : int32_t { kOk = 0, kMixedCharge = 1, kNoGap = 2, kEmpty = 3, kNonFinite = 4, kDeferred = 100 };
 
 // --------------------------------------------------------- wave primitives
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }

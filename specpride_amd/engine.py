@@ -255,3 +255,34 @@ def binned_cosine(batch: DeviceBatch, rep_off, rep_mz, rep_int, mz_space=MZ_SPAC
                                             ctypes.byref(prm), _ptr(out.cos), _ptr(out.avg), _ptr(out.status),
                                             _stream_handle(stream)), "spx_binned_cosine")
     return out
+
+
+@dataclass
+class BestScoreResult:
+    best: object    # [C] i64: global spectrum index of the highest-scoring member (-1: none)
+    status: object  # [C] i32 (STATUS_EMPTY: no member has a PSM; STATUS_NON_FINITE: only NaN scores)
+
+    def to_host(self):
+        return self.best.cpu().numpy(), self.status.cpu().numpy()
+
+
+def best_score(cluster_off, score, rank, out: Optional[BestScoreResult] = None, stream=None) -> BestScoreResult:
+    """get_best_representative (best_spectrum.py:67-100) for every cluster at once.
+
+    Device tensors: ``cluster_off`` [C+1] i64 over the member spectra, ``score``
+    [S] f64 (max non-NaN PSM score per spectrum's USI), ``rank`` [S] i64 (the USI's
+    position in sorted order, -1 = no PSM).  Only offsets are needed, no peaks."""
+    import torch
+
+    C = int(cluster_off.numel()) - 1
+    S = int(score.numel())
+    if C < 0 or int(rank.numel()) != S:
+        raise ValueError("best_score: cluster_off must have C+1 entries and score/rank one per spectrum")
+    dev = cluster_off.device
+    if out is None:
+        out = BestScoreResult(torch.empty(max(C, 1), dtype=torch.int64, device=dev),
+                              torch.empty(max(C, 1), dtype=torch.int32, device=dev))
+    csr = _lib.SpxCsr(C, S, 0, _ptr(cluster_off), _ptr(cluster_off), None, None, None, None, None)
+    _lib.check(_lib.lib().spx_best_score(ctypes.byref(csr), _ptr(score), _ptr(rank), _ptr(out.best),
+                                         _ptr(out.status), _stream_handle(stream)), "spx_best_score")
+    return out

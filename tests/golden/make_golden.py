@@ -19,6 +19,7 @@ Fixtures:
   medoid_<set>.npz          most_similar_representative.main() reps (most_similar_representative.py:22-115)
   pairwise_sum.npz          numpy pairwise summation (the reduction pandas .sum() runs)
   binned_cosine.npz         cos_dist / average_cos_dist per cluster (benchmark.py:10-38)
+  best_spectrum_*           best_spectrum() end to end + get_best_representative (best_spectrum.py:43-175)
 """
 from __future__ import annotations
 
@@ -490,10 +491,113 @@ def gen_binned_cosine():
     print(f"binned_cosine: {len(clusters)} clusters, {len(cos)} members")
 
 
+# ----------------------------------------------------------- best spectrum
+def best_spectrum_cases(rng):
+    """An MGF of clusters (members interleaved across the file) and a MaxQuant
+    msms.txt: duplicate PSMs per scan, NaN scores, unscored members, equal
+    scores across USIs (ties: first USI in string order, 'scan:10' < 'scan:9')."""
+    raws = ["runB", "runA", "run_10", "run_9"]
+    spectra, rows = [], []
+    n_clusters = 60
+    members = {c: [] for c in range(n_clusters)}
+    scan = 0
+    for c in range(n_clusters):
+        for _ in range(int(rng.integers(1, 9))):
+            members[c].append((raws[int(rng.integers(0, len(raws)))], scan))
+            scan += int(rng.integers(1, 4))
+    order = [(c, r, sc) for c in members for r, sc in members[c]]
+    perm = rng.permutation(len(order))  # non-contiguous clusters
+    order = [order[i] for i in perm]
+    for c, r, sc in order:
+        npk = int(rng.integers(1, 5))
+        mz = np.sort(np.round(rng.uniform(100, 1500, npk), 4))
+        it = np.round(rng.lognormal(4, 1, npk), 2)
+        spectra.append((f"cluster-{c}", f"mzspec:PXD004732:{r}.raw::scan:{sc}", mz, it,
+                        float(np.round(rng.uniform(400, 1200), 4)), int(rng.integers(2, 4)),
+                        float(np.round(rng.uniform(0, 3600), 3))))
+        kind = c % 6
+        if kind == 0:  # unscored cluster -> skipped (ValueError)
+            continue
+        k = int(rng.integers(0, 4))
+        for _ in range(k if kind != 5 else max(k, 1)):
+            v = float(rng.integers(0, 4)) * 10.0  # few distinct values: many ties
+            if kind == 4 and rng.random() < 0.5:
+                v = float("nan")
+            rows.append((r, sc, v))
+    # a cluster whose PSM scores are all NaN crashes the reference (KeyError, pinned
+    # separately below): give every scored cluster one real score
+    usi_cluster = {(r, sc): c for c, r, sc in order}
+    real = {usi_cluster[(r, sc)] for r, sc, v in rows if v == v}
+    for c in sorted({usi_cluster[(r, sc)] for r, sc, _ in rows} - real):
+        rows.append((members[c][0][0], members[c][0][1], 20.0))
+    # PSMs for scans that are in no cluster
+    rows += [("runZ", 99999, 50.0), ("runA", 88888, float("nan"))]
+    rows = [rows[i] for i in rng.permutation(len(rows))]
+    return spectra, rows
+
+
+def _write_best_inputs(spectra, rows, mgf_path, msms_path):
+    with open(mgf_path, "w") as fh:
+        for cl, usi, mz, it, pm, z, rt in spectra:
+            fh.write(f"BEGIN IONS\nTITLE={cl};{usi}\nPEPMASS={pm!r}\nCHARGE={z}+\nRTINSECONDS={rt!r}\n")
+            fh.write("".join(f"{float(a)!r} {float(b)!r}\n" for a, b in zip(mz, it)))
+            fh.write("END IONS\n\n")
+    with open(msms_path, "w") as fh:
+        fh.write("Raw file\tScan number\tSequence\tScore\n")
+        for r, sc, v in rows:
+            fh.write(f"{r}\t{sc}\tPEPTIDEK\t{'NaN' if v != v else repr(v)}\n")
+
+
+def gen_best_spectrum():
+    import importlib
+    from types import SimpleNamespace
+
+    from specpride_amd.mgf import iter_mgf
+
+    bs = importlib.import_module("best_spectrum")
+    written = []
+    # pyteomics.mgf is absent: its reader is replaced by the build's (parse parity is
+    # not what this pins); write() captures the reference's spectrum dicts
+    bs.mgf = SimpleNamespace(read=lambda fn: iter_mgf(fn), write=lambda sp, fh: written.extend(sp))
+    rng = np.random.default_rng(23)
+    spectra, rows = best_spectrum_cases(rng)
+    mgf_path = os.path.join(HERE, "best_spectrum_in.mgf")
+    msms_path = os.path.join(HERE, "best_spectrum_msms.txt")
+    _write_best_inputs(spectra, rows, mgf_path, msms_path)
+    with tempfile.TemporaryDirectory() as td:
+        bs.best_spectrum(mgf_path, os.path.join(td, "out.mgf"), msms_path)
+    out = [{"title": d["params"]["title"], "pepmass": float(d["params"]["pepmass"]),
+            "rtinseconds": float(d["params"]["rtinseconds"]), "charge": int(d["params"]["charge"]),
+            "mz": [float(x) for x in d["m/z array"]], "intensity": [float(x) for x in d["intensity array"]]}
+           for d in written]
+    # per cluster (split_into_clusters order): the chosen USI or the exception type
+    scores = bs.get_scores(msms_path)
+    per_cluster = []
+    for cl in bs.split_into_clusters(bs.get_cluster_spectra(mgf_path)):
+        try:
+            per_cluster.append(bs.get_best_representative(cl, scores).identifier)
+        except ValueError:
+            per_cluster.append("ValueError")
+    # a cluster whose only PSM scores are NaN: idxmax -> nan, spectra[nan] -> KeyError
+    nan_cluster = {u: SimpleNamespace(identifier=u) for u in ["mzspec:PXD004732:runA.raw::scan:88888"]}
+    try:
+        bs.get_best_representative(nan_cluster, scores)
+        nan_case = "no error"
+    except KeyError:
+        nan_case = "KeyError"
+    with open(os.path.join(HERE, "best_spectrum.json"), "w") as fh:
+        json.dump({"output": out, "per_cluster": per_cluster, "nan_only_cluster": list(nan_cluster),
+                   "nan_only_result": nan_case}, fh, indent=0)
+    print(f"best_spectrum: {len(per_cluster)} clusters, {len(out)} representatives, nan case {nan_case}")
+
+
 def main():
     if not os.path.isdir(REF_SRC):
         raise SystemExit("reference not present; fixtures are committed under tests/golden/")
     binning, asc, msr = _import_reference()
+    if sys.argv[1:] == ["best_spectrum"]:  # regenerate one set only
+        gen_best_spectrum()
+        return
     gen_bin_mean(binning)
     gen_bin_mean_cli()
     gen_gap_average(asc)
@@ -501,6 +605,7 @@ def main():
     gen_pairwise()
     gen_medoid(msr)
     gen_binned_cosine()
+    gen_best_spectrum()
 
 
 if __name__ == "__main__":

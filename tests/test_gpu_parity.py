@@ -232,11 +232,11 @@ def test_medoid_large_path_skewed_unsorted_and_empty(gpu):
     np.testing.assert_array_equal(tot, ref_tot)
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6"])
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5", "6", "7", "8"])
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_bin_mean_kernel_variants(gpu, synth, monkeypatch, name, variant):
-    """The per-bin list kernel (SPX_BIN_KERNEL=1) and the fold kernel (=2) meet
-    the same bit-exact bar as the default kernel."""
+    """Every bin-mean kernel variant (SPX_BIN_KERNEL, spx_api.hip) meets the same
+    bit-exact bar as the default kernel."""
     monkeypatch.setenv("SPX_BIN_KERNEL", variant)
     z, csr = load_golden(f"bin_mean_{name}.npz")
     ref = dict(status=z["status"], out_off=z["out_off"], out_mz=z["out_mz"], out_int=z["out_int"],
@@ -298,3 +298,58 @@ def test_bin_mean_stream_many_clusters_per_workgroup(gpu, monkeypatch, variant):
     csr = _concat(*parts)
     assert csr.n_clusters > 5 * 1280
     assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
+
+
+def _wave_edge_batch():
+    """Shapes that stress bin_mean_wave_kernel's wave ranges: spectra longer than a
+    wave's 64-peak chunk inside one range, clusters of 100-128 spectra, every peak
+    in one bin (D = 1: three empty ranges), no in-range peak (D = 0), empty spectra
+    inside a cluster, repeated bins inside a spectrum (last wins), peaks on the
+    range ends (min, just below max, max itself)."""
+    rng = np.random.default_rng(77)
+    clusters = []
+    # long spectra: 900 sorted peaks over a narrow window -> runs of >> 64 per wave
+    clusters.append([{"m/z array": np.sort(rng.uniform(500, 540, 900)), "intensity array": rng.lognormal(3, 1, 900),
+                      "precursor mz": 600.0 + k, "precursor charge": 2} for k in range(5)])
+    # 100..128 spectra of ~60 peaks
+    for nspec in (100, 127, 128):
+        t = np.sort(rng.uniform(100, 2000, 60))
+        clusters.append([{"m/z array": np.sort(t + rng.normal(0, 0.003, 60)), "intensity array": rng.lognormal(5, 1, 60),
+                          "precursor mz": 700.0, "precursor charge": 3} for _ in range(nspec)])
+    # every peak in one bin
+    clusters.append([{"m/z array": np.array([300.001, 300.005, 300.011]), "intensity array": np.array([1.0, 2.0, 3.0]),
+                      "precursor mz": 500.0, "precursor charge": 2} for _ in range(7)])
+    # nothing in range
+    clusters.append([{"m/z array": np.array([50.0, 99.99, 2000.0, 2500.0]), "intensity array": np.ones(4),
+                      "precursor mz": 500.0, "precursor charge": 2} for _ in range(3)])
+    # empty spectra between full ones, repeated bins, range ends
+    ends = np.array([100.0, 100.0, 100.019, 1234.5671, 1234.5672, 1999.99999, 2000.0])
+    clusters.append([{"m/z array": ends, "intensity array": np.arange(1.0, 8.0), "precursor mz": 400.0,
+                      "precursor charge": 2},
+                     {"m/z array": np.zeros(0), "intensity array": np.zeros(0), "precursor mz": 401.0,
+                      "precursor charge": 2},
+                     {"m/z array": ends + 0.001, "intensity array": np.arange(2.0, 9.0), "precursor mz": 402.0,
+                      "precursor charge": 2},
+                     {"m/z array": np.zeros(0), "intensity array": np.zeros(0), "precursor mz": 403.0,
+                      "precursor charge": 2}])
+    return SpectraCSR.from_clusters(clusters)
+
+
+@pytest.mark.parametrize("variant", ["8", "7", "0"])
+def test_bin_mean_wave_kernel_edges(gpu, monkeypatch, variant):
+    monkeypatch.setenv("SPX_BIN_KERNEL", variant)
+    csr = _wave_edge_batch()
+    assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
+    assert_bin_mean_equal(_bin_mean(csr), np_oracle.bin_mean(csr))
+
+
+@pytest.mark.parametrize("variant", ["8", "7"])
+def test_bin_mean_wave_kernel_skewed_and_unsorted(gpu, monkeypatch, variant):
+    """Skewed sizes (>128 spectra -> deferred) and shuffled spectra (deferred) mixed
+    with regular clusters in one launch: bit-exact against the oracle."""
+    monkeypatch.setenv("SPX_BIN_KERNEL", variant)
+    csr = make_clusters_np(400, seed=91, skewed=True)
+    csr = csr.select([c for c in range(csr.n_clusters) if csr.cluster_off[c + 1] - csr.cluster_off[c] <= 300])
+    assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
+    sub = _shuffled(csr.select(range(120)))
+    assert_bin_mean_equal(_bin_mean(sub), c_oracle.bin_mean(sub))
