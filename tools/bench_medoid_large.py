@@ -49,10 +49,19 @@ def main():
     ms = ev[0].elapsed_time(ev[1]) / args.reps
     # algorithmic Gram work of the large (n > 64) clusters: 2 * n(n+1)/2 * K_c with K_c <= peaks
     big = np.flatnonzero(sizes > 64)
+    # 2 * n(n+1)/2 * K_c int ops per large cluster, K_c = its distinct
+    # ceil(mz / 0.1) bins (the Gram's K); the MFMA kernel's time comes from rocprofv3
+    mz = t["mz"].cpu().numpy()
+    so = batch.host_spec_off
+    gram_ops = 0
+    for c in big:
+        a, b = so[batch.host_cluster_off[c]], so[batch.host_cluster_off[c + 1]]
+        k_c = len(np.unique(np.ceil(mz[a:b] / 0.1)))
+        gram_ops += int(sizes[c]) * (int(sizes[c]) + 1) * k_c
     out = {"clusters": int(batch.n_clusters), "spectra": int(batch.n_spectra), "peaks": int(batch.n_peaks),
            "large_clusters": int(len(big)), "max_n": int(sizes.max()),
            "spectra_in_large": int(sizes[big].sum()), "medoid_ms": round(ms, 3),
-           "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1)}
+           "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1), "gram_ops": gram_ops}
     if args.check:
         from oracle import c_oracle
         from specpride_amd.csr import SpectraCSR
