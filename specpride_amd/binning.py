@@ -18,6 +18,18 @@ Kept from the reference (same names, arguments, return shapes, errors):
   (default ``merged_spectra.mgf``), ``--verbose``, ``--version``; exit 10
   without ``--mgf_file``; nothing is written if a cluster fails.
 
+mzML + MaRaCluster input path:
+
+* ``.read_cluster_list(file)`` (binning.py:35-52): a cluster ends at each blank
+  line (a trailing cluster with no blank line after it is dropped, as there);
+  column 2 of each line is the scan number (kept as a string).
+* ``.read_spectra(mzml_file, scan_list)`` (binning.py:57-119): MS2 peaklists
+  by Thermo scan id from a plain or ``.gz`` mzML (``specpride_amd.mzml``, a
+  pyteomics stand-in), same INFO/ERROR prints.
+* CLI ``--mara_file`` / ``--mzml_file`` / ``--cluster``: the options the
+  reference keeps commented out (binning.py:253-255, 281-282), run over every
+  cluster (or one) in a single GPU pass; titles are the cluster numbers.
+
 Added: ``.combine_bin_mean_batch(clusters, ...)`` -- all clusters in one GPU
 pass (the CLI uses it).  There is no CPU fallback: without the HIP engine the
 numeric calls raise.
@@ -26,6 +38,7 @@ from __future__ import annotations
 
 import argparse
 import sys
+import timeit
 
 import numpy as np
 
@@ -46,6 +59,56 @@ class RepresentativeSpectrumCreator:
     def __init__(self, verbose=None):
         self.verbose = 0 if verbose is None else verbose
         self.device = "cuda"
+
+    # ----------------------------------------------------- mzML + MaRaCluster
+    def read_cluster_list(self, file):
+        """MaRaCluster TSV -> list of clusters, each a list of scan strings (binning.py:35-52)."""
+        clusters, cluster = [], []
+        with open(file) as infile:
+            for line in infile:
+                columns = line.rstrip().split()
+                if len(columns) == 0:
+                    clusters.append(cluster)
+                    cluster = []
+                    continue
+                cluster.append(columns[1])
+        return clusters
+
+    def read_spectra(self, mzml_file, scan_list, reader=None):
+        """MS2 peaklists for ``scan_list`` from an mzML file (binning.py:57-119)."""
+        from . import mzml
+
+        t0 = timeit.default_timer()
+        n_spectra = 0
+        if self.verbose >= 1:
+            eprint(f"INFO: Reading {len(scan_list)} scans from mzML file {mzml_file}")
+        spectra = []
+        rd = reader if reader is not None else mzml.read(mzml_file)
+        for scan in scan_list:
+            spectrum = rd.get_by_id(f"controllerType=0 controllerNumber=1 scan={scan}")
+            if spectrum["ms level"] == 2 and "m/z array" in spectrum:
+                ion = spectrum["precursorList"]["precursor"][0]["selectedIonList"]["selectedIon"][0]
+                precursor_mz, precursor_charge = ion["selected ion m/z"], ion["charge state"]
+                print(f"INFO: Reading {scan}. Precursor m/z = {precursor_mz}. n peaks={len(spectrum['m/z array'])}")
+                spectra.append({"m/z array": spectrum["m/z array"], "intensity array": spectrum["intensity array"],
+                                "precursor mz": precursor_mz, "precursor charge": precursor_charge})
+            else:
+                print(f"ERROR: scan {scan} is not ms_level=2! Skipping")
+            n_spectra += 1
+        if self.verbose >= 1:
+            eprint("")
+        t1 = timeit.default_timer()
+        print(f"INFO: Read {n_spectra} spectra from {mzml_file}")
+        print(f"INFO: Elapsed time: {t1 - t0}")
+        print(f"INFO: Processed {n_spectra / max(t1 - t0, 1e-12)} spectra per second")
+        return spectra
+
+    def read_spectra_clusters(self, mzml_file, clusters):
+        """read_spectra for several scan lists with ONE parse of the mzML file."""
+        from . import mzml
+
+        rd = mzml.read(mzml_file)
+        return [self.read_spectra(mzml_file, scans, reader=rd) for scans in clusters]
 
     # ------------------------------------------------------------- MGF input
     def read_spectra_clustered_mgf(self, clustered_mgf_file):
@@ -107,10 +170,24 @@ def main(argv=None):
     argparser = argparse.ArgumentParser(description="Creates an index for an MSP spectral library file")
     argparser.add_argument("--verbose", action="count", help="If set, print more information about ongoing processing")
     argparser.add_argument("--version", action="version", version="%(prog)s 0.5")
+    argparser.add_argument("--mara_file", action="store", help="Name of the mara clusters file")
+    argparser.add_argument("--mzml_file", action="store", help="Name of the mzml file")
+    argparser.add_argument("--cluster", action="store", help="Cluster number to combine (default: all)")
     argparser.add_argument("--mgf_file", action="store", help="Name of the clustered MGF file")
     argparser.add_argument("--out", action="store", default="merged_spectra.mgf", help="Name of the output mgf file")
     params = argparser.parse_args(argv)
     verbose = 1 if params.verbose is None else params.verbose
+    if not params.mgf_file and params.mara_file and params.mzml_file:
+        rsc = RepresentativeSpectrumCreator(verbose=verbose)
+        clusters = rsc.read_cluster_list(params.mara_file)
+        ids = [int(params.cluster)] if params.cluster is not None else list(range(len(clusters)))
+        peaklists = rsc.read_spectra_clusters(params.mzml_file, [clusters[i] for i in ids])
+        merged = rsc.combine_bin_mean_batch(peaklists, minimum=100, maximum=2000, binsize=0.02)
+        for cid, spec in zip(ids, merged):
+            spec["cluster_id"] = str(cid)
+        with open(params.out, "wt") as mgf_file:
+            rsc.write_spectrum(merged, mgf_file)
+        return
     if not params.mgf_file:
         print("Example: representative_spectrum_creator.py --mgf_file=../data/clustered_mgf.mgf")
         print("Or use --help for additional usage information")

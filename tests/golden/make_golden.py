@@ -20,6 +20,8 @@ Fixtures:
   pairwise_sum.npz          numpy pairwise summation (the reduction pandas .sum() runs)
   binned_cosine.npz         cos_dist / average_cos_dist per cluster (benchmark.py:10-38)
   best_spectrum_*           best_spectrum() end to end + get_best_representative (best_spectrum.py:43-175)
+  maracluster_*             binning.read_cluster_list (binning.py:35-52) and convert_mgf_cluster.py's
+                            read_clusters / read_peptides / buid_usi_accession / convert-mq-marcluster (:14-79)
 """
 from __future__ import annotations
 
@@ -591,12 +593,67 @@ def gen_best_spectrum():
     print(f"best_spectrum: {len(per_cluster)} clusters, {len(out)} representatives, nan case {nan_case}")
 
 
+# ------------------------------------------------ MaRaCluster / convert_mgf_cluster
+MARA_TSV = ("run.raw\t11\t0.5\nrun.raw\t3\t0.5\nrun.raw\t7\t0.1\n\n"
+            "run.raw\t5\t0.2\n\n\nrun.raw\t012\t0.3\nrun.raw\t1\t0.3\n\n"
+            "run.raw\t20\t0.9\nrun.raw\t21\t0.9\n")  # double blank line; last cluster has no blank after it
+MSMS_TXT = ("Raw file\tScan number\tx\ty\tz\tw\tv\tModified sequence\tScore\n"
+            "run\t11\ta\tb\tc\td\te\t_PEPTIDEK_\t50\n"
+            "run\t5\ta\tb\tc\td\te\t_M(ox)AAK_\t20\n"
+            "run\t11\ta\tb\tc\td\te\t_OTHERR_\t40\n"
+            "run\t20\ta\tb\tc\td\te\t_LASTK_\t10\n")
+
+
+def gen_maracluster(binning):
+    import importlib
+    from types import SimpleNamespace
+
+    from specpride_amd.mgf import iter_mgf
+
+    cmc = importlib.import_module("convert_mgf_cluster")
+    tsv = os.path.join(HERE, "maracluster_clusters.tsv")
+    msms = os.path.join(HERE, "maracluster_msms.txt")
+    mgf_in = os.path.join(HERE, "maracluster_in.mgf")
+    with open(tsv, "w") as fh:
+        fh.write(MARA_TSV)
+    with open(msms, "w") as fh:
+        fh.write(MSMS_TXT)
+    rng = np.random.default_rng(41)
+    with open(mgf_in, "w") as fh:  # scans 1..21 plus a duplicate title and a 'xscan=5' look-alike
+        for scan in list(range(1, 22)) + [11, 55]:
+            title = f"run.{scan}.{scan}.2 File:run.raw, NativeID:controllerType=0 controllerNumber=1 scan={scan}"
+            if scan == 55:
+                title = "run.55 NativeID:xscan=5"
+            mz = np.sort(np.round(rng.uniform(150, 1400, 4), 4))
+            fh.write(f"BEGIN IONS\nTITLE={title}\nPEPMASS={500 + scan}.25\nCHARGE={2 + scan % 2}+\n")
+            fh.write("".join(f"{a!r} {b!r}\n" for a, b in zip(mz, np.round(rng.lognormal(4, 1, 4), 2))))
+            fh.write("END IONS\n\n")
+    written = []
+    cmc.mgf = SimpleNamespace(read=lambda fn: iter_mgf(fn), write=lambda sp, out: written.extend(sp))
+    with contextlib.redirect_stdout(io.StringIO()):
+        cmc.convert_mq_mracluster_mgf.callback(msms, tsv, mgf_in, "unused.mgf", "PXD000001", "run")
+    rsc = binning.RepresentativeSpectrumCreator(verbose=0)
+    g = {"read_cluster_list": rsc.read_cluster_list(tsv),
+         "read_clusters": {str(k): v for k, v in cmc.read_clusters(tsv).items()},
+         "read_peptides": {str(k): v for k, v in cmc.read_peptides(msms).items()},
+         "usi": [cmc.buid_usi_accession("cluster-3", None, 7, "PXD1", "raw", 2),
+                 cmc.buid_usi_accession("cluster-3", "PEPK", 7, "PXD1", "raw", 2)],
+         "converted_titles": [sp["params"]["title"] for sp in written],
+         "converted_pepmass": [float(sp["params"]["pepmass"][0]) for sp in written]}
+    with open(os.path.join(HERE, "maracluster.json"), "w") as fh:
+        json.dump(g, fh, indent=0)
+    print(f"maracluster: {len(g['read_cluster_list'])} clusters, {len(written)} converted spectra")
+
+
 def main():
     if not os.path.isdir(REF_SRC):
         raise SystemExit("reference not present; fixtures are committed under tests/golden/")
     binning, asc, msr = _import_reference()
     if sys.argv[1:] == ["best_spectrum"]:  # regenerate one set only
         gen_best_spectrum()
+        return
+    if sys.argv[1:] == ["maracluster"]:
+        gen_maracluster(binning)
         return
     gen_bin_mean(binning)
     gen_bin_mean_cli()
@@ -606,6 +663,7 @@ def main():
     gen_medoid(msr)
     gen_binned_cosine()
     gen_best_spectrum()
+    gen_maracluster(binning)
 
 
 if __name__ == "__main__":

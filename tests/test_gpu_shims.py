@@ -161,3 +161,41 @@ def test_shard_driver_with_engine_over_rccl(gpu):
         np.testing.assert_array_equal(totals, want_tot)
     finally:
         dist.destroy_process_group()
+
+
+def test_binning_mzml_maracluster_cli(gpu, tmp_path):
+    """The mzML + MaRaCluster input path (binning.py:35-119, the CLI options the
+    reference keeps commented out): every cluster through one GPU pass, consensus
+    bit-exact against the oracle on the same spectra; an MS1 scan is skipped."""
+    from oracle import c_oracle
+    from specpride_amd import mgf_native, mzml
+
+    csr = make_clusters_np(12, seed=8)
+    spectra, tsv, scan = [], [], 100
+    for c in range(csr.n_clusters):
+        for s in range(csr.cluster_off[c], csr.cluster_off[c + 1]):
+            m, i = csr.spectrum(s)
+            spectra.append({"scan": scan, "ms level": 2, "m/z array": m, "intensity array": i,
+                            "precursor mz": float(csr.prec_mz[s]), "precursor charge": int(csr.charge[s])})
+            tsv.append(f"run.raw\t{scan}\t0.1\n")
+            scan += 1
+        tsv.append("\n")
+    spectra.append({"scan": 9999, "ms level": 1, "m/z array": np.array([150.0]), "intensity array": np.ones(1)})
+    tsv.insert(1, "run.raw\t9999\t0.1\n")  # the MS1 scan sits in cluster 0: skipped with an ERROR line
+    path, tpath, out = tmp_path / "run.mzML", tmp_path / "mara.tsv", tmp_path / "out.mgf"
+    mzml.write_mzml(str(path), spectra)
+    tpath.write_text("".join(tsv))
+    with contextlib.redirect_stdout(io.StringIO()) as so:
+        binning.main(["--mara_file", str(tpath), "--mzml_file", str(path), "--out", str(out)])
+    assert "ERROR: scan 9999 is not ms_level=2! Skipping" in so.getvalue()
+    # expected: the oracle on the same clusters (precursors as written to the mzML)
+    ref = c_oracle.bin_mean(csr)
+    merged = []
+    for c in range(csr.n_clusters):
+        a, b = ref["out_off"][c], ref["out_off"][c + 1]
+        merged.append({"cluster_id": str(c), "mzs": ref["out_mz"][a:b], "intensities": ref["out_int"][a:b],
+                       "precursor_mz": np.float64(ref["prec"][c]), "precursor_charge": int(ref["charge"][c])})
+    want = tmp_path / "want.mgf"
+    with open(want, "wt") as fh:
+        mgf_native.write_binning_mgf(merged, fh)
+    assert out.read_bytes() == want.read_bytes()
