@@ -47,6 +47,23 @@ struct PeaksOut {
 
 enum : int32_t { kOk = 0, kMixedCharge = 1, kNoGap = 2, kEmpty = 3, kNonFinite = 4, kDeferred = 100 };
 
+// ------------------------------------------------------------ buffer loads
+__device__ __forceinline__ double bf_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
+// buffer descriptor over n doubles at p, built from readfirstlane'd halves so
+// the compiler sees it wave-uniform (readfirstlane returns int: zero-extend the
+// low half, a sign-extended one would corrupt the base's upper bits)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bf_rsrc(const double* p, int n) {
+  const uint64_t a = (uint64_t)p;
+  const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(lo | (hi << 32)), (short)0,
+                                           __builtin_amdgcn_readfirstlane(n * 8), 0x00020000);
+}
+
+
 // --------------------------------------------------------- wave primitives
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 __device__ __forceinline__ int wave_id() { return threadIdx.x / kWave; }
