@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--check", type=int, default=0, help="compare the first N clusters with the numpy oracle")
+    ap.add_argument("--cpu-sample", type=int, default=20000, help="clusters timed on 1 host core (0: skip)")
     args = ap.parse_args()
     import torch
 
@@ -72,6 +73,21 @@ def main():
         out.update(check_clusters=int(sub.n_clusters),
                    check_status=bool(np.array_equal(got["status"], want["status"])),
                    check_counts=bool(np.array_equal(got["out_off"], want["out_off"])))
+    if args.cpu_sample > 0:
+        # the reference's CPU path (argsort + cumsum groups per cluster), restated in
+        # numpy (oracle/np_oracle.py), on 1 host core over a sample of the same law
+        import time
+
+        from oracle import np_oracle
+        from specpride_amd.synthetic import make_clusters_np
+
+        sample = make_clusters_np(args.cpu_sample, seed=args.seed + 7)
+        t0 = time.perf_counter()
+        np_oracle.gap_average(sample)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(args.cpu_sample / dt, 1), "unit": "clusters/s", "cores": 1,
+                               "kind": "port", "sample": f"{args.cpu_sample} synthetic clusters, numpy "
+                               f"average_spectrum restatement, {dt:.2f} s"}
     print(json.dumps(out), flush=True)
 
 
