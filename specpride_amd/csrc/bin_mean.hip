@@ -169,6 +169,26 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
     for (int64_t j = tid; j < n; j += BM_BLOCK) irregular |= (S.soff[j + 1] - S.soff[j]) > BM_BLOCK;
   }
   constexpr int U1 = 16;
+  if (kSmall && p1 - p0 < (int64_t(1) << 28)) {
+    // 32-bit cluster-relative byte offsets from a wave-uniform base (saddr loads)
+    const char* __restrict__ mzb = reinterpret_cast<const char*>(v.mz + p0);
+    const int np = (int)(p1 - p0);
+    for (int r0 = tid; r0 < np; r0 += U1 * BM_BLOCK) {
+      double m[U1];
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        const int r = r0 + u * BM_BLOCK;
+        m[u] = *reinterpret_cast<const double*>(mzb + (uint32_t)(r < np ? r : 0) * 8u);
+      }
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        if (r0 + u * BM_BLOCK < np && in_range(m[u], P)) {
+          const int32_t b = bin_small(m[u], P);
+          atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
+        }
+      }
+    }
+  } else
   for (int64_t k0 = p0 + tid; k0 < p1; k0 += U1 * BM_BLOCK) {
     double m[U1];
 #pragma unroll
@@ -215,13 +235,18 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
     // chains overlap; one LDS-only barrier per spectrum orders the updates.
     if constexpr (kSmall) {
       struct Pk { double m, it; };
+      // 32-bit cluster-relative offsets from a wave-uniform base: the loads take
+      // the saddr + 32-bit voffset form, no 64-bit address arithmetic per fetch
+      const double* __restrict__ mzc = v.mz + p0;
+      const double* __restrict__ itc = v.inten + p0;
       auto fetch = [&](int64_t j) {
-        const int64_t jj = j < n ? j : n - 1;
-        const int64_t a = p0 + S.soff[jj], e = p0 + S.soff[jj + 1];
-        const int64_t k = a + tid;
+        const int jj = (int)(j < n ? j : n - 1);
+        const uint32_t k = (uint32_t)(S.soff[jj] + tid);
+        const uint32_t idx = k < (uint32_t)S.soff[jj + 1] ? k : 0u;
         Pk q;
-        q.m = v.mz[k < e ? k : p0];
-        q.it = v.inten[k < e ? k : p0];
+        const uint32_t bo = idx * 8u;  // < 2^19: cluster-relative byte offset
+        q.m = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(mzc) + bo);
+        q.it = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(itc) + bo);
         return q;
       };
       const int lane = lane_id(), wid = wave_id();
