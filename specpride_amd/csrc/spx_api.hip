@@ -18,6 +18,7 @@
 #include "bin_mean_stream.hip"  // includes bin_mean.hip
 #include "bin_mean_wave.hip"
 #include "bin_mean_fast.hip"
+#include "bin_mean_ranges.hip"
 #include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
@@ -77,7 +78,8 @@ int32_t ablate_mask() {
 // Bin-mean kernel: 0 = per-cluster two-pass LDS kernel (default: fastest
 // measured), 7 = wave-private bin ranges with no per-spectrum barrier,
 // 8 = buffer-load / float2 variant of 0 (7 and 8 derive counts from the m/z
-// sums, so they run only where bin_counts_derivable holds), 1 = per-bin list
+// sums, so they run only where bin_counts_derivable holds), 9 = wave-private
+// ranges with boundaries found in the first pass, 1 = per-bin list
 // kernel, 2 = fold kernel, 3/4 = per-cluster hash kernel (2048/4096 slots),
 // 5 = persistent stream + hash fold, 6 = persistent stream + bitmap-rank fold
 // (DESIGN.md §3 has the measurements).  SPX_BIN_KERNEL selects (A/B profiling).
@@ -184,6 +186,10 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
       hipLaunchKernelGGL(spx::bin_mean_stream_kernel<spx::BS_H>, dim3((unsigned)G), dim3(spx::BM_BLOCK), 0, s, V, P,
                          O, prec_out, charge_out, status, def, n_def, plan);
     if (int rc = check_launch("bin_mean_stream_kernel")) return rc;
+  } else if (bv == 9) {
+    hipLaunchKernelGGL(spx::bin_mean_ranges_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                       charge_out, status, def, n_def);
+    if (int rc = check_launch("bin_mean_ranges_kernel")) return rc;
   } else if (bv == 8) {
     hipLaunchKernelGGL(spx::bin_mean_fast_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                        charge_out, status, def, n_def);

@@ -232,7 +232,7 @@ def test_medoid_large_path_skewed_unsorted_and_empty(gpu):
     np.testing.assert_array_equal(tot, ref_tot)
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5", "6", "7", "8"])
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9"])
 @pytest.mark.parametrize("name", BIN_SETS)
 def test_bin_mean_kernel_variants(gpu, synth, monkeypatch, name, variant):
     """Every bin-mean kernel variant (SPX_BIN_KERNEL, spx_api.hip) meets the same
@@ -335,7 +335,7 @@ def _wave_edge_batch():
     return SpectraCSR.from_clusters(clusters)
 
 
-@pytest.mark.parametrize("variant", ["8", "7", "0"])
+@pytest.mark.parametrize("variant", ["9", "8", "7", "0"])
 def test_bin_mean_wave_kernel_edges(gpu, monkeypatch, variant):
     monkeypatch.setenv("SPX_BIN_KERNEL", variant)
     csr = _wave_edge_batch()
@@ -343,7 +343,7 @@ def test_bin_mean_wave_kernel_edges(gpu, monkeypatch, variant):
     assert_bin_mean_equal(_bin_mean(csr), np_oracle.bin_mean(csr))
 
 
-@pytest.mark.parametrize("variant", ["8", "7"])
+@pytest.mark.parametrize("variant", ["9", "8", "7"])
 def test_bin_mean_wave_kernel_skewed_and_unsorted(gpu, monkeypatch, variant):
     """Skewed sizes (>128 spectra -> deferred) and shuffled spectra (deferred) mixed
     with regular clusters in one launch: bit-exact against the oracle."""
@@ -353,3 +353,32 @@ def test_bin_mean_wave_kernel_skewed_and_unsorted(gpu, monkeypatch, variant):
     assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
     sub = _shuffled(csr.select(range(120)))
     assert_bin_mean_equal(_bin_mean(sub), c_oracle.bin_mean(sub))
+
+
+def test_bin_mean_ranges_boundaries(gpu, monkeypatch):
+    """bin_mean_ranges_kernel's run boundaries: spectrum 0 unsorted-free but short
+    (bounds from 1-3 peaks), later spectra entirely below / above a boundary, peaks
+    exactly on a boundary bin, runs longer than a wave inside one range, spectra of
+    255 peaks (the cap) and 256 (deferred), all bit-exact against the oracle."""
+    monkeypatch.setenv("SPX_BIN_KERNEL", "9")
+    rng = np.random.default_rng(123)
+    clusters = []
+    for n0 in (1, 2, 3):
+        sp = [{"m/z array": np.sort(rng.uniform(100, 2000, n0)), "intensity array": rng.lognormal(3, 1, n0),
+               "precursor mz": 500.0, "precursor charge": 2}]
+        for k in range(12):
+            lo, hi = [(100, 400), (1500, 2000), (100, 2000), (800, 801)][k % 4]
+            m = int(rng.integers(1, 200))
+            sp.append({"m/z array": np.sort(rng.uniform(lo, hi, m)), "intensity array": rng.lognormal(3, 1, m),
+                       "precursor mz": 500.0 + k, "precursor charge": 2})
+        clusters.append(sp)
+    for length in (255, 256):
+        clusters.append([{"m/z array": np.sort(rng.uniform(100, 2000, length)),
+                          "intensity array": rng.lognormal(3, 1, length), "precursor mz": 600.0,
+                          "precursor charge": 3} for _ in range(4)])
+    # boundary bins hit exactly: every spectrum repeats spectrum 0's peaks
+    base = np.sort(rng.uniform(100, 2000, 40))
+    clusters.append([{"m/z array": base.copy(), "intensity array": rng.lognormal(3, 1, 40), "precursor mz": 700.0,
+                      "precursor charge": 2} for _ in range(9)])
+    csr = SpectraCSR.from_clusters(clusters)
+    assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))

@@ -40,8 +40,8 @@ def main():
     res["medoid_deferred"] = int(b._ws["medoid"][:4].view(torch.int32).item())
     for var in os.environ.get("SPX_VARIANTS", "6,5,0").split(","):
         os.environ["SPX_BIN_KERNEL"] = var
-        masks = (0, 1, 2) if var in ("0", "1", "2", "8") \
-            else ((0,) if var == "7" else (0, 2, 16, 32))
+        masks = {"0": (0, 1, 2), "1": (0, 1, 2), "2": (0, 1, 2), "8": (0, 1, 2), "7": (0,), "9": (0,)}.get(
+            var, (0, 2, 16, 32))
         for mask in masks:
             os.environ["SPX_ABLATE"] = str(mask)
             res[f"bin_mean_v{var}_ablate{mask}_ms"] = timed(lambda: engine.bin_mean(b, out=bm))
