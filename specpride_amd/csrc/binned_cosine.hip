@@ -30,11 +30,14 @@ namespace spx {
 struct CosParams {
   double s, start, e1, d;  // np.arange(start, stop, s) = start, e1, start + i * d
   double p10;              // 10**decimals of scipy's on-edge rounding
+  double inv_d;            // 1 / d: the bin estimate (edge compares make it exact)
 };
 
 constexpr int CS_BLOCK = 256;
 constexpr int CS_RCAP = 1024;  // representative peaks held in LDS
 constexpr int CS_NW = CS_BLOCK / kWave;
+constexpr int CS_BSH = 8;      // run-index buckets of 256 bins (~1.28 Da)
+constexpr int CS_BMAX = 2048;  // buckets held in LDS: bins < 524,288 (m/z < ~2,620)
 
 struct CosSmem {
   int32_t sk[CS_RCAP];       // representative peak bins, input order (rank sort input)
@@ -45,6 +48,7 @@ struct CosSmem {
   int16_t rs[CS_RCAP + 1];   //   first sorted position,
   double rA[CS_RCAP];        //   A_b (summed in input order),
   double rA2[CS_RCAP + 1];   //   exclusive prefix of A_b^2
+  uint16_t bst[CS_BMAX];     // first run with a bin >= t << CS_BSH, per bucket t
   int32_t wk[CS_NW][kWave];  // per-wave member scratch: bins,
   double wI[CS_NW][kWave];   //   intensities
   double tmpd[CS_NW + 1];
@@ -56,10 +60,11 @@ __device__ __forceinline__ double cs_edge(const CosParams& P, int64_t i) {
   return i == 0 ? P.start : (i == 1 ? P.e1 : P.start + (double)i * P.d);
 }
 
-// k with e_k <= x < e_{k+1} over the unbounded edge sequence; -1 below e_0 or NaN
+// k with e_k <= x < e_{k+1} over the unbounded edge sequence; -1 below e_0 or NaN.
+// The reciprocal product is only an estimate; the exact edge compares settle it.
 __device__ __forceinline__ int64_t cs_bin(const CosParams& P, double x) {
   if (!(x >= P.start)) return -1;
-  int64_t k = (int64_t)((x - P.start) / P.d);
+  int64_t k = (int64_t)((x - P.start) * P.inv_d);
   if (k > 0 && cs_edge(P, k) > x) --k;
   if (k > 0 && cs_edge(P, k) > x) --k;
   while (cs_edge(P, k + 1) <= x) ++k;
@@ -117,12 +122,20 @@ __global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosP
     L.sk[i] = k > 0x7ffffffe ? 0x7ffffffe : (int32_t)k;
   }
   __syncthreads();
+  // an m/z-sorted representative (the consensus outputs are) is already in
+  // (bin, index) order: the stable rank sort is the identity
+  int inv = 0;
+  for (int i = tid + 1; i < R; i += CS_BLOCK) inv |= L.sk[i] < L.sk[i - 1];
+  const bool sorted = !__syncthreads_or(inv);
   for (int i = tid; i < R; i += CS_BLOCK) {
     const int32_t k = L.sk[i];
-    int rank = 0;
-    for (int j = 0; j < R; ++j) {
-      const int32_t kj = L.sk[j];
-      rank += kj < k || (kj == k && j < i);
+    int rank = i;
+    if (!sorted) {
+      rank = 0;
+      for (int j = 0; j < R; ++j) {
+        const int32_t kj = L.sk[j];
+        rank += kj < k || (kj == k && j < i);
+      }
     }
     L.pk[rank] = k;
     L.pI[rank] = rep_int[r0 + i];
@@ -170,6 +183,17 @@ __global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosP
       }
     }
     if (tid == 0) L.rA2[nr] = tot;
+    // bucket t: the first run with a bin >= t << CS_BSH (runs are sorted by bin)
+    for (int t = tid; t < CS_BMAX; t += CS_BLOCK) {
+      const int64_t b0 = (int64_t)t << CS_BSH;
+      int lo = 0, hi = nr;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)L.rb[mid] < b0) lo = mid + 1;
+        else hi = mid;
+      }
+      L.bst[t] = (uint16_t)lo;
+    }
     __syncthreads();
   }
   const int NR = L.nruns;
@@ -202,6 +226,11 @@ __global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosP
     if (has_extra) aa = L.rA2[kc_run ? ic - 1 : ic] + A_kc * A_kc;
     auto lookup = [&](int64_t b) -> double {
       if (b == kc) return A_kc;
+      if ((b >> CS_BSH) < CS_BMAX) {  // bucket start, then a short forward walk
+        int u = L.bst[b >> CS_BSH];
+        while (u < NR && (int64_t)L.rb[u] < b) ++u;
+        return (u < NR && (int64_t)L.rb[u] == b) ? L.rA[u] : 0.0;
+      }
       const int u = runs_upper(L.rb, NR, b);
       return (u > 0 && (int64_t)L.rb[u - 1] == b) ? L.rA[u - 1] : 0.0;
     };

@@ -393,6 +393,7 @@ extern "C" int spx_binned_cosine(const spx_csr* csr, const int64_t* rep_off, con
   P.start = -params->mz_space / 2.0;
   P.e1 = P.start + P.s;
   P.d = P.e1 - P.start;
+  P.inv_d = 1.0 / P.d;
   const int dec = (int)(-std::log10(std::min(P.d, P.s))) + 6;
   P.p10 = std::pow(10.0, (double)dec);
   hipLaunchKernelGGL(spx::binned_cosine_kernel, dim3((unsigned)C), dim3(spx::CS_BLOCK), 0,
