@@ -272,7 +272,8 @@ __device__ __forceinline__ void gap_peaks(const CsrView& v, int64_t p0, int64_t 
 // --------------------------------------------------------------- the body
 template <class PrefixT>
 __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState<PrefixT>& S, int64_t c,
-                            const PeaksOut& out, int* tmp, double* red) {
+                            const PeaksOut& out, int* tmp, double* red, const PrecLanes* pl = nullptr,
+                            PrecSummary* early = nullptr) {
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
   const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1], n = s1 - s0;
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1], N = p1 - p0;
@@ -296,6 +297,10 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       }
     }
   }
+  // the precursor summary needs no peaks: wave 0 runs it while the peak loads
+  // above are in flight (its own loads were issued before them), instead of as
+  // a one-wave tail after the last phase
+  if (early && pl && wid == 0 && n <= kWave && !(P.ablate & 32)) *early = precursor_summary_wave(*pl, (int)n, P);
   // f(m, it, tag): tag is scratch the callee may ignore
   auto peaks = [&](auto f) __attribute__((always_inline)) {
     if (inreg) {
@@ -493,7 +498,8 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 template <class PrefixT>
 __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P, int64_t c, int32_t st,
                                            const PeaksOut& out, double* prec_out, int32_t* charge_out,
-                                           double* rt_out, int32_t* status, const PrecLanes* pl = nullptr) {
+                                           double* rt_out, int32_t* status, const PrecLanes* pl = nullptr,
+                                           const PrecSummary* early = nullptr) {
   const int64_t s0 = v.cluster_off[c], n = v.cluster_off[c + 1] - s0;
   if (st == kDeferred) return;
   if (P.ablate & 32) {
@@ -502,7 +508,8 @@ __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P,
   }
   if (wave_id() == 0) {
     PrecSummary R{nan_d(), nan_d(), 0, kOk};
-    if (n > 0) R = (pl && n <= kWave) ? precursor_summary_wave(*pl, (int)n, P) : precursor_summary(v, s0, n, P);
+    if (early && n > 0 && n <= kWave) R = *early;
+    else if (n > 0) R = (pl && n <= kWave) ? precursor_summary_wave(*pl, (int)n, P) : precursor_summary(v, s0, n, P);
     if (lane_id() == 0) {
       // the reference computes the precursor first (:161-163): its error wins
       const int32_t fin = R.status != kOk ? R.status : st;
@@ -522,7 +529,11 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   __shared__ GapSmem L;
   const int64_t c = blockIdx.x;
   GapState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.gcnt, L.kmin, L.kmax, GA_WMAX, GA_DCAP};
-  const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red);
+  const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
+  PrecLanes pl{0, 0.0, 0.0};
+  if (wave_id() == 0 && pn <= kWave) pl = prec_lanes(v, ps0, pn);
+  PrecSummary early{0.0, 0.0, 0, kOk};
+  const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, &pl, &early);
   if (st == kDeferred) {
     if (threadIdx.x == 0) {
       status[c] = kDeferred;
@@ -530,7 +541,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
     }
     return;
   }
-  gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status);
+  gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, nullptr, &early);
 }
 
 // Scratch slice of the deferred path: every array starts 256-B aligned (the
