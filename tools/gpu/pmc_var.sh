@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes for one bin-mean variant (SPX_BIN_KERNEL) and ablation mask (SPX_ABLATE).
-# usage: scripts_gpu_pmc_var.sh <variant> <ablate> <kernel-regex> <outdir>
+# usage: tools/gpu/pmc_var.sh <variant> <ablate> <kernel-regex> <outdir>
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
