@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--clusters", type=int, default=100_000)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-sample", type=int, default=1000, help="clusters in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=2000, help="clusters in the CPU-baseline sample (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
