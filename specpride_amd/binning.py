@@ -138,7 +138,12 @@ class RepresentativeSpectrumCreator:
         for pl in clusters:
             for p in pl:  # the reference indexes these keys (KeyError if absent)
                 p["precursor mz"], p["precursor charge"]
-        csr = SpectraCSR.from_clusters(clusters)
+        return self._combine_csr(SpectraCSR.from_clusters(clusters), clusters, minimum, maximum, binsize,
+                                 apply_peak_quorum)
+
+    def _combine_csr(self, csr, clusters, minimum=100, maximum=2000, binsize=0.02, apply_peak_quorum=True):
+        """The device pass over a packed batch; ``clusters[c]`` (peaklists) or None
+        per cluster -- the output's precursor_charge is its first member's charge."""
         res = engine.bin_mean(engine.DeviceBatch.from_host(csr, self.device), minimum, maximum, binsize,
                               apply_peak_quorum).to_host()
         out = []
@@ -153,7 +158,8 @@ class RepresentativeSpectrumCreator:
             out.append({"minimum": minimum, "maximum": maximum, "binsize": binsize,
                         "intensities": res["out_int"][a:b].copy(), "mzs": res["out_mz"][a:b].copy(),
                         "precursor_mz": np.float64(res["prec"][c]),
-                        "precursor_charge": pl[0]["precursor charge"]})
+                        "precursor_charge": pl[0]["precursor charge"] if pl is not None
+                        else int(csr.charge[csr.cluster_off[c]])})
         return out
 
     # ------------------------------------------------------------ MGF output
@@ -163,6 +169,41 @@ class RepresentativeSpectrumCreator:
         from . import mgf_native
 
         mgf_native.write_binning_mgf(spectra, mgf_file)
+
+
+def _flat_clusters(path):
+    """read_spectra_clustered_mgf + packing without per-spectrum Python objects:
+    the native parser's flat arrays regrouped by cluster (first appearance, members
+    in file order: binning.py:122-167).  None when the file is
+    outside the native subset or a spectrum lacks the fields the reference indexes
+    (the dict path then raises exactly as the reference does)."""
+    from . import mgf_native
+    from .csr import concat_ranges
+
+    try:
+        flat = mgf_native.parse_native(path)
+    except ValueError:
+        return None
+    if flat is None or not flat["titles"] or not (flat["has_prec"].all() and flat["has_charge"].all()):
+        return None
+    order, cl = {}, []
+    for title in flat["titles"]:
+        parts = title.split(";")
+        if len(parts) < 2:  # the reference's parts[1] raises: let the dict path do it
+            return None
+        cl.append(order.setdefault(parts[0], len(order)))
+    cl = np.asarray(cl, np.int64)
+    perm = np.argsort(cl, kind="stable")
+    so = flat["spec_off"]
+    lens = (so[1:] - so[:-1])[perm]
+    spec_off = np.zeros(len(perm) + 1, np.int64)
+    np.cumsum(lens, out=spec_off[1:])
+    idx = concat_ranges(so[:-1][perm], lens)
+    cluster_off = np.zeros(len(order) + 1, np.int64)
+    np.cumsum(np.bincount(cl, minlength=len(order)), out=cluster_off[1:])
+    csr = SpectraCSR(cluster_off, spec_off, flat["mz"][idx], flat["inten"][idx], flat["prec_mz"][perm],
+                     flat["charge"][perm].astype(np.int32), np.full(len(perm), np.nan))
+    return list(order.keys()), csr
 
 
 def main(argv=None):
@@ -194,10 +235,16 @@ def main(argv=None):
         sys.exit(10)
     rsc = RepresentativeSpectrumCreator(verbose=verbose)
     print("Reading spectra...")
-    clusters = rsc.read_spectra_clustered_mgf(params.mgf_file)
-    print("Clustering...")
-    ids = list(clusters.keys())
-    merged = rsc.combine_bin_mean_batch([clusters[k] for k in ids], minimum=100, maximum=2000, binsize=0.02)
+    flat = _flat_clusters(params.mgf_file)
+    if flat is not None:  # native parse straight to the cluster-segmented CSR
+        ids, csr = flat
+        print("Clustering...")
+        merged = rsc._combine_csr(csr, [None] * len(ids), minimum=100, maximum=2000, binsize=0.02)
+    else:  # the reference's own line loop decides (malformed or unusual input)
+        clusters = rsc.read_spectra_clustered_mgf(params.mgf_file)
+        print("Clustering...")
+        ids = list(clusters.keys())
+        merged = rsc.combine_bin_mean_batch([clusters[k] for k in ids], minimum=100, maximum=2000, binsize=0.02)
     for cid, spec in zip(ids, merged):
         spec["cluster_id"] = cid
     with open(params.out, "wt") as mgf_file:

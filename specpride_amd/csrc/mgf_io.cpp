@@ -9,7 +9,8 @@
 //   a line whose first char is an ASCII digit is "mz intensity" (single space,
 //   extra fields ignored); a stripped "END IONS" stores the spectrum.
 // Numbers use the plain decimal grammar [+-]digits[.digits][e[+-]digits]; the
-// values equal Python float() because strtod is correctly rounded too.  Any
+// values equal Python float(): both are correctly rounded (Clinger's exact fast
+// path for short decimals, strtod otherwise).  Any
 // line outside that subset (underscores in numbers, inf/nan, tabs between
 // fields, non-ASCII text, PEPMASS before the first TITLE, a repeated END IONS,
 // a TITLE without ';') makes the parse report "fallback: ..." and the caller
@@ -84,6 +85,45 @@ bool parse_float(const char* b, const char* e, double& out) {
     if (p == x0) return false;
   }
   if (p != e) return false;
+  // Clinger's exact fast path: an integer significand w <= 2^53 scaled by an
+  // exactly representable 10^k (|k| <= 22) is ONE correctly rounded IEEE
+  // multiply or divide of exact operands -- the correctly rounded value of the
+  // decimal, i.e. what strtod and Python's float() return.  m/z and intensity
+  // lines ("1234.56789 17.25") take this path; anything longer falls to strtod.
+  {
+    static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                      1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    const char* q = b;
+    const bool neg = *q == '-';
+    if (*q == '+' || *q == '-') ++q;
+    uint64_t w = 0;
+    int nd = 0, frac = 0;
+    bool in_frac = false, ok = true;
+    for (; q < e && *q != 'e' && *q != 'E'; ++q) {
+      if (*q == '.') { in_frac = true; continue; }
+      if (w == 0 && *q == '0') { frac += in_frac; continue; }  // leading zeros: no significant digit
+      if (++nd > 19) { ok = false; break; }
+      w = w * 10 + (uint64_t)(*q - '0');
+      frac += in_frac;
+    }
+    int ex = 0;
+    if (ok && q < e) {  // exponent (grammar checked above)
+      ++q;
+      const bool eneg = *q == '-';
+      if (*q == '+' || *q == '-') ++q;
+      for (; q < e && ok; ++q) {
+        ex = ex * 10 + (*q - '0');
+        if (ex > 400) ok = false;
+      }
+      if (eneg) ex = -ex;
+    }
+    const int k = ex - frac;
+    if (ok && w <= (uint64_t(1) << 53) && k >= -22 && k <= 22) {
+      const double v = k < 0 ? (double)w / kPow10[-k] : (double)w * kPow10[k];
+      out = neg ? -v : v;
+      return true;
+    }
+  }
   char buf[128];
   const size_t n = (size_t)(e - b);
   if (n >= sizeof(buf)) {

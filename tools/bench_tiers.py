@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""The two host-inclusive measurement tiers of SURVEY.md §8(d) (never `value`):
+
+* tier 2 -- a packed host CSR (configs[1] law) -> H2D -> spx_bin_mean + spx_medoid
+  -> compaction + D2H of the consensus peaks and representatives;
+* tier 3 -- the binning.py CLI end to end (binning.py:250-302): MGF text in
+  (native parser) -> device -> MGF text out, on a synthetic clustered MGF.
+
+Prints one JSON line.  The reference's own CLI is timed on the same file shape by
+tools/time_reference_cli.py in the build container (the reference never reaches the
+GPU box); DESIGN.md §6 sets the two side by side.
+
+    python tools/bench_tiers.py [--t2-clusters 20000] [--t3-clusters 2000]
+"""
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--t2-clusters", type=int, default=20000)
+    ap.add_argument("--t3-clusters", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+
+    from specpride_amd import binning, engine
+    from specpride_amd.mgf import write_csr_mgf
+    from specpride_amd.synthetic import make_clusters_np
+
+    out = {}
+    # ---------------------------------------------------------------- tier 2
+    csr = make_clusters_np(args.t2_clusters, seed=args.seed)
+    for rep in range(2):  # the first pass warms the allocator and the code object
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        b = engine.DeviceBatch.from_host(csr)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        bm = engine.bin_mean(b)
+        md = engine.medoid(b)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        r = bm.to_host()
+        rep_idx, _ = md.to_host()
+        t3 = time.perf_counter()
+    out["tier2"] = {"clusters": int(csr.n_clusters), "peaks": int(csr.n_peaks),
+                    "h2d_s": round(t1 - t0, 4), "kernels_s": round(t2 - t1, 4), "d2h_s": round(t3 - t2, 4),
+                    "clusters_per_s": round(csr.n_clusters / (t3 - t0), 1),
+                    "h2d_GBs": round(16.0 * csr.n_peaks / (t1 - t0) / 1e9, 1),
+                    "kept_peaks": int(r["out_off"][-1]), "reps_ok": bool((rep_idx >= 0).all())}
+    # ---------------------------------------------------------------- tier 3
+    small = make_clusters_np(args.t3_clusters, seed=args.seed + 1)
+    with tempfile.TemporaryDirectory() as td:
+        mgf_in, mgf_out = os.path.join(td, "in.mgf"), os.path.join(td, "out.mgf")
+        write_csr_mgf(small, mgf_in)
+        size = os.path.getsize(mgf_in)
+        with contextlib.redirect_stdout(io.StringIO()):
+            binning.main(["--mgf_file", mgf_in, "--out", mgf_out])  # warm
+            t0 = time.perf_counter()
+            binning.main(["--mgf_file", mgf_in, "--out", mgf_out])
+            t1 = time.perf_counter()
+        out["tier3"] = {"clusters": int(small.n_clusters), "peaks": int(small.n_peaks),
+                        "mgf_MB": round(size / 1e6, 1), "cli_s": round(t1 - t0, 3),
+                        "clusters_per_s": round(small.n_clusters / (t1 - t0), 1),
+                        "out_MB": round(os.path.getsize(mgf_out) / 1e6, 2)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
