@@ -169,3 +169,38 @@ def test_binning_cli_without_mgf_file_exits_10():
         binning.main([])
     assert e.value.code == g["no_args_returncode"]
     assert buf.getvalue() == g["no_args_stdout"]
+
+
+def test_native_decimal_parse_matches_python_float(tmp_path):
+    """The native parser's Clinger fast path and its strtod fallback agree with
+    Python's float() bit for bit: short and long significands, exponents, leading
+    zeros, signs, subnormal/huge values, 19-20 digit boundaries."""
+    import random
+
+    import numpy as np
+
+    from specpride_amd import mgf_native
+
+    rng = random.Random(7)
+    fixed = ["0", "0.0", "-0.0", "+1.5", "00012.500", "1e5", "1E-5", "2.5e+3", "123456789012345678",
+             "1234567890123456789", "12345678901234567890", "9007199254740993", "9007199254740992.0",
+             "0.000123", "1.7976931348623157e308", "5e-324", "2.2250738585072014e-308", "1e22", "1e23",
+             "4.35679", "0.1", "0.3", "100.00001", "1999.99999", "3.141592653589793238462643383279"]
+    nums = fixed + [f"{rng.uniform(0, 2000):.{rng.randint(0, 12)}f}" for _ in range(3000)]
+    nums += [f"{rng.uniform(0, 1):.{rng.randint(13, 25)}f}" for _ in range(500)]
+    nums += [f"{rng.uniform(1, 10):.6f}e{rng.randint(-30, 30)}" for _ in range(500)]
+    path = tmp_path / "nums.mgf"
+    with open(path, "w") as fh:
+        for k in range(0, len(nums), 50):
+            fh.write(f"BEGIN IONS\nTITLE=c{k % 7};usi{k}\nPEPMASS={nums[k]}\nCHARGE=2+\n")
+            block = [n for n in nums[k:k + 50] if n[0].isdigit()]
+            fh.write("".join(f"{a} {b}\n" for a, b in zip(block, block[1:] + block[:1])))
+            fh.write("END IONS\n\n")
+    flat = mgf_native.parse_native(str(path))
+    ref = mgf_native._read_binning_py(str(path))
+    mz = np.concatenate([np.asarray(s["m/z array"], np.float64) for s in ref])
+    it = np.concatenate([np.asarray(s["intensity array"], np.float64) for s in ref])
+    assert np.array_equal(flat["mz"].view(np.int64), mz.view(np.int64))
+    assert np.array_equal(flat["inten"].view(np.int64), it.view(np.int64))
+    prec = np.array([s["precursor mz"] for s in ref])
+    assert np.array_equal(flat["prec_mz"].view(np.int64), prec.view(np.int64))
