@@ -56,8 +56,14 @@ struct BinMeanState {
   int nmax;  // clusters with more spectra are deferred (leaf-only pairwise mean)
 };
 
+#ifndef SPX_BM_LENRING
+#define SPX_BM_LENRING 1  // spectrum lengths ride the register ring (no per-step offset read)
+#endif
+#ifndef SPX_BM_MINW
+#define SPX_BM_MINW 5  // __launch_bounds__ minimum waves per SIMD for bin_mean_lds_kernel (LDS allows 5)
+#endif
 #ifndef SPX_BM_PF
-#define SPX_BM_PF 12  // spectra in flight per thread in the fast path's register ring
+#define SPX_BM_PF 10  // spectra in flight per thread in the fast path's register ring
 #endif
 
 constexpr int BM_BLOCK = 256;
@@ -234,16 +240,19 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
     // 63's exchange, then the slot read-modify-write), so the two latency
     // chains overlap; one LDS-only barrier per spectrum orders the updates.
     if constexpr (kSmall) {
-      struct Pk { double m, it; };
+      // the ring also carries the spectrum's length, so a step reads no offsets
+      struct Pk { double m, it; int len; };
       // 32-bit cluster-relative offsets from a wave-uniform base: the loads take
       // the saddr + 32-bit voffset form, no 64-bit address arithmetic per fetch
       const double* __restrict__ mzc = v.mz + p0;
       const double* __restrict__ itc = v.inten + p0;
       auto fetch = [&](int64_t j) {
         const int jj = (int)(j < n ? j : n - 1);
-        const uint32_t k = (uint32_t)(S.soff[jj] + tid);
-        const uint32_t idx = k < (uint32_t)S.soff[jj + 1] ? k : 0u;
+        const int a = S.soff[jj], e = S.soff[jj + 1];
+        const uint32_t k = (uint32_t)(a + tid);
+        const uint32_t idx = k < (uint32_t)e ? k : 0u;
         Pk q;
+        q.len = e - a;
         const uint32_t bo = idx * 8u;  // < 2^19: cluster-relative byte offset
         q.m = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(mzc) + bo);
         q.it = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(itc) + bo);
@@ -271,9 +280,13 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
           if (jb + j < n) {  // uniform
             const int64_t js = jb + j;
             const int par = (int)(js & 1);
-            const int len = S.soff[js + 1] - S.soff[js];
-            const bool active = tid < len, has_next = tid + 1 < len;
             const Pk q = R[j];
+#if SPX_BM_LENRING
+            const int len = q.len;
+#else
+            const int len = S.soff[js + 1] - S.soff[js];
+#endif
+            const bool active = tid < len, has_next = tid + 1 < len;
             R[j] = fetch(js + PF);
             bad |= active && (q.m != q.m);
             const bool inr = active && in_range(q.m, P);
@@ -283,7 +296,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
               key = bin_small(q.m, P);
               slot = bitmap_rank(S.bitmap, S.wprefix, (int64_t)key);
             }
-            const int32_t kn = __shfl_down(key, 1, kWave);
+            const int32_t kn = wave_next(key, 0x7fffffff);  // lane 63: from xch below
             if (lane == 0) S.xch[par * NW + wid] = key;
             bool last = true;
             if (lane < kWave - 1 && has_next) {
@@ -387,7 +400,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   return kOk;
 }
 
-__global__ __launch_bounds__(BM_BLOCK) void bin_mean_lds_kernel(CsrView v, BinMeanParams P, PeaksOut out,
+__global__ __launch_bounds__(BM_BLOCK, SPX_BM_MINW) void bin_mean_lds_kernel(CsrView v, BinMeanParams P, PeaksOut out,
                                                                 double* prec_out, int32_t* charge_out,
                                                                 int32_t* status, int32_t* deferred,
                                                                 int32_t* n_deferred) {
@@ -1024,11 +1037,6 @@ __device__ __forceinline__ uint32_t bh_home(uint32_t key) {
   return __umul24(key, 0x9E3779u) >> (24 - LG) & (H / 4 - 1);
 }
 __device__ __forceinline__ uint32_t bh_stride(uint32_t key) { return (__umul24(key, 0x85EBCAu) >> 12) | 1u; }
-
-// lane i receives lane i+1's value (DPP wave_shl:1); lane 63 receives `old`
-__device__ __forceinline__ int32_t wave_next(int32_t x, int32_t old) {
-  return __builtin_amdgcn_update_dpp(old, x, 0x130, 0xF, 0xF, false);
-}
 
 // First word of a group that is `key` or empty (-1: neither; the group is full
 // of other bins).  Sets hit when it is `key`.

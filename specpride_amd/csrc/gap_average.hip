@@ -44,7 +44,17 @@ struct GapParams {
 
 constexpr int GA_BLOCK = 512;  // 2 workgroups per CU (LDS): 16 waves
 constexpr int GA_NW = GA_BLOCK / kWave;
-constexpr int GA_U = 12;  // peaks per thread held in registers (8,192 per cluster)
+constexpr int GA_U = 12;  // peaks per thread held in registers, m/z + intensity (6,144 per cluster)
+#ifndef SPX_GA_MONLY
+#define SPX_GA_MONLY 1  // registers hold m/z only (GA_UM per thread); intensities streamed in passes 1 and 5
+#endif
+#ifndef SPX_GA_UM
+#define SPX_GA_UM 16
+#endif
+#ifndef SPX_GA_TAGS
+#define SPX_GA_TAGS 1  // pass 3's per-peak slots kept in registers (u16 pairs) for pass 5
+#endif
+constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (8,192 per cluster)
 constexpr int GA_WMAX = 3584;  // 229,376 buckets (2,293 Da at 0.01)
 constexpr int GA_DCAP = 1536;  // occupied buckets per cluster
 
@@ -279,6 +289,69 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1], N = p1 - p0;
   if (n == 0) return kNoGap;
 
+#if SPX_GA_MONLY
+  // The cluster's m/z values are read from HBM ONCE into registers when they
+  // fit (<= GA_UM per thread = 8,192 peaks: ~80% of the U{2..50} clusters of
+  // the configs); passes 2-3 run from registers, and pass 3's slot per peak is
+  // kept (u16 pairs) for pass 5.  Intensities are needed only by
+  // passes 1 and 5 and are streamed there (8 loads in flight), so the register
+  // budget holds twice as many peaks as m/z + intensity pairs would.  Larger
+  // clusters re-read both per pass.
+  const bool inreg = N <= (int64_t)GA_UM * GA_BLOCK;  // uniform
+  double rm[GA_UM];
+  uint32_t tags[(GA_UM + 1) / 2];  // pass-3 slot of each register peak (u16 pairs), reused by pass 5
+#pragma unroll
+  for (int q = 0; q < (GA_UM + 1) / 2; ++q) tags[q] = 0u;
+  if (inreg) {
+#pragma unroll
+    for (int u = 0; u < GA_UM; ++u) {
+      const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
+      const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
+      rm[u] = N > 0 ? v.mz[kk] : 0.0;
+    }
+  }
+  if (early && pl && wid == 0 && n <= kWave && !(P.ablate & 32)) *early = precursor_summary_wave(*pl, (int)n, P);
+  // f(m, it, tag) over every peak; kInten false passes it = 0 and loads none
+  auto peaks_g = [&](auto inten_c, auto tagout_c, auto f) __attribute__((always_inline)) {
+    constexpr bool kInten = decltype(inten_c)::value;
+    constexpr bool kTagOut = decltype(tagout_c)::value;
+    if (inreg) {
+#pragma unroll
+      for (int u0 = 0; u0 < GA_UM; u0 += 8) {
+        double itb[8];
+        if constexpr (kInten) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int64_t k = p0 + (int64_t)(u0 + q) * GA_BLOCK + tid;
+            itb[q] = (u0 + q < GA_UM) ? v.inten[k < p1 ? k : (N > 0 ? p0 : 0)] : 0.0;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int u = u0 + q;
+          if (u < GA_UM) {
+            const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
+            int32_t tag = (int32_t)((tags[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+            if (k < p1) f(rm[u], kInten ? itb[q] : 0.0, tag);
+            if constexpr (kTagOut) {
+              if (u & 1) tags[u >> 1] |= (uint32_t)tag << 16;
+              else tags[u >> 1] = (uint32_t)tag & 0xFFFFu;
+            }
+          }
+        }
+      }
+    } else {
+      gap_peaks<kInten>(v, p0, p1, [&](int64_t, double m, double it) {
+        int32_t tag = 0;
+        f(m, it, tag);
+      });
+    }
+  };
+  auto peaks = [&](auto f) __attribute__((always_inline)) { peaks_g(std::true_type{}, std::false_type{}, f); };
+  auto peaks_m = [&](auto f) __attribute__((always_inline)) { peaks_g(std::false_type{}, std::false_type{}, f); };
+  auto peaks_m_tag = [&](auto f) __attribute__((always_inline)) { peaks_g(std::false_type{}, std::true_type{}, f); };
+  const bool tagged = SPX_GA_TAGS && inreg;  // pass 5 takes pass 3's slots from registers (uniform)
+#else
   // The cluster's peaks are read from HBM ONCE into registers when they fit
   // (<= GA_U per thread: every config's U{2..50} clusters); the passes below
   // then run from registers.  Larger clusters re-read them per pass.
@@ -317,6 +390,10 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       });
     }
   };
+  auto peaks_m = peaks;
+  auto peaks_m_tag = peaks;
+  constexpr bool tagged = false;
+#endif
 
   // 1: extrema and finiteness
   double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
@@ -370,7 +447,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     imax = fmax(imax, red[2 * GA_NW + w]);
   }
   const int64_t kb = floor_div_exact(lo, P.bucket_w, P.inv_bucket_w);
-  constexpr bool tagged = false;  // (no per-peak bucket cache: the registers go to the peaks)
   const int64_t ke = floor_div_exact(hi, P.bucket_w, P.inv_bucket_w);
   const int64_t nw = (ke - kb) / 64 + 1;
   if (nw > S.wcap) return kDeferred;
@@ -378,8 +454,8 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   // 2: occupied buckets
   for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
   __syncthreads();
-  peaks([&](double m, double, int32_t& tag) {
-    const int64_t b = (tagged ? (int64_t)tag : floor_div_exact(m, P.bucket_w, P.inv_bucket_w)) - kb;
+  peaks_m([&](double m, double, int32_t& tag) {
+    const int64_t b = floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
     SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
     atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
   });
@@ -396,9 +472,8 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   __syncthreads();
 
   // 3: per-slot count and m/z extent
-  peaks([&](double m, double, int32_t& tag) {
-    const int slot =
-        bitmap_rank(S.bitmap, S.wprefix, (tagged ? (int64_t)tag : floor_div_exact(m, P.bucket_w, P.inv_bucket_w)) - kb);
+  peaks_m_tag([&](double m, double, int32_t& tag) {
+    const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
     tag = slot;
     const uint64_t key = f64_order_key(m);
     SPX_GUARD(slot >= 0 && slot < D, "gap slot c=%ld slot=%d D=%d\n", (long)c, slot, D)

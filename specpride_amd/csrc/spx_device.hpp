@@ -66,6 +66,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t bf_rsrc(const double* p, int n
 
 // --------------------------------------------------------- wave primitives
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+// lane i receives lane i+1's value (DPP wave_shl:1, a VALU op: no LDS round
+// trip as __shfl_down's ds_bpermute costs); lane 63 receives `old`.  Call with
+// the whole wave active.
+__device__ __forceinline__ int32_t wave_next(int32_t x, int32_t old) {
+  return __builtin_amdgcn_update_dpp(old, x, 0x130, 0xF, 0xF, false);
+}
 __device__ __forceinline__ int wave_id() { return threadIdx.x / kWave; }
 
 template <class T>
