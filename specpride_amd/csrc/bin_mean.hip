@@ -56,6 +56,9 @@ struct BinMeanState {
   int nmax;  // clusters with more spectra are deferred (leaf-only pairwise mean)
 };
 
+#ifndef SPX_BM_OVL
+#define SPX_BM_OVL 1  // fast path: 63 owned peaks per wave, lane 63 = neighbour only (no cross-wave key exchange)
+#endif
 #ifndef SPX_BM_LENRING
 #define SPX_BM_LENRING 1  // spectrum lengths ride the register ring (no per-step offset read)
 #endif
@@ -67,6 +70,13 @@ struct BinMeanState {
 #endif
 
 constexpr int BM_BLOCK = 256;
+#if SPX_BM_OVL
+// fast path: wave w's lanes 0..62 own peaks 63w..63w+62 of the spectrum; lane 63
+// loads peak 63w+63 (owned by wave w+1's lane 0) only to hand lane 62 its key
+constexpr int BM_FASTLEN = 4 * 63;
+#else
+constexpr int BM_FASTLEN = BM_BLOCK;
+#endif
 constexpr int BM_WMAX = 1536;  // 98,304 bins
 constexpr int BM_DCAP = 1536;  // distinct occupied bins per cluster
 constexpr int BM_NMAX = 128;
@@ -172,7 +182,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   // phase 1: occupied-bin bitmap (16 independent loads in flight per thread)
   int irregular = 0;  // a spectrum longer than the block: no fast path
   if constexpr (kSmall) {
-    for (int64_t j = tid; j < n; j += BM_BLOCK) irregular |= (S.soff[j + 1] - S.soff[j]) > BM_BLOCK;
+    for (int64_t j = tid; j < n; j += BM_BLOCK) irregular |= (S.soff[j + 1] - S.soff[j]) > BM_FASTLEN;
   }
   constexpr int U1 = 16;
   if (kSmall && p1 - p0 < (int64_t(1) << 28)) {
@@ -246,10 +256,15 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
       // the saddr + 32-bit voffset form, no 64-bit address arithmetic per fetch
       const double* __restrict__ mzc = v.mz + p0;
       const double* __restrict__ itc = v.inten + p0;
+#if SPX_BM_OVL
+      const int fpos = wave_id() * (kWave - 1) + lane_id();  // this lane's peak in every spectrum
+#else
+      const int fpos = tid;
+#endif
       auto fetch = [&](int64_t j) {
         const int jj = (int)(j < n ? j : n - 1);
         const int a = S.soff[jj], e = S.soff[jj + 1];
-        const uint32_t k = (uint32_t)(a + tid);
+        const uint32_t k = (uint32_t)(a + fpos);
         const uint32_t idx = k < (uint32_t)e ? k : 0u;
         Pk q;
         q.len = e - a;
@@ -286,17 +301,35 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
 #else
             const int len = S.soff[js + 1] - S.soff[js];
 #endif
+#if SPX_BM_OVL
+            const bool active = fpos < len && lane < kWave - 1, has_next = fpos + 1 < len;
+            const bool inr = fpos < len && in_range(q.m, P);  // lane 63 too: its key is lane 62's neighbour
+#else
             const bool active = tid < len, has_next = tid + 1 < len;
+            const bool inr = active && in_range(q.m, P);
+#endif
             R[j] = fetch(js + PF);
             bad |= active && (q.m != q.m);
-            const bool inr = active && in_range(q.m, P);
             int32_t key = q.m < P.minimum ? -1 : 0x7fffffff;
             int slot = -1;
             if (inr) {
               key = bin_small(q.m, P);
               slot = bitmap_rank(S.bitmap, S.wprefix, (int64_t)key);
             }
-            const int32_t kn = wave_next(key, 0x7fffffff);  // lane 63: from xch below
+            const int32_t kn = wave_next(key, 0x7fffffff);
+#if SPX_BM_OVL
+            bool last = true;
+            if (active && has_next) {
+              bad |= key > kn;
+              last = kn != key;
+            }
+            if (pslot >= 0) accumulate(S, pslot, pm, pit);
+            lds_barrier();
+            pslot = (active && last) ? slot : -1;
+            pm = q.m;
+            pit = q.it;
+            (void)par;
+#else
             if (lane == 0) S.xch[par * NW + wid] = key;
             bool last = true;
             if (lane < kWave - 1 && has_next) {
@@ -316,6 +349,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
             pcheck = lane == kWave - 1 && has_next;
             pm = q.m;
             pit = q.it;
+#endif
           }
         }
       }
