@@ -316,6 +316,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     constexpr bool kInten = decltype(inten_c)::value;
     constexpr bool kTagOut = decltype(tagout_c)::value;
     if (inreg) {
+      if (N == 0) return;  // uniform: no peaks (and the batch may hold none to load)
 #pragma unroll
       for (int u0 = 0; u0 < GA_UM; u0 += 8) {
         double itb[8];
@@ -323,7 +324,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const int64_t k = p0 + (int64_t)(u0 + q) * GA_BLOCK + tid;
-            itb[q] = (u0 + q < GA_UM) ? v.inten[k < p1 ? k : (N > 0 ? p0 : 0)] : 0.0;
+            itb[q] = (u0 + q < GA_UM) ? v.inten[k < p1 ? k : p0] : 0.0;
           }
         }
 #pragma unroll

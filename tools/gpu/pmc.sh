@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 rm -rf gpurun_out/pmc && mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-K='spx::(bin_mean_lds_kernel|medoid_small_kernel|medoid_gram_mfma_kernel)'
+K='spx::(bin_mean_lds_kernel|medoid_reg_kernel|medoid_gram_mfma_kernel)'
 run() {  # name script counters...
   local name=$1 scr=$2; shift 2
   timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$K" -d "$R/gpurun_out/pmc/$name" -o "$name" --output-format csv -- python3 $scr > "gpurun_out/pmc/$name.log" 2>&1 || { tail -5 "gpurun_out/pmc/$name.log"; return 1; }
