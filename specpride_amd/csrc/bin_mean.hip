@@ -59,6 +59,9 @@ struct BinMeanState {
 #ifndef SPX_BM_OVL
 #define SPX_BM_OVL 1  // fast path: 63 owned peaks per wave, lane 63 = neighbour only (no cross-wave key exchange)
 #endif
+#ifndef SPX_BM_EMIT2
+#define SPX_BM_EMIT2 1  // phase 4 (LDS kernel): striped slots, ballot positions, one barrier
+#endif
 #ifndef SPX_BM_LENRING
 #define SPX_BM_LENRING 1  // spectrum lengths ride the register ring (no per-step offset read)
 #endif
@@ -403,23 +406,67 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   // phase 4: quorum filter and ordered output (binning.py:181-183, 209-222)
   const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
   const int per = (D + BM_BLOCK - 1) / BM_BLOCK;
-  const int d0 = tid * per;
-  int mine = 0;
-  for (int j = 0; j < per; ++j) {
-    const int d = d0 + j;
-    if (d < D && S.cnt[d] >= quorum && !isnan(S.acc_i[d])) ++mine;  // cnt >= 1: mean NaN iff sum NaN
-  }
   int total;
-  int o = block_exclusive_scan<BM_BLOCK>(mine, tmp, total);
-  for (int j = 0; j < per; ++j) {
-    const int d = d0 + j;
-    if (d < D && S.cnt[d] >= quorum) {
-      const double cn = (double)S.cnt[d];
-      const double mi = (double)S.acc_i[d] / cn;
-      if (isnan(mi)) continue;
-      out.inten[p0 + o] = mi;
-      out.mz[p0 + o] = S.acc_m[d] == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)S.acc_m[d] / cn;
-      ++o;
+#if SPX_BM_EMIT2
+  if constexpr (kSmall) {
+    // Slots striped over the block (slot j*256 + tid): conflict-free LDS reads and
+    // coalesced stores.  A slot's output position = kept slots before it = kept in
+    // earlier stripes + kept in earlier waves of its stripe + earlier lanes of its
+    // wave (ballot).  Per-(stripe, wave) counts go to the dead bitmap: one barrier.
+    constexpr int NW = BM_BLOCK / kWave;
+    int* wcnt = reinterpret_cast<int*>(S.bitmap);  // [per][NW], per <= BM_DCAP / BM_BLOCK
+    const int lane = lane_id(), wid = wave_id();
+    const unsigned long long below = (1ull << lane) - 1ull;
+    uint32_t keep = 0u;  // bit j: slot j*256 + tid is emitted
+    for (int j = 0; j < per; ++j) {
+      const int d = j * BM_BLOCK + tid;
+      const bool k = d < D && S.cnt[d] >= quorum && !isnan(S.acc_i[d]);  // cnt >= 1: mean NaN iff sum NaN
+      const unsigned long long b = __ballot(k);
+      if (lane == 0) wcnt[j * NW + wid] = __popcll(b);
+      keep |= (uint32_t)k << j;
+    }
+    lds_barrier();
+    int base = 0;
+    for (int j = 0; j < per; ++j) {
+      int tot = 0, before = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int x = wcnt[j * NW + w];
+        tot += x;
+        before += w < wid ? x : 0;
+      }
+      const bool k = (keep >> j) & 1u;
+      const unsigned long long b = __ballot(k);
+      if (k) {
+        const int d = j * BM_BLOCK + tid;
+        const int o = base + before + __popcll(b & below);
+        const double cn = (double)S.cnt[d];
+        out.inten[p0 + o] = (double)S.acc_i[d] / cn;
+        out.mz[p0 + o] = S.acc_m[d] == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)S.acc_m[d] / cn;
+      }
+      base += tot;
+    }
+    total = base;
+  } else
+#endif
+  {
+    const int d0 = tid * per;
+    int mine = 0;
+    for (int j = 0; j < per; ++j) {
+      const int d = d0 + j;
+      if (d < D && S.cnt[d] >= quorum && !isnan(S.acc_i[d])) ++mine;  // cnt >= 1: mean NaN iff sum NaN
+    }
+    int o = block_exclusive_scan<BM_BLOCK>(mine, tmp, total);
+    for (int j = 0; j < per; ++j) {
+      const int d = d0 + j;
+      if (d < D && S.cnt[d] >= quorum) {
+        const double cn = (double)S.cnt[d];
+        const double mi = (double)S.acc_i[d] / cn;
+        if (isnan(mi)) continue;
+        out.inten[p0 + o] = mi;
+        out.mz[p0 + o] = S.acc_m[d] == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)S.acc_m[d] / cn;
+        ++o;
+      }
     }
   }
   if (tid == 0) {
