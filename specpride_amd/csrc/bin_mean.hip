@@ -59,6 +59,9 @@ struct BinMeanState {
 #ifndef SPX_BM_OVL
 #define SPX_BM_OVL 1  // fast path: 63 owned peaks per wave, lane 63 = neighbour only (no cross-wave key exchange)
 #endif
+#ifndef SPX_BM_EARLY
+#define SPX_BM_EARLY 1  // fast path: spectrum j-1's accumulator reads issued before spectrum j's key work
+#endif
 #ifndef SPX_BM_EMIT2
 #define SPX_BM_EMIT2 1  // phase 4 (LDS kernel): striped slots, ballot positions, one barrier
 #endif
@@ -298,6 +301,14 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
           if (jb + j < n) {  // uniform
             const int64_t js = jb + j;
             const int par = (int)(js & 1);
+#if SPX_BM_OVL && SPX_BM_EARLY
+            // spectrum j - 1's read-modify-write: the reads go out first (every
+            // lane; non-owners read slot 0 and discard), so their LDS latency
+            // overlaps spectrum j's key and rank work below
+            const int ps = pslot >= 0 ? pslot : 0;
+            const float e_ai = S.acc_i[ps], e_am = S.acc_m[ps];
+            const CountT e_cn = S.cnt[ps];
+#endif
             const Pk q = R[j];
 #if SPX_BM_LENRING
             const int len = q.len;
@@ -326,7 +337,15 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
               bad |= key > kn;
               last = kn != key;
             }
+#if SPX_BM_EARLY
+            if (pslot >= 0) {
+              S.cnt[pslot] = (CountT)(e_cn + 1u);
+              S.acc_i[pslot] = (float)((double)e_ai + pit);
+              S.acc_m[pslot] = (float)((double)e_am + pm);
+            }
+#else
             if (pslot >= 0) accumulate(S, pslot, pm, pit);
+#endif
             lds_barrier();
             pslot = (active && last) ? slot : -1;
             pm = q.m;
