@@ -56,18 +56,6 @@ struct BinMeanState {
   int nmax;  // clusters with more spectra are deferred (leaf-only pairwise mean)
 };
 
-#ifndef SPX_BM_OVL
-#define SPX_BM_OVL 1  // fast path: 63 owned peaks per wave, lane 63 = neighbour only (no cross-wave key exchange)
-#endif
-#ifndef SPX_BM_EARLY
-#define SPX_BM_EARLY 1  // fast path: spectrum j-1's accumulator reads issued before spectrum j's key work
-#endif
-#ifndef SPX_BM_EMIT2
-#define SPX_BM_EMIT2 1  // phase 4 (LDS kernel): striped slots, ballot positions, one barrier
-#endif
-#ifndef SPX_BM_LENRING
-#define SPX_BM_LENRING 1  // spectrum lengths ride the register ring (no per-step offset read)
-#endif
 #ifndef SPX_BM_MINW
 #define SPX_BM_MINW 5  // __launch_bounds__ minimum waves per SIMD for bin_mean_lds_kernel (LDS allows 5)
 #endif
@@ -76,13 +64,9 @@ struct BinMeanState {
 #endif
 
 constexpr int BM_BLOCK = 256;
-#if SPX_BM_OVL
 // fast path: wave w's lanes 0..62 own peaks 63w..63w+62 of the spectrum; lane 63
 // loads peak 63w+63 (owned by wave w+1's lane 0) only to hand lane 62 its key
 constexpr int BM_FASTLEN = 4 * 63;
-#else
-constexpr int BM_FASTLEN = BM_BLOCK;
-#endif
 constexpr int BM_WMAX = 1536;  // 98,304 bins
 constexpr int BM_DCAP = 1536;  // distinct occupied bins per cluster
 constexpr int BM_NMAX = 128;
@@ -96,7 +80,6 @@ struct BinMeanSmem {
   double prec[BM_NMAX];       // precursor m/z (np.mean at the end, from LDS)
   int32_t soff[BM_NMAX + 1];  // the cluster's spectrum offsets, relative to its first peak
   int votes[2 * (BM_BLOCK / kWave)];
-  int32_t xch[2 * (BM_BLOCK / kWave)];  // lane-0 bin key of each wave (fast path neighbour)
   int tmp[BM_BLOCK / kWave + 1];
   int flag;
 };
@@ -244,17 +227,18 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   // phase 3: ordered accumulation, one spectrum at a time
   int64_t slow_from = (P.ablate & 1) ? s1 : s0;
   if (fast && !(P.ablate & 1)) {
-    // Fast path (every spectrum <= 256 peaks; lane t holds peak t of the
-    // spectrum).  Each lane computes ONE bin key (-1 below min, INT_MAX at or
-    // above max) and its slot, and takes its neighbour's key by shuffle; lane
-    // 63's neighbour is the next wave's lane 0, exchanged through LDS.  If keys
-    // are non-decreasing inside every spectrum, equal bins are contiguous and
-    // "last peak of its bin" is a neighbour compare; a key inversion or a NaN
-    // anywhere defers the whole cluster to the generic kernel.
-    // Software-pipelined by one spectrum: iteration j computes spectrum j's
-    // keys and slots (no shared state) while it finishes spectrum j-1 (lane
-    // 63's exchange, then the slot read-modify-write), so the two latency
-    // chains overlap; one LDS-only barrier per spectrum orders the updates.
+    // Fast path (every spectrum <= BM_FASTLEN = 252 peaks).  Wave w's lanes
+    // 0..62 own peaks 63w..63w+62 of the spectrum; lane 63 loads peak 63w+63
+    // (owned by wave w+1's lane 0) only to hand lane 62 its key.  Each lane
+    // computes ONE bin key (-1 below min, INT_MAX at or above max) and its slot,
+    // and takes its neighbour's key by a DPP move.  If keys are non-decreasing
+    // inside every spectrum, equal bins are contiguous and "last peak of its
+    // bin" is a neighbour compare; a key inversion or a NaN anywhere defers the
+    // whole cluster to the generic kernel.
+    // Software-pipelined by one spectrum: iteration j first issues the
+    // accumulator reads of spectrum j-1's read-modify-write, computes spectrum
+    // j's keys and slots (no shared state) while they are in flight, then
+    // writes j-1's sums; one LDS-only barrier per spectrum orders the updates.
     if constexpr (kSmall) {
       // the ring also carries the spectrum's length, so a step reads no offsets
       struct Pk { double m, it; int len; };
@@ -262,11 +246,8 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
       // the saddr + 32-bit voffset form, no 64-bit address arithmetic per fetch
       const double* __restrict__ mzc = v.mz + p0;
       const double* __restrict__ itc = v.inten + p0;
-#if SPX_BM_OVL
-      const int fpos = wave_id() * (kWave - 1) + lane_id();  // this lane's peak in every spectrum
-#else
-      const int fpos = tid;
-#endif
+      const int lane = lane_id();
+      const int fpos = wave_id() * (kWave - 1) + lane;  // this lane's peak in every spectrum
       auto fetch = [&](int64_t j) {
         const int jj = (int)(j < n ? j : n - 1);
         const int a = S.soff[jj], e = S.soff[jj + 1];
@@ -279,8 +260,6 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
         q.it = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(itc) + bo);
         return q;
       };
-      const int lane = lane_id(), wid = wave_id();
-      constexpr int NW = BM_BLOCK / kWave;
       int bad = 0;
       // Rolling register ring: slot j holds spectrum jb + j and is refilled with
       // spectrum jb + j + PF right after it is read, so every load has PF steps
@@ -290,38 +269,23 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
       Pk R[PF];
 #pragma unroll
       for (int j = 0; j < PF; ++j) R[j] = fetch(j);
-      // spectrum j - 1 in flight: its slot (or -1), values, and lane 63's pending key
+      // spectrum j - 1 in flight: its slot (or -1) and values
       int pslot = -1;
-      int32_t pkey = 0;
-      bool pcheck = false;
       double pm = 0.0, pit = 0.0;
       for (int64_t jb = 0; jb < n; jb += PF) {
 #pragma unroll
         for (int j = 0; j < PF; ++j) {
           if (jb + j < n) {  // uniform
             const int64_t js = jb + j;
-            const int par = (int)(js & 1);
-#if SPX_BM_OVL && SPX_BM_EARLY
-            // spectrum j - 1's read-modify-write: the reads go out first (every
-            // lane; non-owners read slot 0 and discard), so their LDS latency
-            // overlaps spectrum j's key and rank work below
+            // spectrum j - 1's accumulator reads first (every lane; non-owners
+            // read slot 0 and discard)
             const int ps = pslot >= 0 ? pslot : 0;
             const float e_ai = S.acc_i[ps], e_am = S.acc_m[ps];
             const CountT e_cn = S.cnt[ps];
-#endif
             const Pk q = R[j];
-#if SPX_BM_LENRING
             const int len = q.len;
-#else
-            const int len = S.soff[js + 1] - S.soff[js];
-#endif
-#if SPX_BM_OVL
             const bool active = fpos < len && lane < kWave - 1, has_next = fpos + 1 < len;
             const bool inr = fpos < len && in_range(q.m, P);  // lane 63 too: its key is lane 62's neighbour
-#else
-            const bool active = tid < len, has_next = tid + 1 < len;
-            const bool inr = active && in_range(q.m, P);
-#endif
             R[j] = fetch(js + PF);
             bad |= active && (q.m != q.m);
             int32_t key = q.m < P.minimum ? -1 : 0x7fffffff;
@@ -331,54 +295,22 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
               slot = bitmap_rank(S.bitmap, S.wprefix, (int64_t)key);
             }
             const int32_t kn = wave_next(key, 0x7fffffff);
-#if SPX_BM_OVL
             bool last = true;
             if (active && has_next) {
               bad |= key > kn;
               last = kn != key;
             }
-#if SPX_BM_EARLY
-            if (pslot >= 0) {
+            if (pslot >= 0) {  // finish spectrum j - 1
               S.cnt[pslot] = (CountT)(e_cn + 1u);
               S.acc_i[pslot] = (float)((double)e_ai + pit);
               S.acc_m[pslot] = (float)((double)e_am + pm);
             }
-#else
-            if (pslot >= 0) accumulate(S, pslot, pm, pit);
-#endif
             lds_barrier();
             pslot = (active && last) ? slot : -1;
             pm = q.m;
             pit = q.it;
-            (void)par;
-#else
-            if (lane == 0) S.xch[par * NW + wid] = key;
-            bool last = true;
-            if (lane < kWave - 1 && has_next) {
-              bad |= key > kn;
-              last = kn != key;
-            }
-            // finish spectrum j - 1: lane 63's neighbour key, then its update
-            if (pcheck) {
-              const int32_t kx = S.xch[(par ^ 1) * NW + wid + 1];
-              bad |= pkey > kx;
-              if (kx == pkey) pslot = -1;
-            }
-            if (pslot >= 0) accumulate(S, pslot, pm, pit);
-            lds_barrier();
-            pslot = last ? slot : -1;
-            pkey = key;
-            pcheck = lane == kWave - 1 && has_next;
-            pm = q.m;
-            pit = q.it;
-#endif
           }
         }
-      }
-      if (pcheck) {
-        const int32_t kx = S.xch[(int)((n - 1) & 1) * NW + wid + 1];
-        bad |= pkey > kx;
-        if (kx == pkey) pslot = -1;
       }
       if (pslot >= 0) accumulate(S, pslot, pm, pit);
       if (block_any<BM_BLOCK, true>(bad, S.votes, 1)) return kDeferred;  // generic kernel redoes it
@@ -426,7 +358,6 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
   const int per = (D + BM_BLOCK - 1) / BM_BLOCK;
   int total;
-#if SPX_BM_EMIT2
   if constexpr (kSmall) {
     // Slots striped over the block (slot j*256 + tid): conflict-free LDS reads and
     // coalesced stores.  A slot's output position = kept slots before it = kept in
@@ -466,9 +397,7 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
       base += tot;
     }
     total = base;
-  } else
-#endif
-  {
+  } else {
     const int d0 = tid * per;
     int mine = 0;
     for (int j = 0; j < per; ++j) {
@@ -506,7 +435,7 @@ __global__ __launch_bounds__(BM_BLOCK, SPX_BM_MINW) void bin_mean_lds_kernel(Csr
                                                                 int32_t* n_deferred) {
   __shared__ BinMeanSmem L;
   const int64_t c = blockIdx.x;
-  BinMeanState<uint16_t, uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, nullptr, L.soff, L.prec, L.votes, L.xch,
+  BinMeanState<uint16_t, uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, nullptr, L.soff, L.prec, L.votes, nullptr,
                            BM_DCAP, BM_NMAX};
   const int32_t st = bin_mean_body<true>(v, P, S, c, out, prec_out, charge_out, L.tmp, &L.flag);
   if (threadIdx.x == 0) {

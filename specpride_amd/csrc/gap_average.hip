@@ -44,10 +44,6 @@ struct GapParams {
 
 constexpr int GA_BLOCK = 512;  // 2 workgroups per CU (LDS): 16 waves
 constexpr int GA_NW = GA_BLOCK / kWave;
-constexpr int GA_U = 12;  // peaks per thread held in registers, m/z + intensity (6,144 per cluster)
-#ifndef SPX_GA_MONLY
-#define SPX_GA_MONLY 1  // registers hold m/z only (GA_UM per thread); intensities streamed in passes 1 and 5
-#endif
 #ifndef SPX_GA_UM
 #define SPX_GA_UM 16
 #endif
@@ -289,7 +285,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1], N = p1 - p0;
   if (n == 0) return kNoGap;
 
-#if SPX_GA_MONLY
   // The cluster's m/z values are read from HBM ONCE into registers when they
   // fit (<= GA_UM per thread = 8,192 peaks: ~80% of the U{2..50} clusters of
   // the configs); passes 2-3 run from registers, and pass 3's slot per peak is
@@ -352,49 +347,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   auto peaks_m = [&](auto f) __attribute__((always_inline)) { peaks_g(std::false_type{}, std::false_type{}, f); };
   auto peaks_m_tag = [&](auto f) __attribute__((always_inline)) { peaks_g(std::false_type{}, std::true_type{}, f); };
   const bool tagged = SPX_GA_TAGS && inreg;  // pass 5 takes pass 3's slots from registers (uniform)
-#else
-  // The cluster's peaks are read from HBM ONCE into registers when they fit
-  // (<= GA_U per thread: every config's U{2..50} clusters); the passes below
-  // then run from registers.  Larger clusters re-read them per pass.
-  const bool inreg = N <= (int64_t)GA_U * GA_BLOCK;  // uniform
-  double rm[GA_U], ri[GA_U];
-  if (inreg) {
-#pragma unroll
-    for (int u = 0; u < GA_U; ++u) {
-      const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
-      const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
-      if (N > 0) {
-        rm[u] = v.mz[kk];
-        ri[u] = v.inten[kk];
-      } else {
-        rm[u] = ri[u] = 0.0;
-      }
-    }
-  }
-  // the precursor summary needs no peaks: wave 0 runs it while the peak loads
-  // above are in flight (its own loads were issued before them), instead of as
-  // a one-wave tail after the last phase
-  if (early && pl && wid == 0 && n <= kWave && !(P.ablate & 32)) *early = precursor_summary_wave(*pl, (int)n, P);
-  // f(m, it, tag): tag is scratch the callee may ignore
-  auto peaks = [&](auto f) __attribute__((always_inline)) {
-    if (inreg) {
-#pragma unroll
-      for (int u = 0; u < GA_U; ++u) {
-        const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
-        int32_t tag = 0;
-        if (k < p1) f(rm[u], ri[u], tag);
-      }
-    } else {
-      gap_peaks<true>(v, p0, p1, [&](int64_t, double m, double it) {
-        int32_t tag = 0;
-        f(m, it, tag);
-      });
-    }
-  };
-  auto peaks_m = peaks;
-  auto peaks_m_tag = peaks;
-  constexpr bool tagged = false;
-#endif
 
   // 1: extrema and finiteness
   double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;

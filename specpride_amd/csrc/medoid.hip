@@ -361,9 +361,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, Medoi
 //   P6  lowest index of the minimum (:103-110), one wave
 // Deferred to the large path: n > 64, > MR_UMAX*256 peaks, a bin outside
 // [0, 65,536), > 1,984 distinct bins.
-#ifndef SPX_MD_SEGOR
-#define SPX_MD_SEGOR 0  // (measured slower: 0.52 vs 0.44 ms for P3) P3: segmented OR of equal row words across lanes before the LDS atomic
-#endif
 constexpr int MR_UMAX = 48;                  // peaks per thread (12,288 per cluster)
 constexpr int MR_PMAX = MR_UMAX * MD_BLOCK;
 constexpr int MR_WMAX = 512;                 // union-bitmap words: bins < 32,768 (m/z < 3,276.8 at 0.1)
@@ -553,45 +550,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
       const uint32_t swlo = __builtin_amdgcn_readlane((uint32_t)my_sw, u);
       const uint32_t swhi = __builtin_amdgcn_readlane((uint32_t)(my_sw >> 32), u);
       const int spw = __builtin_amdgcn_readlane(my_sp, u);
-#if SPX_MD_SEGOR
-      if (!(P.ablate & (128 | 256))) {
-        // Neighbouring peaks of a spectrum mostly share a 32-bit row word, and
-        // same-address LDS atomics serialise: OR the bits of equal words within
-        // each 16-lane row first (DPP row_shl 1/2/4/8 doubling; an equal key at
-        // distance k only ever adds bits of that same word, so any input order
-        // stays exact), then one atomic per run head.
-        int32_t key = -1 - lane;  // inactive lanes: unique, never equal
-        uint32_t bit = 0u;
-        if (r < np) {
-          const uint32_t b = (bins[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-          const MrRec R = L.u.a.rec[b >> 6];
-          const int col = (int)R.pre + __popcll(R.bits & ((1ull << (b & 63)) - 1ull));
-          const unsigned long long sw = ((unsigned long long)swhi << 32) | swlo;
-          const int sp = has_empty ? spectrum_of(L.soff, n, r) : spw + __popcll(sw & upto);
-          key = sp * (2 * KW) + (col >> 5);
-          bit = 1u << (col & 31);
-        }
-        const int32_t kprev = __builtin_amdgcn_update_dpp(-0x7fffffff, key, 0x111, 0xF, 0xF, false);  // row_shr:1
-        uint32_t acc = bit;
-        {
-          const int32_t k1 = __builtin_amdgcn_update_dpp(-0x7fffffff, key, 0x101, 0xF, 0xF, false);
-          const uint32_t b1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x101, 0xF, 0xF, false);
-          if (k1 == key) acc |= b1;
-          const int32_t k2 = __builtin_amdgcn_update_dpp(-0x7fffffff, key, 0x102, 0xF, 0xF, false);
-          const uint32_t b2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x102, 0xF, 0xF, false);
-          if (k2 == key) acc |= b2;
-          const int32_t k4 = __builtin_amdgcn_update_dpp(-0x7fffffff, key, 0x104, 0xF, 0xF, false);
-          const uint32_t b4 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x104, 0xF, 0xF, false);
-          if (k4 == key) acc |= b4;
-          const int32_t k8 = __builtin_amdgcn_update_dpp(-0x7fffffff, key, 0x108, 0xF, 0xF, false);
-          const uint32_t b8 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x108, 0xF, 0xF, false);
-          if (k8 == key) acc |= b8;
-        }
-        if (r < np && ((lane & 15) == 0 || kprev != key))
-          atomicOr(reinterpret_cast<uint32_t*>(L.u.a.rows) + key, acc);
-        continue;
-      }
-#endif
       if (r < np) {
         const uint32_t b = (bins[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
         const MrRec R = L.u.a.rec[b >> 6];
