@@ -2,20 +2,27 @@
 """Headline benchmark: clusters/sec for medoid + bin-mean consensus on MI355X.
 
 BASELINE.json metric: "clusters/sec (whole node) for medoid + binned consensus
-at 1/2/4/8 MI355X"; workload = configs[1]: 100k synthetic clusters of U{2..50}
-spectra, ~200 peaks per spectrum, generated directly in HBM.
+at 1/2/4/8 MI355X".  The metric is quoted on configs[4], the full pipeline on a
+PRIDE-scale dataset of ~10M spectra; real PRIDE data is not available offline,
+so the workload is its synthetic stand-in: 385k clusters of
+U{2..50} spectra (~10.0M spectra, ~2.0G peaks, 32 GB of f64 peaks) generated
+directly in HBM on every rank.
 
-One step = one pass of the hot path over one batch already resident in HBM:
-  spx_bin_mean (combine_bin_mean for every cluster) + spx_medoid (medoid
-  representative for every cluster), results left in HBM.
-Multi-GPU: one process per GPU (torchrun); every rank owns its own 100k-cluster
-shard (clusters are independent: no data-path collective), so scaling is weak
-and value = all ranks' clusters / max-over-ranks time.
+One step = one pass of the hot path over the resident batch:
+  spx_bin_mean (combine_bin_mean, binning.py:170-231, for every cluster) +
+  spx_medoid  (medoid representative, most_similar_representative.py:60-111).
+Multi-GPU (torchrun, one process per GPU): every rank owns its own 385k-cluster
+shard (clusters are independent: weak scaling), and each step's results --
+representatives and the compacted consensus peaks -- are gathered to rank 0
+over RCCL inside the timed region, on a second stream that overlaps the next
+step's kernels.  value = all ranks' clusters / max-over-ranks time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--clusters C]
+Extra keys (single GPU): the gap-average consensus on the same batch, the
+north-star run (1M clusters on one MI355X) and the configs[3] skewed medoid.
 
-Prints ONE JSON line (rank 0).  Also: per-kernel HIP-event timing for the
-roofline object, and the oracle timed on a bounded host sample (cpu_baseline).
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--clusters C] [--ns-clusters 1000000]
+
+Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
 
@@ -30,7 +37,9 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_ACHIEVABLE_GBS = 6290.0  # measured float4 copy ceiling (MI355X_MICROARCH.md chip table)
+I8_DENSE_TOPS = 5000.0       # i8 MFMA dense peak, 2x BF16's ~2.5 PF (MI355X_MICROARCH.md MFMA table)
 
 
 def parse():
@@ -38,8 +47,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--clusters", type=int, default=100_000)
+    ap.add_argument("--clusters", type=int, default=385_000, help="clusters per GPU (configs[4]: ~10M spectra)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--ns-clusters", type=int, default=1_000_000,
+                    help="north-star run size on one GPU (0: skip)")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (profiling runs)")
     ap.add_argument("--cpu-sample", type=int, default=2000, help="clusters in the CPU-baseline sample (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -78,8 +90,8 @@ def max_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-def bin_mean_bytes(batch, kept_peaks: int) -> int:
-    """Algorithmic HBM bytes of one spx_bin_mean launch:
+def consensus_bytes(batch, kept_peaks: int) -> int:
+    """Algorithmic HBM bytes of one spx_bin_mean / spx_gap_average launch:
     read mz+inten (16 B/peak), spec_off + prec_mz + charge (20 B/spectrum),
     cluster_off (8 B/cluster); write 16 B per kept peak + count/prec/charge/status
     (24 B/cluster)."""
@@ -92,14 +104,41 @@ def medoid_bytes(batch) -> int:
     return 8 * batch.n_peaks + 8 * batch.n_spectra + 16 * batch.n_clusters
 
 
-def load_pmc_traffic(kernel: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+def load_pmc_traffic(kernel: str, batch):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (collected on
+    this configuration), scaled to this batch's peak count if it differs."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
-            return json.load(fh).get(kernel)
+            d = json.load(fh)
     except (OSError, ValueError):
         return None
+    v = d.get(kernel)
+    if v is None:
+        return None
+    peaks = d.get("_peaks")
+    return v if not peaks or peaks == batch.n_peaks else v * batch.n_peaks / peaks
+
+
+def roofline(name, kernel, nbytes, ms, traffic=None):
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "frac_of_achievable": round(gbs / HBM_ACHIEVABLE_GBS, 4),
+            "achievable": HBM_ACHIEVABLE_GBS, "traffic": traffic, "launch_ms": round(ms, 4),
+            "algorithmic_bytes": int(nbytes), "entry_point": name}
+
+
+def time_launches(fn, reps, stream):
+    """Average launch duration of fn() by HIP events recorded on its stream."""
+    import torch
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
 
 
 def cpu_baseline(n_clusters: int, seed: int):
@@ -161,15 +200,75 @@ def cpu_baseline_parallel(n_clusters: int, seed: int):
                        f"cluster-parallel): {dt:.2f} s")}
 
 
-def main():
-    args = parse()
+class Gatherer:
+    """Per-step gather of a rank's results to rank 0 over RCCL, on its own stream.
+
+    Each rank compacts its consensus peaks (capacity layout -> dense) and sends
+    counts, representatives and peaks; rank 0 receives every peer's shard into
+    its own buffers (reordering into global cluster order is a host-side index,
+    not part of the device pass).  The gather of step k runs on `self.stream`
+    while step k+1's kernels run on the compute stream; the results of step k
+    are double-buffered so step k+1 never overwrites what is in flight."""
+
+    def __init__(self, batch, rank, world):
+        import torch
+
+        self.rank, self.world, self.batch = rank, world, batch
+        self.stream = torch.cuda.Stream()
+        self.dev = batch.device
+        self.recv = {}
+
+    def launch(self, bm, md, done_event):
+        """Enqueue the gather of one step's results (after `done_event`); returns
+        an event that completes when this rank's part of the gather has."""
+        import torch
+        import torch.distributed as dist
+
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(done_event)
+            if self.rank == 0:
+                ops = []
+                for r in range(1, self.world):
+                    c_r, p_r = self.recv_sizes[r]
+                    bufs = self.recv.get(r)
+                    if bufs is None:
+                        bufs = (torch.empty(c_r, dtype=torch.int64, device=self.dev),
+                                torch.empty(c_r, dtype=torch.int64, device=self.dev),
+                                torch.empty(max(p_r, 1), dtype=torch.float64, device=self.dev),
+                                torch.empty(max(p_r, 1), dtype=torch.float64, device=self.dev))
+                        self.recv[r] = bufs
+                    ops += [dist.P2POp(dist.irecv, b, r) for b in bufs]
+            else:
+                # device-side compaction of this rank's consensus peaks (count known: no sync)
+                _, dmz, dint = bm.compact(stream=self.stream, total=self.send_peaks)
+                n = self.batch.n_clusters
+                one = lambda x: x if x.numel() else torch.zeros(1, dtype=x.dtype, device=x.device)  # noqa: E731
+                ops = [dist.P2POp(dist.isend, bm.count[:n].contiguous(), 0),
+                       dist.P2POp(dist.isend, md.rep[:n].contiguous(), 0),
+                       dist.P2POp(dist.isend, one(dmz), 0), dist.P2POp(dist.isend, one(dint), 0)]
+            for q in (dist.batch_isend_irecv(ops) if ops else []):
+                q.wait()
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return ev
+
+    def plan(self, kept_peaks: int):
+        """Exchange the (fixed) per-rank cluster and kept-peak counts once, so
+        every step's receive buffers are sized without a per-step handshake."""
+        import torch
+        import torch.distributed as dist
+
+        sizes = torch.tensor([self.batch.n_clusters, kept_peaks], dtype=torch.int64, device=self.dev)
+        allsz = [torch.empty_like(sizes) for _ in range(self.world)]
+        dist.all_gather(allsz, sizes)
+        self.recv_sizes = [tuple(int(v) for v in t.cpu()) for t in allsz]
+        self.send_peaks = kept_peaks
+        return sum(s[0] for s in self.recv_sizes), sum(s[1] for s in self.recv_sizes)
+
+
+def headline(args, rank, world, local, out):
     import torch
 
-    world0 = int(os.environ.get("WORLD_SIZE", "1"))
-    cpu_par = None
-    if world0 == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
-        cpu_par = cpu_baseline_parallel(4 * args.cpu_sample, args.seed)
-    rank, world, local = dist_init()
     from specpride_amd import engine
     from specpride_amd.synthetic import make_clusters_torch
 
@@ -178,47 +277,58 @@ def main():
     batch = engine.DeviceBatch.from_device(t)
     torch.cuda.synchronize()
 
+    # checked once, before timing: every cluster resolved by the launches the step makes
     bm = engine.bin_mean(batch)
-    md = engine.medoid(batch)
+    md = engine.medoid(batch, check=True)
     torch.cuda.synchronize()
-    st = bm.status.cpu().numpy()
-    if np.any(st != 0) or np.any(md.rep.cpu().numpy() < 0):
-        raise RuntimeError(f"unexpected statuses: bin-mean {np.unique(st)}, medoid min rep {md.rep.min().item()}")
-    kept = int(bm.count.sum().item())
+    st = bm.status.cpu().numpy()[:batch.n_clusters]
+    rep = md.rep.cpu().numpy()[:batch.n_clusters]
+    if np.any(st != 0) or np.any(rep < 0):
+        raise RuntimeError(f"unexpected statuses: bin-mean {np.unique(st)}, medoid min rep {rep.min()}")
+    kept = int(bm.count[:batch.n_clusters].sum().item())
+    large = engine.medoid_needs_large_path(batch) or bool(batch._ws.get("medoid_extra"))
+    stream = torch.cuda.current_stream()
 
-    def step():
-        engine.bin_mean(batch, out=bm)
-        engine.medoid(batch, out=md)
+    # double-buffered results when gathering (step k's are in flight during step k+1)
+    bufs = [(bm, md)]
+    gat = None
+    if world > 1:
+        bufs.append((engine.bin_mean(batch), engine.medoid(batch, check=False)))
+        gat = Gatherer(batch, rank, world)
+        total_c, total_p = gat.plan(kept)
 
-    for _ in range(args.warmup):
-        step()
+    inflight = [None] * len(bufs)  # per buffer: the event of the gather reading it
+
+    def step(k):
+        i = k % len(bufs)
+        b, m = bufs[i]
+        if inflight[i] is not None:
+            stream.wait_event(inflight[i])  # this buffer's previous gather (step k-2) is done
+        engine.bin_mean(batch, out=b)
+        engine.medoid(batch, out=m, check=False)
+        if gat is not None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            inflight[i] = gat.launch(b, m, ev)
+
+    for k in range(args.warmup):
+        step(k)
     barrier(world)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(k)
+    if gat is not None:
+        gat.stream.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     value = world * batch.n_clusters * args.steps / elapsed
 
-    # per-kernel timing (events on the stream the kernels run on)
-    stream = torch.cuda.current_stream()
+    # per-kernel timing: HIP events on the stream the kernels are launched on
     reps = max(3, args.steps)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    ev[0].record(stream)
-    for _ in range(reps):
-        engine.bin_mean(batch, out=bm)
-    ev[1].record(stream)
-    for _ in range(reps):
-        engine.medoid(batch, out=md)
-    ev[2].record(stream)
-    torch.cuda.synchronize()
-    bm_ms = ev[0].elapsed_time(ev[1]) / reps
-    md_ms = ev[1].elapsed_time(ev[2]) / reps
-    bm_gbs = bin_mean_bytes(batch, kept) / (bm_ms * 1e-3) / 1e9
-    md_gbs = medoid_bytes(batch) / (md_ms * 1e-3) / 1e9
-    traffic = load_pmc_traffic("bin_mean_lds_kernel")
-
-    out = {
+    bm_ms = time_launches(lambda: engine.bin_mean(batch, out=bm), reps, stream)
+    md_ms = time_launches(lambda: engine.medoid(batch, out=md, check=False), reps, stream)
+    bm_bytes = consensus_bytes(batch, kept)
+    out.update({
         "metric": "clusters/sec (whole node) for medoid + binned consensus",
         "value": round(value, 1),
         "unit": "clusters/s",
@@ -230,22 +340,110 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (SURVEY.md §8(d) law, generated in HBM per rank)",
-        "config": {"workload": "configs[1]: binning.py bin-mean + most_similar_representative medoid, "
-                               "U{2..50} spectra/cluster, ~200 peaks/spectrum",
+        "data": "synthetic (SURVEY.md §8(d) law, generated in HBM per rank; stand-in for the ~10M-spectrum PRIDE set)",
+        "config": {"workload": "configs[4]: full pipeline (bin-mean consensus + medoid representative) on a "
+                               "PRIDE-scale clustered dataset of ~10M spectra, U{2..50} spectra/cluster, "
+                               "~200 peaks/spectrum",
                    "clusters_per_gpu": batch.n_clusters, "spectra_per_gpu": batch.n_spectra,
-                   "peaks_per_gpu": batch.n_peaks, "parallelism": f"cluster-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "spx_bin_mean", "achieved": round(bm_gbs, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bm_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "launch_ms": round(bm_ms, 4),
-                     "algorithmic_bytes": bin_mean_bytes(batch, kept)},
-        "kernels": {"spx_bin_mean_ms": round(bm_ms, 4), "spx_medoid_ms": round(md_ms, 4),
-                    "spx_medoid_algorithmic_GBs": round(md_gbs, 1)},
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_sample > 0:
+                   "peaks_per_gpu": batch.n_peaks, "parallelism": f"cluster-sharded x{world}",
+                   "gather": ("per-step RCCL gather of reps + compacted consensus peaks to rank 0, "
+                              "overlapped with the next step" if world > 1 else "none (1 GPU: results stay in HBM)"),
+                   "medoid_large_path": bool(large)},
+        "roofline": roofline("spx_bin_mean", "bin_mean_lds_kernel", bm_bytes, bm_ms,
+                             load_pmc_traffic("bin_mean_lds_kernel", batch)),
+        "roofline_medoid": roofline("spx_medoid", "medoid_reg_kernel", medoid_bytes(batch), md_ms,
+                                    load_pmc_traffic("medoid_reg_kernel", batch)),
+        "kernels": {"spx_bin_mean_ms": round(bm_ms, 4), "spx_medoid_ms": round(md_ms, 4)},
+    })
+    if gat is not None:
+        out["config"]["gathered_clusters_per_step"] = total_c
+        out["config"]["gathered_peaks_per_step"] = total_p
+    if rank == 0 and world == 1 and not args.no_extras:
+        # gap-average consensus on the same resident batch (average_spectrum_clustering.py:26-148)
+        ga = engine.gap_average(batch)
+        torch.cuda.synchronize()
+        gst = ga.status.cpu().numpy()[:batch.n_clusters]
+        gkept = int(ga.count[:batch.n_clusters].sum().item())
+        ga_ms = time_launches(lambda: engine.gap_average(batch, out=ga), reps, stream)
+        out["gap_average"] = {"clusters_per_s": round(batch.n_clusters / (ga_ms * 1e-3), 1), "launch_ms": round(ga_ms, 4),
+                              "ok_clusters": int((gst == 0).sum()),
+                              "roofline": roofline("spx_gap_average", "gap_average_lds_kernel",
+                                                   consensus_bytes(batch, gkept), ga_ms,
+                                                   load_pmc_traffic("gap_average_lds_kernel", batch))}
+        del ga
+    del bm, md, bufs, batch, t
+    torch.cuda.empty_cache()
+
+
+def north_star(args, out):
+    """BASELINE.json north_star: 1M synthetic clusters on one MI355X (configs[2]'s
+    size), bin-mean + medoid, inputs resident in HBM (5.2G peaks, 83 GB)."""
+    import torch
+
+    from specpride_amd import engine
+    from specpride_amd.synthetic import make_clusters_torch
+
+    t = make_clusters_torch(args.ns_clusters, seed=args.seed + 7)
+    batch = engine.DeviceBatch.from_device(t)
+    bm = engine.bin_mean(batch)
+    md = engine.medoid(batch, check=True)
+    torch.cuda.synchronize()
+    ok = bool(np.all(bm.status.cpu().numpy()[:batch.n_clusters] == 0) and
+              np.all(md.rep.cpu().numpy()[:batch.n_clusters] >= 0))
+    steps = max(3, args.steps // 2)
+    engine.bin_mean(batch, out=bm)
+    engine.medoid(batch, out=md, check=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        engine.bin_mean(batch, out=bm)
+        engine.medoid(batch, out=md, check=False)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out["north_star_1m"] = {"clusters": batch.n_clusters, "spectra": batch.n_spectra, "peaks": batch.n_peaks,
+                            "clusters_per_s": round(batch.n_clusters * steps / dt, 1),
+                            "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "all_resolved": ok,
+                            "hbm_gb_resident": round(torch.cuda.max_memory_allocated() / 1e9, 1)}
+    del bm, md, batch, t
+    torch.cuda.empty_cache()
+
+
+def config3(args, out):
+    """configs[3]: medoid on the skewed long tail (MFMA dense-Gram path)."""
+    import torch
+
+    from specpride_amd import engine
+    from specpride_amd.synthetic import make_clusters_torch
+
+    t = make_clusters_torch(20000, seed=4, skewed=True, forced_large=4, large_size=5000)
+    batch = engine.DeviceBatch.from_device(t)
+    md = engine.medoid(batch, check=True)
+    torch.cuda.synchronize()
+    ok = bool(np.all(md.rep.cpu().numpy()[:batch.n_clusters] >= 0))
+    ms = time_launches(lambda: engine.medoid(batch, out=md, check=False), 5, torch.cuda.current_stream())
+    sizes = np.diff(batch.host_cluster_off)
+    out["config3_medoid"] = {"clusters": batch.n_clusters, "spectra": batch.n_spectra, "max_n": int(sizes.max()),
+                             "large_clusters": int((sizes > 64).sum()), "medoid_ms": round(ms, 3),
+                             "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1), "all_resolved": ok}
+    del md, batch, t
+    torch.cuda.empty_cache()
+
+
+def main():
+    args = parse()
+    world0 = int(os.environ.get("WORLD_SIZE", "1"))
+    want_cpu = world0 == 1 and not args.no_cpu_baseline and args.cpu_sample > 0
+    cpu_par = cpu_baseline_parallel(4 * args.cpu_sample, args.seed) if want_cpu else None
+    rank, world, local = dist_init()
+    out = {}
+    headline(args, rank, world, local, out)
+    if rank == 0 and world == 1 and not args.no_extras:
+        config3(args, out)
+        if args.ns_clusters > 0:
+            north_star(args, out)
+    if rank == 0 and want_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.seed)
-        if cpu_par is not None:
-            out["cpu_baseline_all_cores"] = cpu_par
+        out["cpu_baseline_all_cores"] = cpu_par
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define SPX_ABI_VERSION 1
+#define SPX_ABI_VERSION 2
 
 typedef enum spx_error {
   SPX_SUCCESS = 0,
@@ -126,13 +126,31 @@ int spx_gap_average(const spx_csr *csr, const spx_gap_params *params, const spx_
 /* ---- medoid: most_similar_representative.py distance(s1, s2, 'xcorr') with
  *      XQuestScores().xCorrelationPrescore(s1, s2, 0.1) + argmin of summed distance ---- */
 typedef struct spx_medoid_params {
-  double tolerance; /* 0.1 at most_similar_representative.py:15 */
+  double tolerance;   /* 0.1 at most_similar_representative.py:15 */
+  int32_t large_path; /* 1: run the large-cluster (MFMA Gram) passes for clusters the
+                         small-cluster kernel defers; 0: skip them (their rep[c] is then
+                         SPX_REP_DEFERRED).  0 saves ~11 small launches per call when
+                         spx_medoid_needs_large_path() says no cluster is large by size. */
 } spx_medoid_params;
 
-/* Needs the HOST copies of the offsets: the large-cluster arena is sized from them. */
+/* rep[c] codes besides a spectrum index */
+#define SPX_REP_EMPTY (-1)      /* empty cluster */
+#define SPX_REP_RANGE (-2)      /* m/z range > 4.2M bins (> 420k Da at tol 0.1) */
+#define SPX_REP_ARENA (-3)      /* workspace arena exhausted: grow it (extra clusters below), re-run */
+#define SPX_REP_DEFERRED (-4)   /* deferred to the large path, skipped (params.large_path = 0) */
+
+/* Needs the HOST copies of the offsets: the large-cluster arena is sized from them.
+ * `extra` (nullable, n_extra entries) lists clusters to budget a full arena share for on
+ * top of the ones large by size -- the clusters a previous call reported SPX_REP_ARENA
+ * for (small clusters deferred at run time: m/z >= 3276.8 at tol 0.1, > 1,984 distinct
+ * bins).  Budgeting them makes the re-run's arena sufficient. */
 size_t spx_medoid_workspace_size(const int64_t *host_cluster_off, const int64_t *host_spec_off,
-                                 int64_t n_clusters);
-/* rep[c] = global index of the chosen spectrum (-1 empty cluster, <= -2 unresolved);
+                                 int64_t n_clusters, const int64_t *extra, int64_t n_extra);
+/* 1 if some cluster takes the large path by size alone (n > 64 spectra or > 12,288
+ * peaks): then params.large_path must be 1.  0: only run-time deferrals are possible. */
+int spx_medoid_needs_large_path(const int64_t *host_cluster_off, const int64_t *host_spec_off,
+                                int64_t n_clusters);
+/* rep[c] = global index of the chosen spectrum, or an SPX_REP_* code (< 0);
  * totals (nullable) [n_spectra] = the reference's total_dist per spectrum. */
 int spx_medoid(const spx_csr *csr, const spx_medoid_params *params, int64_t *rep, double *totals,
                void *workspace, size_t workspace_bytes, void *stream);

@@ -85,3 +85,42 @@ def medoid(csr, tol=0.1, dense_tables=False, with_totals=False):
     if rc:
         raise MemoryError("spxo_medoid")
     return (rep, totals[:csr.n_spectra]) if with_totals else rep
+
+
+def medoid_parallel(csr, tol=0.1, with_totals=False, threads=None):
+    """:func:`medoid` over cluster chunks in a thread pool (ctypes releases the GIL
+    during the C call): the same per-cluster results, for large test batches."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    C = csr.n_clusters
+    threads = threads or min(16, os.cpu_count() or 1)
+    sizes = np.diff(csr.cluster_off).astype(np.float64)
+    cost = np.cumsum(sizes * sizes + 1.0)
+    bounds = np.searchsorted(cost, np.linspace(0, cost[-1] if C else 0, 4 * threads + 1)[1:-1])
+    edges = np.unique(np.concatenate([[0], bounds, [C]])).astype(np.int64)
+    # the largest clusters on their own, first: they bound the wall time
+    order = np.argsort(-sizes)[:threads]
+    chunks = [np.array([c]) for c in order]
+    rest = np.setdiff1d(np.arange(C), order)
+    for a, b in zip(edges[:-1], edges[1:]):
+        part = rest[(rest >= a) & (rest < b)]
+        if len(part):
+            chunks.append(part)
+    rep = np.zeros(C, np.int64)
+    totals = np.zeros(csr.n_spectra) if with_totals else None
+
+    def run(cl):
+        sub = csr.select(cl)
+        r = medoid(sub, tol, with_totals=with_totals)
+        return cl, sub, r
+
+    with ThreadPoolExecutor(threads) as ex:
+        for cl, sub, r in ex.map(run, chunks):
+            rr, tt = (r if with_totals else (r, None))
+            base = csr.cluster_off[cl]
+            rep[cl] = np.where(rr >= 0, rr - sub.cluster_off[:-1] + base, rr)
+            if with_totals:
+                from specpride_amd.csr import concat_ranges
+
+                totals[concat_ranges(base, np.diff(sub.cluster_off))] = tt
+    return (rep, totals) if with_totals else rep

@@ -56,7 +56,7 @@ class SpxGapParams(ctypes.Structure):
 
 
 class SpxMedoidParams(ctypes.Structure):
-    _fields_ = [("tolerance", _dbl)]
+    _fields_ = [("tolerance", _dbl), ("large_path", _i32)]
 
 
 class SpxCosineParams(ctypes.Structure):
@@ -65,11 +65,11 @@ class SpxCosineParams(ctypes.Structure):
 
 # every symbol include/specpride.h declares (checked by tests/test_host.py)
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_gap_average_workspace_size", "spx_gap_average",
-            "spx_medoid_workspace_size", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine", "spx_best_score",
+            "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine", "spx_best_score",
             "spx_compact_peaks",
             "spx_abi_version", "spx_last_error"]
 
-SPX_ABI_VERSION = 1
+SPX_ABI_VERSION = 2
 _lib = None
 
 
@@ -130,7 +130,9 @@ def lib():
     L.spx_gap_average_workspace_size.argtypes = [_p, _p, _p]
     L.spx_gap_average.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]
     L.spx_medoid_workspace_size.restype = _sz
-    L.spx_medoid_workspace_size.argtypes = [_p, _p, _i64]
+    L.spx_medoid_workspace_size.argtypes = [_p, _p, _i64, _p, _i64]
+    L.spx_medoid_needs_large_path.restype = ctypes.c_int
+    L.spx_medoid_needs_large_path.argtypes = [_p, _p, _i64]
     L.spx_medoid.argtypes = [_p, _p, _p, _p, _p, _sz, _p]
     L.spx_compact_peaks.argtypes = [_p, _p, _p, _p, _p, _p]
     L.spx_xcorr_distance.argtypes = [_p, _p, _p, _i64, _p, _p]

@@ -166,3 +166,28 @@ class SpectraCSR:
     def from_device(cls, d: dict) -> "SpectraCSR":
         g = lambda k: d[k].detach().cpu().numpy()  # noqa: E731
         return cls(g("cluster_off"), g("spec_off"), g("mz"), g("inten"), g("prec_mz"), g("charge"), g("rt"))
+
+    @classmethod
+    def select_from_device(cls, d: dict, clusters) -> "SpectraCSR":
+        """Host copy of only ``clusters`` (in the given order) of a device batch:
+        the peaks are gathered on the device, so a batch of tens of GB need not
+        cross PCIe to check a sample of it."""
+        import torch
+
+        clusters = np.asarray(clusters, np.int64)
+        co = d["cluster_off"].cpu().numpy()
+        so = d["spec_off"].cpu().numpy()
+        sizes = co[clusters + 1] - co[clusters]
+        cluster_off = np.zeros(len(clusters) + 1, np.int64)
+        np.cumsum(sizes, out=cluster_off[1:])
+        spectra = concat_ranges(co[clusters], sizes)
+        lens = so[spectra + 1] - so[spectra]
+        spec_off = np.zeros(len(spectra) + 1, np.int64)
+        np.cumsum(lens, out=spec_off[1:])
+        dev = d["mz"].device
+        idx = torch.from_numpy(concat_ranges(so[spectra], lens)).to(dev)
+        sidx = torch.from_numpy(spectra).to(dev)
+        g = lambda k, i: d[k].index_select(0, i).cpu().numpy()  # noqa: E731
+        return cls(cluster_off, spec_off, g("mz", idx), g("inten", idx), g("prec_mz", sidx), g("charge", sidx),
+                   g("rt", sidx))
+

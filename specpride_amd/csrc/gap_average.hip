@@ -38,7 +38,6 @@ struct GapParams {
   double bucket_w, inv_bucket_w;  // mz_accuracy (LDS path) or mz_accuracy/2 (global path)
   int32_t pepmass_mode;  // 0 lower_median, 1 naive_average, 2 neutral_average
   int32_t rt_mode;       // 0 median, 1 mass_lower_median
-  int32_t ablate;        // profiling only (SPX_ABLATE): stop after phase 1/2/3/4/5 (bits 1..16), 32 no precursor
 };
 
 
@@ -305,7 +304,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       rm[u] = N > 0 ? v.mz[kk] : 0.0;
     }
   }
-  if (early && pl && wid == 0 && n <= kWave && !(P.ablate & 32)) *early = precursor_summary_wave(*pl, (int)n, P);
+  if (early && pl && wid == 0 && n <= kWave) *early = precursor_summary_wave(*pl, (int)n, P);
   // f(m, it, tag) over every peak; kInten false passes it = 0 and loads none
   auto peaks_g = [&](auto inten_c, auto tagout_c, auto f) __attribute__((always_inline)) {
     constexpr bool kInten = decltype(inten_c)::value;
@@ -358,7 +357,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     imax = fmax(imax, fabs(it));
   });
   if (__syncthreads_or(bad)) return kNonFinite;
-  if (P.ablate & 1) return kEmpty;
 
   if (n == 1) {
     // passthrough + dynamic-range filter on the raw spectrum (:88-98)
@@ -415,7 +413,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   __syncthreads();
   const int D = bitmap_prefix<GA_BLOCK>(S.bitmap, S.wprefix, (int)nw, tmp);
   if (D > S.dcap) return kDeferred;
-  if (P.ablate & 2) return kEmpty;
   for (int d = tid; d < D; d += GA_BLOCK) {
     S.cnt[d] = 0u;
     S.gcnt[d] = 0u;
@@ -436,7 +433,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   });
   __syncthreads();
 
-  if (P.ablate & 4) return kEmpty;
   // 4: gaps between consecutive occupied buckets -> emitted group per slot
   const int per = (D + GA_BLOCK - 1) / GA_BLOCK;
   const int d0 = tid * per;
@@ -467,7 +463,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
   __syncthreads();
 
-  if (P.ablate & 8) return kEmpty;
   // 5: fixed-point group sums (exact integer adds: order-independent)
   int ex_m, ex_i;
   frexp(fmax(fabs(lo), fabs(hi)) * (double)N, &ex_m);
@@ -483,7 +478,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   });
   __syncthreads();
 
-  if (P.ablate & 16) return kEmpty;
   // 6: min_fraction filter, dynamic range, ordered output
   const double min_len = P.min_fraction * (double)n;
   const int gper = (E + GA_BLOCK - 1) / GA_BLOCK;
@@ -530,10 +524,6 @@ __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P,
                                            const PrecSummary* early = nullptr) {
   const int64_t s0 = v.cluster_off[c], n = v.cluster_off[c + 1] - s0;
   if (st == kDeferred) return;
-  if (P.ablate & 32) {
-    if (threadIdx.x == 0) status[c] = st;
-    return;
-  }
   if (wave_id() == 0) {
     PrecSummary R{nan_d(), nan_d(), 0, kOk};
     if (early && n > 0 && n <= kWave) R = *early;

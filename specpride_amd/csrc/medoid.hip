@@ -10,17 +10,11 @@
 // is exact and the f64 epilogue follows the reference's operation order, so the
 // chosen index is bit-exact.
 //
-// Small clusters (n <= 64): one 256-thread workgroup per cluster, all in LDS.
-//   1  min/max bin of the cluster, union bitmap of occupied bins (ds_or_b64)
-//   2  popcount prefix -> compact column id per occupied bin (K columns)
-//   3  per spectrum a bit-packed row over the K columns ("densified" bin matrix)
-//   4  all pairs i <= j: c_ij = sum_w popcount(row_i[w] & row_j[w])  (64 bin
-//      pairs per AND+2xBCNT: the bit-packed Gram is cheaper than unpacking)
-//   5  thread i: both pairwise sums over j in one pass, total_i
-//   6  first argmin
-// Large clusters (n > 64, or an LDS overflow) go to a deferred list and run
-// through medoid_build -> medoid_tile_scan -> medoid_gram -> medoid_totals with
-// state in a bump-allocated global scratch.
+// Small clusters (n <= 64): medoid_reg_kernel, one 256-thread workgroup per
+// cluster, all state in LDS (bit-packed rows over the compact bin columns, the
+// bit-packed Gram by AND + popcount).  Large clusters (n > 64, or an LDS
+// overflow) go to a deferred list and through the grid-parallel passes and the
+// MFMA Gram kernel below, with state in a bump-allocated global arena.
 #include <type_traits>
 
 #include "spx_device.hpp"
@@ -29,27 +23,12 @@ namespace spx {
 
 struct MedoidParams {
   double tol, inv_tol;
-  int32_t ablate;  // profiling only (SPX_ABLATE): 16 skip rows+pairs, 32 skip totals
 };
 
 constexpr int MD_BLOCK = 256;
 constexpr int MD_NMAX = 64;
-constexpr int MD_WMAX = 1024;    // union-bitmap words: bin range <= 65,536 (6,553 Da at 0.1)
 constexpr int MD_KWMAX = 31;     // row words (odd stride): <= 1,984 occupied bins per small cluster
-constexpr int MD_PMAX = 16384;   // peaks per small cluster (spectrum-start bitmap)
 
-struct MedoidSmem {
-  unsigned long long bitmap[MD_WMAX];
-  uint16_t wprefix[MD_WMAX];
-  unsigned long long rows[MD_NMAX * MD_KWMAX];
-  uint16_t cmat[MD_NMAX * MD_NMAX];
-  int32_t soff[MD_NMAX + 1];
-  unsigned long long sbits[MD_PMAX / 64];  // bit k set: peak k starts spectrum >= 1
-  uint8_t spre[MD_PMAX / 64];              // spectra started before word w
-  double totals[MD_NMAX];
-  int tmp[MD_BLOCK / kWave + 1];
-  long long red[2 * (MD_BLOCK / kWave)];
-};
 
 __device__ __forceinline__ int64_t md_bin(double m, const MedoidParams& P) {
   return ceil_div_exact(m, P.tol, P.inv_tol);
@@ -104,35 +83,6 @@ __device__ __forceinline__ void dual_pw_leaf(const F& f, int n, int i, double& r
   col = 0.0 + cs;
 }
 
-// Block min/max of the cluster's bins -> (lo, hi); returns false if no peak.
-__device__ bool cluster_bin_range(const CsrView& v, int64_t p0, int64_t p1, const MedoidParams& P,
-                                  long long* red, int64_t& lo, int64_t& hi) {
-  long long l = 0x7fffffffffffffffll, h = -0x7fffffffffffffffll;
-  for (int64_t k = p0 + threadIdx.x; k < p1; k += MD_BLOCK) {
-    const long long b = md_bin(v.mz[k], P);
-    l = b < l ? b : l;
-    h = b > h ? b : h;
-  }
-#pragma unroll
-  for (int o = kWave / 2; o > 0; o >>= 1) {
-    const long long lo2 = __shfl_xor(l, o, kWave), hi2 = __shfl_xor(h, o, kWave);
-    l = lo2 < l ? lo2 : l;
-    h = hi2 > h ? hi2 : h;
-  }
-  if (lane_id() == 0) { red[wave_id()] = l; red[MD_BLOCK / kWave + wave_id()] = h; }
-  __syncthreads();
-  l = red[0];
-  h = red[MD_BLOCK / kWave];
-  for (int w = 1; w < MD_BLOCK / kWave; ++w) {
-    l = red[w] < l ? red[w] : l;
-    h = red[MD_BLOCK / kWave + w] > h ? red[MD_BLOCK / kWave + w] : h;
-  }
-  __syncthreads();
-  lo = l;
-  hi = h;
-  return p1 > p0;
-}
-
 // spectrum (local index) holding cluster-relative peak k, from LDS offsets
 __device__ __forceinline__ int spectrum_of(const int32_t* soff, int n, int32_t k) {
   int lo = 0, hi = n;  // soff[lo] <= k < soff[hi]
@@ -152,8 +102,11 @@ struct MedoidMeta {
   int32_t n, nw1, B1, KW, L, tiles, units, ok;
 };
 
+// Appends cluster c to the deferred list; rep[c] = -4 until the large path
+// (if the call runs it) writes the result.
 __device__ __forceinline__ void md_defer(int64_t c, int64_t s0, int n, int32_t* deferred, int32_t* n_deferred,
-                                         MedoidMeta* meta) {
+                                         MedoidMeta* meta, int64_t* rep) {
+  rep[c] = -4;
   const int32_t slot = atomicAdd(n_deferred, 1);
   deferred[slot] = (int32_t)c;
   MedoidMeta M = {};
@@ -163,180 +116,8 @@ __device__ __forceinline__ void md_defer(int64_t c, int64_t s0, int n, int32_t* 
   meta[slot] = M;
 }
 
-__global__ __launch_bounds__(MD_BLOCK) void medoid_small_kernel(CsrView v, MedoidParams P, int64_t* rep,
-                                                                double* totals_out, int32_t* deferred,
-                                                                int32_t* n_deferred, MedoidMeta* meta) {
-  __shared__ MedoidSmem L;
-  const int tid = threadIdx.x;
-  const int64_t c = blockIdx.x;
-  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
-  const int n = (int)(s1 - s0);
-  if (s1 - s0 > MD_NMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
-    return;
-  }
-  if (n <= 1) {
-    if (tid == 0) {
-      rep[c] = n == 1 ? s0 : -1;
-      if (totals_out && n == 1) totals_out[s0] = 0.0;
-    }
-    return;
-  }
-  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
-  if (p1 - p0 > MD_PMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
-    return;
-  }
-  const int nsw = (int)((p1 - p0 + 63) / 64);
-  for (int w = tid; w < nsw; w += MD_BLOCK) L.sbits[w] = 0ull;
-  // bin range from each spectrum's first and last peak (m/z-sorted spectra);
-  // pass 1 verifies every bin falls inside and defers the cluster otherwise
-  long long blo = 0x7fffffffffffffffll, bhi = -0x7fffffffffffffffll;
-  if (tid <= n) L.soff[tid] = (int32_t)(v.spec_off[s0 + tid] - p0);
-  if (tid < n) {
-    const int64_t a = v.spec_off[s0 + tid], e = v.spec_off[s0 + tid + 1];
-    if (e > a) {
-      blo = md_bin(v.mz[a], P);
-      bhi = md_bin(v.mz[e - 1], P);
-    }
-  }
-  if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
-    const bool empty_spec = tid < n && v.spec_off[s0 + tid + 1] == v.spec_off[s0 + tid];
-    const unsigned long long any_empty = __ballot(empty_spec);
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      const long long l2 = __shfl_xor(blo, o, kWave), h2 = __shfl_xor(bhi, o, kWave);
-      blo = l2 < blo ? l2 : blo;
-      bhi = h2 > bhi ? h2 : bhi;
-    }
-    if (tid == 0) { L.red[0] = blo; L.red[1] = bhi; L.red[2] = any_empty != 0ull; }
-  }
-  __syncthreads();
-  blo = L.red[0];
-  bhi = L.red[1];
-  const bool has_empty = L.red[2] != 0;
-  const bool any = p1 > p0;
-  const int64_t nw = any ? (bhi - blo) / 64 + 1 : 0;
-  if (nw > MD_WMAX || (any && bhi < blo)) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
-    return;
-  }
-  // spectrum of a peak in O(1): a start bit at every spectrum boundary and a
-  // per-word count of the boundaries before it
-  for (int j = 1 + tid; j < n; j += MD_BLOCK) {
-    const int r = L.soff[j];
-    if (r < p1 - p0) atomicOr(&L.sbits[r >> 6], 1ull << (r & 63));
-  }
-  // 1: union bitmap (8 loads in flight per thread)
-  for (int w = tid; w < nw; w += MD_BLOCK) L.bitmap[w] = 0ull;
-  __syncthreads();
-  if (tid < kWave) {  // prefix of start bits (<= 256 words, one wave)
-    int carry = 0;
-    for (int w0 = 0; w0 < nsw; w0 += kWave) {
-      const int w = w0 + tid;
-      const int c1 = w < nsw ? __popcll(L.sbits[w]) : 0;
-      const int inc = wave_inclusive_sum(c1);
-      if (w < nsw) L.spre[w] = (uint8_t)(carry + inc - c1);
-      carry += __shfl(inc, kWave - 1, kWave);
-    }
-  }
-  int outside = 0;
-  for (int64_t k0 = p0 + tid; k0 < p1; k0 += 8 * MD_BLOCK) {
-    double m[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t k = k0 + (int64_t)u * MD_BLOCK;
-      m[u] = k < p1 ? v.mz[k] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (k0 + (int64_t)u * MD_BLOCK >= p1) continue;
-      const int64_t b = md_bin(m[u], P) - blo;
-      if (b < 0 || b >= nw * 64) { outside = 1; continue; }
-      atomicOr(&L.bitmap[b >> 6], 1ull << (b & 63));
-    }
-  }
-  if (__syncthreads_or(outside)) {  // an unsorted spectrum: general path
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
-    return;
-  }
-  // 2: compact columns
-  const int K = bitmap_prefix<MD_BLOCK>(L.bitmap, L.wprefix, (int)nw, L.tmp);
-  // row stride KW is odd: lanes reading rows j, j+1, ... at one word hit
-  // different LDS banks (an even stride of u64s would fold them together)
-  const int KW = ((K + 63) / 64) | 1;
-  if (KW > MD_KWMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
-    return;
-  }
-  // 3: bit-packed rows
-  for (int w = tid; w < n * KW; w += MD_BLOCK) L.rows[w] = 0ull;
-  __syncthreads();
-  if (P.ablate & 16) { if (tid == 0) rep[c] = s0; return; }
-  for (int64_t k0 = p0 + tid; k0 < p1; k0 += 8 * MD_BLOCK) {
-    double m[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t k = k0 + (int64_t)u * MD_BLOCK;
-      m[u] = k < p1 ? v.mz[k] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t k = k0 + (int64_t)u * MD_BLOCK;
-      if (k >= p1) continue;
-      const int col = bitmap_rank(L.bitmap, L.wprefix, md_bin(m[u], P) - blo);
-      const int r = (int)(k - p0);
-      // empty spectra share a start bit: then fall back to the binary search
-      const int sp = has_empty ? spectrum_of(L.soff, n, r)
-                               : (int)L.spre[r >> 6] + __popcll(L.sbits[r >> 6] & ((2ull << (r & 63)) - 1ull));
-      atomicOr(&L.rows[sp * KW + (col >> 6)], 1ull << (col & 63));
-    }
-  }
-  __syncthreads();
-  // 4: shared-bin counts for every pair i <= j: pair p of the row-major upper
-  // triangle, row i starting at i*n - i*(i-1)/2 (recovered by a float sqrt +
-  // integer fix-up: no idle half, no integer division per pair)
-  if (P.ablate & 64) { if (tid == 0) rep[c] = s0; return; }
-  const int NP = n * (n + 1) / 2;
-  auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
-  for (int p = tid; p < NP; p += MD_BLOCK) {
-    const float b2 = 2.0f * n + 1.0f;
-    int i = (int)((b2 - sqrtf(b2 * b2 - 8.0f * (float)p)) * 0.5f);
-    i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
-    while (i > 0 && row_start(i) > p) --i;
-    while (i + 1 < n && row_start(i + 1) <= p) ++i;
-    const int j = i + (p - row_start(i));
-    uint32_t cnt = 0;
-    for (int w = 0; w < KW; ++w) cnt += (uint32_t)__popcll(L.rows[i * KW + w] & L.rows[j * KW + w]);
-    L.cmat[i * n + j] = (uint16_t)cnt;
-    L.cmat[j * n + i] = (uint16_t)cnt;
-  }
-  __syncthreads();
-  // 5: totals (most_similar_representative.py:98-100)
-  if (P.ablate & 32) { if (tid == 0) rep[c] = s0; return; }
-  if (tid < n) {
-    const int i = tid;
-    const int64_t pi = L.soff[i + 1] - L.soff[i];
-    double row, col;
-    dual_pw_leaf([&](int j) { return md_dist(L.cmat[i * n + j], pi, L.soff[j + 1] - L.soff[j]); }, n, i, row, col);
-    const double t = (row + col) / (double)n;
-    L.totals[i] = t;
-    if (totals_out) totals_out[s0 + i] = t;
-  }
-  __syncthreads();
-  // 6: first index of the minimum (:103-110)
-  if (tid == 0) {
-    int best = 0;
-    double bt = L.totals[0];
-    for (int i = 1; i < n; ++i)
-      if (L.totals[i] < bt) { bt = L.totals[i]; best = i; }
-    rep[c] = s0 + best;
-  }
-}
-
-// ------------------------------------------------- small clusters, v2 (default)
-// medoid_reg_kernel: the same algorithm as medoid_small_kernel with every m/z
-// read from HBM exactly ONCE (8 B per peak, the algorithmic minimum) and the
+// ---------------------------------------------------------- small clusters
+// medoid_reg_kernel: every m/z read from HBM exactly ONCE (8 B per peak, the algorithmic minimum) and the
 // per-peak LDS traffic cut to two operations:
 //   P1  flat coalesced pass over the cluster's peaks (peak r = u*256 + tid,
 //       8 loads in flight per thread): absolute bin ceil(mz/tol) < 65,536, kept
@@ -396,7 +177,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
   const int n = (int)(s1 - s0);
   if (s1 - s0 > MD_NMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
     return;
   }
   if (n <= 1) {
@@ -409,7 +190,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
   const int np = (int)(p1 - p0);
   if (p1 - p0 > MR_PMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
     return;
   }
   const double* __restrict__ mzc = v.mz + p0;
@@ -444,7 +225,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     }
   }
 
-  if (P.ablate & 1024) { if (tid == 0) rep[c] = s0; return; }  // profiling: P0 only
   // P1: one read of every m/z; bins packed two per register.  Batches of 8
   // loads per thread, double-buffered (batch b+1 in flight while b is binned).
   // The batch count is a compile-time constant per size class, so every load
@@ -482,8 +262,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
               b = (uint32_t)bb;
               bmax = b > bmax ? b : bmax;
               // 32-bit half of the occupancy word (same-address LDS atomics serialise)
-              if (!(P.ablate & 2048))
-                atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rec[b >> 6].bits) + ((b >> 5) & 1), 1u << (b & 31));
+              atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rec[b >> 6].bits) + ((b >> 5) & 1), 1u << (b & 31));
             }
           }
           if (u & 1) bins[u >> 1] |= b << 16;
@@ -504,11 +283,10 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   static_assert(NB == 6, "size classes above cover MR_UMAX = 48");
   if (bmax) atomicMax(reinterpret_cast<int*>(&L.red[0]), (int)bmax);
   if (__syncthreads_or(outside)) {  // m/z out of the LDS bitmap's range: general path
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
     return;
   }
   const int nw = np > 0 ? (int)(L.red[0] >> 6) + 1 : 0;
-  if (P.ablate & 4096) { if (tid == 0) rep[c] = s0 + (bins[0] & 1); return; }  // profiling: P0 + P1
   // P2: compact columns (exclusive popcount prefix into the records)
   int K;
   {
@@ -528,7 +306,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   // different LDS banks (an even stride of u64s would fold them together)
   const int KW = ((K + 63) / 64) | 1;
   if (KW > MD_KWMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta);
+    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
     return;
   }
   // P3: bit-packed rows from the register bins
@@ -541,7 +319,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     if (lane < MR_UMAX && w < nsw) { my_sw = L.u.a.sbits[w]; my_sp = L.u.a.spre[w]; }
   }
   __syncthreads();
-  if (P.ablate & 16) { if (tid == 0) rep[c] = s0; return; }
   const unsigned long long upto = (2ull << lane) - 1ull;  // bits 0..lane
 #pragma unroll
   for (int u = 0; u < MR_UMAX; ++u) {
@@ -557,20 +334,13 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
         // empty spectra share a start bit: then the binary search
         const unsigned long long sw = ((unsigned long long)swhi << 32) | swlo;
         const int sp = has_empty ? spectrum_of(L.soff, n, r) : spw + __popcll(sw & upto);
-        if (P.ablate & 128) {  // profiling: no row update
-          if (col < 0) L.u.a.rows[0] = 1ull;
-        } else if (P.ablate & 256) {  // profiling: conflict-free addresses
-          atomicOr(&L.u.a.rows[(tid + (sp * KW + (col >> 6)) * 0) % (n * KW)], 1ull << (col & 63));
-        } else {
-          // 32-bit halves: consecutive peaks of a spectrum share a row word, and
-          // same-address LDS atomics serialise -- half as many per address
-          atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[sp * KW]) + (col >> 5), 1u << (col & 31));
-        }
+        // 32-bit halves: consecutive peaks of a spectrum share a row word, and
+        // same-address LDS atomics serialise -- half as many per address
+        atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[sp * KW]) + (col >> 5), 1u << (col & 31));
       }
     }
   }
   __syncthreads();
-  if (P.ablate & 64) { if (tid == 0) rep[c] = s0; return; }
 
   // P4: every pair i <= j of the row-major upper triangle (row i starts at
   // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
@@ -610,7 +380,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   // D(a, b) of the reference's dense matrix: the upper triangle incl. the
   // diagonal, zeros below (most_similar_representative.py:91-93)
   auto dval = [&](int a, int b) -> double { return b >= a ? L.u.d[row_start(a) + b - a] : 0.0; };
-  if (P.ablate & 32) { if (tid == 0) rep[c] = s0; return; }
 
   // P5: totals, 16 lanes per spectrum (8 row accumulators, 8 column ones)
   const int k = lane & 7;

@@ -15,10 +15,7 @@
 
 #include "../../include/specpride.h"
 #include "best_score.hip"
-#include "bin_mean_stream.hip"  // includes bin_mean.hip
-#include "bin_mean_wave.hip"
-#include "bin_mean_fast.hip"
-#include "bin_mean_ranges.hip"
+#include "bin_mean.hip"
 #include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
@@ -69,47 +66,6 @@ constexpr int kFallbackBlocks = 64;
 
 int64_t fallback_grid(int64_t C) { return std::max<int64_t>(1, std::min<int64_t>(C, kFallbackBlocks)); }
 
-// Profiling-only phase ablation (SPX_ABLATE bitmask, see the kernels); 0 in normal use.
-int32_t ablate_mask() {
-  const char* e = std::getenv("SPX_ABLATE");
-  return e ? (int32_t)std::atoi(e) : 0;
-}
-
-// Bin-mean kernel: 0 = per-cluster two-pass LDS kernel (default: fastest
-// measured), 7 = wave-private bin ranges with no per-spectrum barrier,
-// 8 = buffer-load / float2 variant of 0 (7 and 8 derive counts from the m/z
-// sums, so they run only where bin_counts_derivable holds), 9 = wave-private
-// ranges with boundaries found in the first pass, 1 = per-bin list
-// kernel, 2 = fold kernel, 3/4 = per-cluster hash kernel (2048/4096 slots),
-// 5 = persistent stream + hash fold, 6 = persistent stream + bitmap-rank fold
-// (DESIGN.md §3 has the measurements).  SPX_BIN_KERNEL selects (A/B profiling).
-bool bin_counts_derivable(const spx_bin_params* p) {
-  return p->minimum > 0.0 && 128.0 * (p->binsize / p->minimum) + 128.0 * 128.0 * 0x1p-23 < 0.45;
-}
-
-int bin_kernel_variant(const spx_bin_params* p) {
-  const char* e = std::getenv("SPX_BIN_KERNEL");
-  const int v = e ? std::atoi(e) : 0;
-  return ((v == 7 || v == 8) && !bin_counts_derivable(p)) ? 0 : v;
-}
-
-// Workgroups of the persistent bin-mean kernel: BS_BLOCKS_PER_CU per CU (its
-// LDS and VGPR budgets admit exactly that many), never more than clusters.
-int64_t stream_grid(int64_t C) {
-  int dev = 0, ncu = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                               hipSuccess || ncu <= 0)
-    ncu = 256;
-  return std::max<int64_t>(1, std::min<int64_t>({C, (int64_t)ncu * spx::BS_BLOCKS_PER_CU, spx::BS_PLAN_MAX}));
-}
-
-// Small-cluster medoid kernel: 0 = medoid_reg_kernel (one m/z read, default),
-// 1 = medoid_small_kernel (two reads).  SPX_MEDOID_KERNEL selects (A/B profiling).
-int medoid_kernel_variant() {
-  const char* e = std::getenv("SPX_MEDOID_KERNEL");
-  return e ? std::atoi(e) : 0;
-}
-
 int32_t bin_words(const spx_bin_params* p) {
   const double nb = std::trunc((p->maximum - p->minimum) / p->binsize) + 1.0;  // binning.py:172
   return (int32_t)((nb + 63.0) / 64.0);
@@ -133,7 +89,6 @@ size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* par
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   return align256(sizeof(int32_t)) + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
-         align256(sizeof(int32_t) * (spx::BS_PLAN_MAX + 1)) +
          (size_t)fallback_grid(C) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
@@ -153,7 +108,6 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
   int32_t* n_def = w.take<int32_t>(1);
   int32_t* def = w.take<int32_t>((size_t)C);
-  int32_t* plan = w.take<int32_t>(spx::BS_PLAN_MAX + 1);
   char* scratch = w.base + w.used;
 
   spx::BinMeanParams P;
@@ -163,62 +117,14 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   P.inv_binsize = 1.0 / params->binsize;
   P.apply_quorum = params->apply_peak_quorum ? 1 : 0;
   P.n_words = bin_words(params);
-  P.ablate = ablate_mask();
   spx::PeaksOut O{out->mz, out->inten, out->count};
   const spx::CsrView V = view(csr);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
   if (hipMemsetAsync(n_def, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
-  const int64_t G = stream_grid(C);
-  // the stream kernel addresses a workgroup's range with 32-bit offsets: bound
-  // the range (weight / G + one cluster) well below 2^28 peaks
-  const int64_t wtot = csr->n_peaks + 64 * csr->n_spectra + 1024 * C;
-  const bool range_ok = wtot / G + info->max_cluster_peaks + 64 * info->max_cluster_spectra + 1024 < (int64_t(1) << 28);
-  const int bv = bin_kernel_variant(params);
-  if ((bv == 5 || bv == 6) && P.n_words <= spx::BM_WMAX && range_ok) {
-    const unsigned pg = (unsigned)std::min<int64_t>((C + 1 + 255) / 256, 1024);
-    hipLaunchKernelGGL(spx::range_plan_kernel, dim3(pg), dim3(256), 0, s, V, (int32_t)G, plan);
-    if (int rc = check_launch("range_plan_kernel")) return rc;
-    if (bv == 6)
-      hipLaunchKernelGGL(spx::bin_mean_stream2_kernel, dim3((unsigned)G), dim3(spx::BM_BLOCK), 0, s, V, P, O,
-                         prec_out, charge_out, status, def, n_def, plan);
-    else
-      hipLaunchKernelGGL(spx::bin_mean_stream_kernel<spx::BS_H>, dim3((unsigned)G), dim3(spx::BM_BLOCK), 0, s, V, P,
-                         O, prec_out, charge_out, status, def, n_def, plan);
-    if (int rc = check_launch("bin_mean_stream_kernel")) return rc;
-  } else if (bv == 9) {
-    hipLaunchKernelGGL(spx::bin_mean_ranges_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                       charge_out, status, def, n_def);
-    if (int rc = check_launch("bin_mean_ranges_kernel")) return rc;
-  } else if (bv == 8) {
-    hipLaunchKernelGGL(spx::bin_mean_fast_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                       charge_out, status, def, n_def);
-    if (int rc = check_launch("bin_mean_fast_kernel")) return rc;
-  } else if (bv == 7) {
-    hipLaunchKernelGGL(spx::bin_mean_wave_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                       charge_out, status, def, n_def);
-    if (int rc = check_launch("bin_mean_wave_kernel")) return rc;
-  } else if (bv == 3 || bv == 4) {
-    if (bv == 3)
-      hipLaunchKernelGGL(spx::bin_mean_hash_kernel<2048>, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O,
-                         prec_out, charge_out, status, def, n_def);
-    else
-      hipLaunchKernelGGL(spx::bin_mean_hash_kernel<4096>, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O,
-                         prec_out, charge_out, status, def, n_def);
-    if (int rc = check_launch("bin_mean_hash_kernel")) return rc;
-  } else if (bv == 2) {
-    hipLaunchKernelGGL(spx::bin_mean_fold_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                       charge_out, status, def, n_def);
-    if (int rc = check_launch("bin_mean_fold_kernel")) return rc;
-  } else if (bv == 1) {
-    hipLaunchKernelGGL(spx::bin_mean_list_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                       charge_out, status, def, n_def);
-    if (int rc = check_launch("bin_mean_list_kernel")) return rc;
-  } else {
-    hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                       charge_out, status, def, n_def);
-    if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
-  }
+  hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                     charge_out, status, def, n_def);
+  if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)fallback_grid(C)), dim3(spx::BM_BLOCK), 0, s, V, P,
                      O, prec_out, charge_out, status, def, n_def, scratch,
                      spx::bin_mean_slice_bytes(P.n_words, dcap), (int)std::min<int64_t>(dcap, INT32_MAX));
@@ -261,7 +167,6 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   P.rt_mode = params->rt_mode;
   P.bucket_w = params->mz_accuracy;
   P.inv_bucket_w = 1.0 / params->mz_accuracy;
-  P.ablate = ablate_mask();
   spx::PeaksOut O{out->mz, out->inten, out->count};
   const spx::CsrView V = view(csr);
   const int wcap = gap_wcap(params, info);
@@ -281,8 +186,29 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
 }
 
 // ------------------------------------------------------------------- medoid
-size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t C) {
-  if (C < 0 || (C > 0 && (!hco || !hso))) return 0;
+}  // extern "C"
+
+namespace {
+// Arena bytes of one deferred cluster of n spectra and p peaks (K <= p columns).
+size_t medoid_cluster_bytes(int64_t n, int64_t p) {
+  const int64_t K = std::max<int64_t>(p, 1);  // occupied bins <= peaks
+  const int64_t KW = ((K + 63) / 64 + 7) / 8 * 8;
+  const int64_t T = (n + spx::MD_GT - 1) / spx::MD_GT;
+  const int64_t B1 = std::min<int64_t>(K, 64 * (int64_t)spx::MD_L1WORDS);
+  const int64_t L = spx::md_max_leaves(n);
+  return (size_t)(spx::md_l1_bytes() + spx::md_align(B1 * 12 + 8) + spx::md_align(T * spx::MD_GT * KW * 8) +
+                  spx::md_align(n * n * 4) + spx::md_align((5 * L + 1) * 4) + spx::md_align(2 * (2 * L) * n * 8) +
+                  spx::md_align(n * 8));
+}
+
+bool medoid_large_by_size(int64_t n, int64_t p) { return n > spx::MD_NMAX || p > spx::MR_PMAX; }
+}  // namespace
+
+extern "C" {
+
+size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t C, const int64_t* extra,
+                                 int64_t n_extra) {
+  if (C < 0 || (C > 0 && (!hco || !hso)) || n_extra < 0 || (n_extra > 0 && !extra)) return 0;
   const size_t Cm = (size_t)std::max<int64_t>(C, 1);
   size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(sizeof(int32_t) * Cm) +
                  align256(sizeof(spx::MedoidMeta) * Cm) + 3 * align256(sizeof(int64_t) * (Cm + 1));
@@ -290,21 +216,25 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
   for (int64_t c = 0; c < C; ++c) {
     const int64_t n = hco[c + 1] - hco[c];
     const int64_t p = hso[hco[c + 1]] - hso[hco[c]];
-    const int64_t K = std::max<int64_t>(p, 1);  // occupied bins <= peaks
-    const int64_t KW = ((K + 63) / 64 + 7) / 8 * 8;
-    const int64_t T = (n + spx::MD_GT - 1) / spx::MD_GT;
-    const int64_t B1 = std::min<int64_t>(K, 64 * (int64_t)spx::MD_L1WORDS);
-    const int64_t L = spx::md_max_leaves(n);
-    const size_t bytes = (size_t)(spx::md_l1_bytes() + spx::md_align(B1 * 12 + 8) +
-                                  spx::md_align(T * spx::MD_GT * KW * 8) + spx::md_align(n * n * 4) +
-                                  spx::md_align((5 * L + 1) * 4) + spx::md_align(2 * (2 * L) * n * 8) +
-                                  spx::md_align(n * 8));
-    if (n > spx::MD_NMAX) arena += bytes;
+    const size_t bytes = medoid_cluster_bytes(n, p);
+    if (medoid_large_by_size(n, p)) arena += bytes;
     else if (n > 1) margin = std::max(margin, bytes);
   }
-  // small clusters that overflow LDS at run time land in the arena too: keep room
-  // for a few of the largest ones on top of the clusters routed there by size.
+  for (int64_t k = 0; k < n_extra; ++k) {
+    const int64_t c = extra[k];
+    if (c < 0 || c >= C) return 0;
+    arena += medoid_cluster_bytes(hco[c + 1] - hco[c], hso[hco[c + 1]] - hso[hco[c]]);
+  }
+  // small clusters deferred at run time land in the arena too: room for a few of
+  // the largest on top (a call that runs out reports SPX_REP_ARENA for them, and a
+  // re-run with those clusters in `extra` has room for every one)
   return fixed + arena + 8 * margin + (size_t(1) << 20);
+}
+
+int spx_medoid_needs_large_path(const int64_t* hco, const int64_t* hso, int64_t C) {
+  for (int64_t c = 0; c < C; ++c)
+    if (medoid_large_by_size(hco[c + 1] - hco[c], hso[hco[c + 1]] - hso[hco[c]])) return 1;
+  return 0;
 }
 
 int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep, double* totals, void* workspace,
@@ -326,7 +256,7 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   if (w.used >= workspace_bytes) return fail(SPX_ENOSPACE, "spx_medoid: workspace too small");
   char* arena = w.base + w.used;
   const int64_t arena_bytes = (int64_t)(workspace_bytes - w.used);
-  spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance, ablate_mask()};
+  spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance};
   const spx::CsrView V = view(csr);
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024));
   // grid-stride passes: 32 deferred clusters at a time x 64 blocks fills the chip,
@@ -334,11 +264,9 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   const dim3 grid2(spx::MD_GRIDX, std::min<unsigned>(g, 32u)), blk(spx::MD_BLOCK);
 
   if (hipMemsetAsync(n_def, 0, 512, s) != hipSuccess) return check_launch("spx_medoid memset");
-  if (medoid_kernel_variant() == 1)
-    hipLaunchKernelGGL(spx::medoid_small_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, def, n_def, meta);
-  else
-    hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, def, n_def, meta);
-  if (int rc = check_launch("medoid small-cluster kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, def, n_def, meta);
+  if (int rc = check_launch("medoid_reg_kernel")) return rc;
+  if (!params->large_path) return SPX_SUCCESS;  // deferred clusters keep rep = SPX_REP_DEFERRED
   hipLaunchKernelGGL(spx::medoid_range_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena, bump, arena_bytes);
   if (int rc = check_launch("medoid_range_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_l1_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena);
@@ -371,7 +299,7 @@ extern "C" int spx_xcorr_distance(const spx_csr* csr, const spx_medoid_params* p
     return fail(SPX_EINVAL, "spx_xcorr_distance: null argument");
   if (!(params->tolerance > 0)) return fail(SPX_EINVAL, "spx_xcorr_distance: tolerance must be > 0");
   if (n_pairs <= 0) return SPX_SUCCESS;
-  spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance, 0};
+  spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance};
   hipLaunchKernelGGL(spx::xcorr_pairs_kernel, dim3((unsigned)((n_pairs + 3) / 4)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), view(csr), P, pairs, n_pairs, out);
   return check_launch("xcorr_pairs_kernel");

@@ -103,21 +103,27 @@ class PeaksResult:
     prec: object
     charge: object
     rt: object = None
+    stream: object = None  # the torch stream the producing kernel was enqueued on
 
-    def compact(self):
-        """Dense device arrays: (out_off [C+1], mz, inten)."""
+    def compact(self, stream=None, total: Optional[int] = None):
+        """Dense device arrays: (out_off [C+1], mz, inten).  Enqueued on ``stream``
+        (default: the stream the producing kernel ran on, so compaction never
+        reads a result that is still being written).  ``total`` = the known number
+        of kept peaks skips the one host read of the count sum (no sync)."""
         import torch
 
+        st = stream if stream is not None else (self.stream or torch.cuda.current_stream())
         C = self.batch.n_clusters
-        out_off = torch.zeros(C + 1, dtype=torch.int64, device=self.count.device)
-        if C:
-            torch.cumsum(self.count, 0, out=out_off[1:])
-        n = int(out_off[-1].item()) if C else 0
-        dmz = torch.empty(max(n, 1), dtype=torch.float64, device=self.count.device)
-        dint = torch.empty_like(dmz)
-        src = _lib.SpxPeaksOut(_ptr(self.mz), _ptr(self.inten), _ptr(self.count))
-        _lib.check(_lib.lib().spx_compact_peaks(ctypes.byref(self.batch.csr), ctypes.byref(src), _ptr(out_off),
-                                                _ptr(dmz), _ptr(dint), _stream_handle()), "spx_compact_peaks")
+        with torch.cuda.stream(st):
+            out_off = torch.zeros(C + 1, dtype=torch.int64, device=self.count.device)
+            if C:
+                torch.cumsum(self.count[:C], 0, out=out_off[1:])
+            n = total if total is not None else (int(out_off[-1].item()) if C else 0)
+            dmz = torch.empty(max(n, 1), dtype=torch.float64, device=self.count.device)
+            dint = torch.empty_like(dmz)
+            src = _lib.SpxPeaksOut(_ptr(self.mz), _ptr(self.inten), _ptr(self.count))
+            _lib.check(_lib.lib().spx_compact_peaks(ctypes.byref(self.batch.csr), ctypes.byref(src), _ptr(out_off),
+                                                    _ptr(dmz), _ptr(dint), _stream_handle(st)), "spx_compact_peaks")
         return out_off, dmz[:n], dint[:n]
 
     def to_host(self) -> dict:
@@ -149,6 +155,7 @@ def bin_mean(batch: DeviceBatch, minimum=100.0, maximum=2000.0, binsize=0.02, ap
     if out is None:
         mz, it, cnt, st, prec, ch = _alloc_peaks(batch)
         out = PeaksResult(batch, mz, it, cnt, st, prec, ch)
+    out.stream = stream
     po = _lib.SpxPeaksOut(_ptr(out.mz), _ptr(out.inten), _ptr(out.count))
     _lib.check(L.spx_bin_mean(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info), ctypes.byref(po),
                               _ptr(out.prec), _ptr(out.charge), _ptr(out.status), _ptr(ws), ws.numel(),
@@ -173,6 +180,7 @@ def gap_average(batch: DeviceBatch, mz_accuracy=0.01, dyn_range=1000.0, min_frac
         mz, it, cnt, st, prec, ch = _alloc_peaks(batch)
         out = PeaksResult(batch, mz, it, cnt, st, prec, ch,
                           rt=torch.empty(max(batch.n_clusters, 1), dtype=torch.float64, device=batch.device))
+    out.stream = stream
     po = _lib.SpxPeaksOut(_ptr(out.mz), _ptr(out.inten), _ptr(out.count))
     _lib.check(L.spx_gap_average(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info),
                                  ctypes.byref(po), _ptr(out.prec), _ptr(out.charge), _ptr(out.rt), _ptr(out.status),
@@ -180,35 +188,77 @@ def gap_average(batch: DeviceBatch, mz_accuracy=0.01, dyn_range=1000.0, min_frac
     return out
 
 
+REP_EMPTY, REP_RANGE, REP_ARENA, REP_DEFERRED = -1, -2, -3, -4  # include/specpride.h SPX_REP_*
+
+
 @dataclass
 class MedoidResult:
-    rep: object     # [C] int64 global spectrum index (-1 empty, <= -2 unresolved)
+    rep: object     # [C] int64 global spectrum index, or a REP_* code (< 0)
     totals: object  # [S] f64 or None
 
     def to_host(self):
         return self.rep.cpu().numpy(), (None if self.totals is None else self.totals.cpu().numpy())
 
 
-def medoid(batch: DeviceBatch, tolerance=0.1, with_totals=False, out: Optional[MedoidResult] = None,
-           stream=None) -> MedoidResult:
-    """distance() + the medoid loop (most_similar_representative.py:13-111) for every cluster."""
-    import torch
-
+def _medoid_launch(batch: DeviceBatch, tolerance, large_path: bool, out: MedoidResult, extra, stream):
     L = _lib.lib()
-    prm = _lib.SpxMedoidParams(float(tolerance))
-    key = "medoid_size"
+    key = ("medoid_size", tuple(extra))
     need = batch._ws.get(key)
     if need is None:
+        ex = np.ascontiguousarray(extra, np.int64)
         need = L.spx_medoid_workspace_size(batch.host_cluster_off.ctypes.data_as(ctypes.c_void_p),
-                                           batch.host_spec_off.ctypes.data_as(ctypes.c_void_p), batch.n_clusters)
+                                           batch.host_spec_off.ctypes.data_as(ctypes.c_void_p), batch.n_clusters,
+                                           ex.ctypes.data_as(ctypes.c_void_p) if len(ex) else None, len(ex))
+        if need == 0:
+            raise ValueError("spx_medoid_workspace_size: invalid offsets")
         batch._ws[key] = need
     ws = batch.workspace("medoid", need)
+    prm = _lib.SpxMedoidParams(float(tolerance), int(bool(large_path)))
+    _lib.check(L.spx_medoid(ctypes.byref(batch.csr), ctypes.byref(prm), _ptr(out.rep), _ptr(out.totals), _ptr(ws),
+                            ws.numel(), _stream_handle(stream)), "spx_medoid")
+
+
+def medoid_needs_large_path(batch: DeviceBatch) -> bool:
+    """True if some cluster takes the large (MFMA) path by size alone (host query, cached)."""
+    v = batch._ws.get("medoid_needs_large")
+    if v is None:
+        v = bool(_lib.lib().spx_medoid_needs_large_path(batch.host_cluster_off.ctypes.data_as(ctypes.c_void_p),
+                                                         batch.host_spec_off.ctypes.data_as(ctypes.c_void_p),
+                                                         batch.n_clusters))
+        batch._ws["medoid_needs_large"] = v
+    return v
+
+
+def medoid(batch: DeviceBatch, tolerance=0.1, with_totals=False, out: Optional[MedoidResult] = None,
+           stream=None, check: bool = True) -> MedoidResult:
+    """distance() + the medoid loop (most_similar_representative.py:13-111) for every cluster.
+
+    The large-cluster passes are launched only when some cluster is large by size
+    (spx_medoid_needs_large_path).  With ``check`` (the default) the call then waits
+    for the result and, if a cluster was deferred at run time (REP_DEFERRED) or
+    ran out of arena (REP_ARENA), re-runs with the large path on and those clusters
+    budgeted in the arena, so every cluster comes back resolved or REP_RANGE.
+    ``check=False`` only enqueues (timed loops that were checked once)."""
+    import torch
+
     if out is None:
         out = MedoidResult(torch.empty(max(batch.n_clusters, 1), dtype=torch.int64, device=batch.device),
                            torch.empty(max(batch.n_spectra, 1), dtype=torch.float64, device=batch.device)
                            if with_totals else None)
-    _lib.check(L.spx_medoid(ctypes.byref(batch.csr), ctypes.byref(prm), _ptr(out.rep), _ptr(out.totals), _ptr(ws),
-                            ws.numel(), _stream_handle(stream)), "spx_medoid")
+    large = medoid_needs_large_path(batch)
+    extra = batch._ws.get("medoid_extra", ())
+    _medoid_launch(batch, tolerance, large or bool(extra), out, extra, stream)
+    if not check or batch.n_clusters == 0:
+        return out
+    for _ in range(2):
+        rep = out.rep[:batch.n_clusters]
+        bad = torch.nonzero((rep == REP_DEFERRED) | (rep == REP_ARENA)).flatten().cpu().numpy()
+        if len(bad) == 0:
+            break
+        arena = np.flatnonzero(out.rep[:batch.n_clusters].cpu().numpy() == REP_ARENA)
+        extra = tuple(sorted(set(extra) | set(int(c) for c in arena)))
+        batch._ws["medoid_extra"] = extra
+        _medoid_launch(batch, tolerance, True, out, extra, stream)
     return out
 
 
@@ -219,7 +269,7 @@ def xcorr_distance(batch: DeviceBatch, pairs, tolerance=0.1, stream=None):
 
     pairs_t = torch.as_tensor(np.asarray(pairs, np.int64).reshape(-1, 2), device=batch.device).contiguous()
     out = torch.empty(max(len(pairs_t), 1), dtype=torch.float64, device=batch.device)
-    prm = _lib.SpxMedoidParams(float(tolerance))
+    prm = _lib.SpxMedoidParams(float(tolerance), 0)
     _lib.check(_lib.lib().spx_xcorr_distance(ctypes.byref(batch.csr), ctypes.byref(prm), _ptr(pairs_t),
                                              len(pairs_t), _ptr(out), _stream_handle(stream)), "spx_xcorr_distance")
     return out[:len(pairs_t)]

@@ -147,11 +147,24 @@ def make_clusters_torch(n_clusters: int, seed: int = 0, *, device="cuda", min_si
         lens_parts.append(valid.sum(dim=1))
         mz_parts.append(block[valid])
         del t, jit, keep, noise, block, valid
-    mz = torch.cat(mz_parts)
     lens = torch.cat(lens_parts)
-    P = mz.numel()
-    inten = torch.exp(5.0 + 1.5 * torch.randn(P, generator=g, device=device, dtype=f64))
-    inten = torch.clamp(torch.round(inten * 100.0) / 100.0, min=0.01)
+    P = int(sum(p.numel() for p in mz_parts))
+    # fill preallocated arrays chunk by chunk: peak memory ~ one copy of the peaks
+    # plus one chunk (a 1M-cluster batch is 5.2G peaks = 42 GB per array)
+    mz = torch.empty(P, dtype=f64, device=device)
+    o = 0
+    while mz_parts:
+        part = mz_parts.pop(0)
+        mz[o:o + part.numel()] = part
+        o += part.numel()
+        del part
+    inten = torch.empty(P, dtype=f64, device=device)
+    step = 1 << 28
+    for a in range(0, P, step):
+        b = min(P, a + step)
+        x = torch.exp(5.0 + 1.5 * torch.randn(b - a, generator=g, device=device, dtype=f64))
+        inten[a:b] = torch.clamp(torch.round(x * 100.0) / 100.0, min=0.01)
+        del x
     spec_off = torch.zeros(S + 1, dtype=torch.int64, device=device)
     spec_off[1:] = torch.cumsum(lens, 0)
     cluster_off = torch.zeros(C + 1, dtype=torch.int64, device=device)

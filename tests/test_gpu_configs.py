@@ -1,0 +1,120 @@
+"""GPU tests at BASELINE.json's configuration sizes (the configs the headline and
+the north star are quoted on), generated directly in HBM.
+
+* configs[3] -- medoid on the skewed long tail (20k clusters, n = min(5000,
+  max(2, floor(2 U^(-1/1.1)))) plus four forced n = 5000 clusters; MFMA Gram
+  path): every cluster with n > 64 plus 2,000 random small ones against the C
+  oracle, representatives AND totals bit-exact.
+* configs[4] -- the full pipeline on ~10M spectra (385k clusters, U{2..50}):
+  bin-mean + medoid over the whole device batch, size-independent properties
+  for every cluster, and a random 2,000-cluster subset of the same device
+  batch against the oracle (bit-exact).
+* configs[2] -- one 125k-cluster shard of the 1M-cluster gap-average config
+  (what each of 8 GPUs holds): properties for every cluster, a 2,000-cluster
+  subset against the numpy oracle (structure exact, values within GAP_RTOL).
+
+Reference semantics: binning.py:170-231 / :291-297, average_spectrum_clustering.py
+:26-103, most_similar_representative.py:60-111.
+"""
+import numpy as np
+import pytest
+
+from oracle import c_oracle, np_oracle
+from specpride_amd import engine
+from specpride_amd.csr import SpectraCSR
+from specpride_amd.synthetic import make_clusters_torch
+from test_gpu_parity import GAP_RTOL, assert_bin_mean_equal, assert_gap_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _subset_host(t, res_host, clusters):
+    """Slice a capacity-layout device result (to_host of the full batch is dense) to
+    the given clusters, in the oracle's dense layout."""
+    off = res_host["out_off"]
+    parts_m, parts_i, oo = [], [], [0]
+    for c in clusters:
+        parts_m.append(res_host["out_mz"][off[c]:off[c + 1]])
+        parts_i.append(res_host["out_int"][off[c]:off[c + 1]])
+        oo.append(oo[-1] + off[c + 1] - off[c])
+    d = dict(out_off=np.asarray(oo, np.int64), out_mz=np.concatenate(parts_m), out_int=np.concatenate(parts_i))
+    for k in ("status", "prec", "charge"):
+        d[k] = res_host[k][clusters]
+    return d
+
+
+def _check_peaks_properties(batch, h, lo=None, hi=None):
+    """Size-independent facts of a consensus result: statuses, count <= peaks,
+    finite values, m/z inside the binned range."""
+    co, so = batch.host_cluster_off, batch.host_spec_off
+    peaks = so[co[1:]] - so[co[:-1]]
+    counts = np.diff(h["out_off"])
+    assert np.all(counts <= peaks)
+    assert np.all(counts[h["status"] == 0] >= 0)
+    assert np.all(np.isfinite(h["out_mz"])) and np.all(np.isfinite(h["out_int"]))
+    assert np.all(h["out_int"] > 0)
+    if lo is not None:
+        assert h["out_mz"].min() >= lo - 1e-3 and h["out_mz"].max() < hi + 1e-3
+    return counts
+
+
+def test_config3_skewed_medoid_n5000_vs_oracle(gpu):
+    t = make_clusters_torch(20000, seed=4, skewed=True, forced_large=4, large_size=5000)
+    batch = engine.DeviceBatch.from_device(t)
+    sizes = np.diff(batch.host_cluster_off)
+    assert sizes.max() == 5000 and (sizes == 5000).sum() >= 4
+    rep, tot = engine.medoid(batch, with_totals=True).to_host()
+    co = batch.host_cluster_off
+    assert np.all((rep >= co[:-1]) & (rep < co[1:]))
+    rng = np.random.default_rng(0)
+    small = np.flatnonzero(sizes <= 64)
+    pick = np.concatenate([np.flatnonzero(sizes > 64), rng.choice(small, 2000, replace=False)])
+    sub = SpectraCSR.select_from_device(t, pick)
+    want_rep, want_tot = c_oracle.medoid_parallel(sub, with_totals=True)
+    np.testing.assert_array_equal(rep[pick] - co[pick], want_rep - sub.cluster_off[:-1])
+    from specpride_amd.csr import concat_ranges
+
+    sel = concat_ranges(co[pick], sizes[pick])
+    np.testing.assert_array_equal(tot[sel], want_tot)
+
+
+def test_config5_full_pipeline_10m_spectra(gpu):
+    """configs[4]: ~10M spectra resident in HBM, one device pass of each method."""
+    t = make_clusters_torch(385_000, seed=5)
+    batch = engine.DeviceBatch.from_device(t)
+    assert batch.n_spectra > 9_500_000
+    bm = engine.bin_mean(batch).to_host()
+    md_rep, _ = engine.medoid(batch).to_host()
+    co = batch.host_cluster_off
+    assert np.all(bm["status"] == 0)
+    _check_peaks_properties(batch, bm, 100.0, 2000.0)
+    assert np.all((md_rep >= co[:-1]) & (md_rep < co[1:]))
+    rng = np.random.default_rng(1)
+    pick = np.sort(rng.choice(batch.n_clusters, 2000, replace=False))
+    sub = SpectraCSR.select_from_device(t, pick)
+    assert_bin_mean_equal(_subset_host(t, bm, pick), c_oracle.bin_mean(sub))
+    want = c_oracle.medoid_parallel(sub)
+    np.testing.assert_array_equal(md_rep[pick] - co[pick], want - sub.cluster_off[:-1])
+
+
+def test_config2_gap_average_shard_125k(gpu):
+    """configs[2] is 1M clusters over 8 GPUs: one GPU's 125k-cluster shard."""
+    t = make_clusters_torch(125_000, seed=2)
+    batch = engine.DeviceBatch.from_device(t)
+    ga = engine.gap_average(batch).to_host()
+    ok = ga["status"] == 0
+    assert ok.mean() > 0.99
+    counts = _check_peaks_properties(batch, ga)
+    # groups are disjoint sorted m/z runs: means strictly increase within a cluster
+    off = ga["out_off"]
+    d = np.diff(ga["out_mz"])
+    inside = np.ones(len(d), bool)
+    b = off[1:-1] - 1  # d index between cluster c-1's last peak and cluster c's first
+    inside[b[(b >= 0) & (b < len(d))]] = False
+    assert np.all(d[inside] > 0)
+    assert np.all(counts[~ok] == 0)
+    rng = np.random.default_rng(2)
+    pick = np.sort(rng.choice(batch.n_clusters, 2000, replace=False))
+    sub = SpectraCSR.select_from_device(t, pick)
+    got = _subset_host(t, ga, pick)
+    assert_gap_close(got, np_oracle.gap_average(sub), 1000.0, rtol=GAP_RTOL)

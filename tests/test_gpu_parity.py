@@ -126,10 +126,7 @@ def test_gap_average_synthetic_vs_oracle(gpu, synth):
     assert_gap_close(got, np_oracle.gap_average(sub), 1000.0)
 
 
-@pytest.mark.parametrize("variant", ["0", "1"])
-def test_medoid_synthetic_vs_oracle(gpu, synth, monkeypatch, variant):
-    """Default single-read kernel (SPX_MEDOID_KERNEL=0) and the two-read v1 kernel (=1)."""
-    monkeypatch.setenv("SPX_MEDOID_KERNEL", variant)
+def test_medoid_synthetic_vs_oracle(gpu, synth):
     rep, tot = engine.medoid(engine.DeviceBatch.from_host(synth), with_totals=True).to_host()
     ref_rep, ref_tot = c_oracle.medoid(synth, with_totals=True)
     np.testing.assert_array_equal(rep, ref_rep)
@@ -232,22 +229,6 @@ def test_medoid_large_path_skewed_unsorted_and_empty(gpu):
     np.testing.assert_array_equal(tot, ref_tot)
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9"])
-@pytest.mark.parametrize("name", BIN_SETS)
-def test_bin_mean_kernel_variants(gpu, synth, monkeypatch, name, variant):
-    """Every bin-mean kernel variant (SPX_BIN_KERNEL, spx_api.hip) meets the same
-    bit-exact bar as the default kernel."""
-    monkeypatch.setenv("SPX_BIN_KERNEL", variant)
-    z, csr = load_golden(f"bin_mean_{name}.npz")
-    ref = dict(status=z["status"], out_off=z["out_off"], out_mz=z["out_mz"], out_int=z["out_int"],
-               prec=z["out_prec"], charge=z["out_charge"])
-    assert_bin_mean_equal(_bin_mean(csr, **bin_params(z)), ref)
-    if name == "synthetic":
-        assert_bin_mean_equal(_bin_mean(synth), c_oracle.bin_mean(synth))
-        sub = _shuffled(synth.select(range(200)))
-        assert_bin_mean_equal(_bin_mean(sub), c_oracle.bin_mean(sub))
-
-
 def _concat(*parts):
     """Concatenate SpectraCSR batches (cluster order kept)."""
     co, so, n_s, n_p = [np.zeros(1, np.int64)], [np.zeros(1, np.int64)], 0, 0
@@ -261,13 +242,10 @@ def _concat(*parts):
                       cat("charge"), cat("rt"))
 
 
-@pytest.mark.parametrize("variant", ["5", "6"])
-def test_bin_mean_stream_many_clusters_per_workgroup(gpu, monkeypatch, variant):
-    """The persistent streaming kernels (hash fold = 5, bitmap-rank fold = 6): far more clusters than
-    workgroups, so every workgroup folds a long range -- with empty clusters,
-    empty spectra, mixed charges, a spectrum longer than one step (252 peaks),
-    an unsorted spectrum and a > 128-spectrum cluster scattered through it."""
-    monkeypatch.setenv("SPX_BIN_KERNEL", variant)
+def test_bin_mean_many_clusters_with_special_shapes(gpu):
+    """Thousands of clusters with empty clusters, empty spectra, mixed charges, a
+    spectrum longer than one fast-path step (252 peaks), an unsorted spectrum and
+    a > 128-spectrum cluster scattered through them (deferred to the global kernel)."""
     rng = np.random.default_rng(21)
     base = make_clusters_np(7000, seed=8, min_size=1, max_size=12, n_template=60)
     co = base.cluster_off.copy()
@@ -300,9 +278,8 @@ def test_bin_mean_stream_many_clusters_per_workgroup(gpu, monkeypatch, variant):
     assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
 
 
-def _wave_edge_batch():
-    """Shapes that stress bin_mean_wave_kernel's wave ranges: spectra longer than a
-    wave's 64-peak chunk inside one range, clusters of 100-128 spectra, every peak
+def _edge_batch():
+    """Edge shapes: spectra longer than a fast-path step, clusters of 100-128 spectra, every peak
     in one bin (D = 1: three empty ranges), no in-range peak (D = 0), empty spectra
     inside a cluster, repeated bins inside a spectrum (last wins), peaks on the
     range ends (min, just below max, max itself)."""
@@ -335,19 +312,15 @@ def _wave_edge_batch():
     return SpectraCSR.from_clusters(clusters)
 
 
-@pytest.mark.parametrize("variant", ["9", "8", "7", "0"])
-def test_bin_mean_wave_kernel_edges(gpu, monkeypatch, variant):
-    monkeypatch.setenv("SPX_BIN_KERNEL", variant)
-    csr = _wave_edge_batch()
+def test_bin_mean_edge_shapes(gpu):
+    csr = _edge_batch()
     assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
     assert_bin_mean_equal(_bin_mean(csr), np_oracle.bin_mean(csr))
 
 
-@pytest.mark.parametrize("variant", ["9", "8", "7"])
-def test_bin_mean_wave_kernel_skewed_and_unsorted(gpu, monkeypatch, variant):
+def test_bin_mean_skewed_and_unsorted(gpu):
     """Skewed sizes (>128 spectra -> deferred) and shuffled spectra (deferred) mixed
     with regular clusters in one launch: bit-exact against the oracle."""
-    monkeypatch.setenv("SPX_BIN_KERNEL", variant)
     csr = make_clusters_np(400, seed=91, skewed=True)
     csr = csr.select([c for c in range(csr.n_clusters) if csr.cluster_off[c + 1] - csr.cluster_off[c] <= 300])
     assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
@@ -355,12 +328,10 @@ def test_bin_mean_wave_kernel_skewed_and_unsorted(gpu, monkeypatch, variant):
     assert_bin_mean_equal(_bin_mean(sub), c_oracle.bin_mean(sub))
 
 
-def test_bin_mean_ranges_boundaries(gpu, monkeypatch):
-    """bin_mean_ranges_kernel's run boundaries: spectrum 0 unsorted-free but short
-    (bounds from 1-3 peaks), later spectra entirely below / above a boundary, peaks
-    exactly on a boundary bin, runs longer than a wave inside one range, spectra of
-    255 peaks (the cap) and 256 (deferred), all bit-exact against the oracle."""
-    monkeypatch.setenv("SPX_BIN_KERNEL", "9")
+def test_bin_mean_range_boundaries(gpu):
+    """Short spectra (1-3 peaks), spectra entirely below / above parts of the range,
+    repeated identical spectra (every bin hit by every spectrum), spectra of 255
+    and 256 peaks (around the fast-path step), all bit-exact against the oracle."""
     rng = np.random.default_rng(123)
     clusters = []
     for n0 in (1, 2, 3):
@@ -382,3 +353,46 @@ def test_bin_mean_ranges_boundaries(gpu, monkeypatch):
                       "precursor charge": 2} for _ in range(9)])
     csr = SpectraCSR.from_clusters(clusters)
     assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
+
+
+def _zero_tail_batches():
+    """(a) a batch whose LAST cluster has spectra but no peaks (so its peak range
+    starts at n_peaks), (b) a batch with no peaks at all."""
+    rng = np.random.default_rng(31)
+
+    def spec(k):
+        return {"m/z array": np.round(np.sort(rng.uniform(100.0, 1999.0, k)), 5),
+                "intensity array": np.round(rng.lognormal(5, 1.5, k), 2) + 0.01,
+                "precursor mz": 500.0, "precursor charge": 2}
+
+    empty = {"m/z array": [], "intensity array": [], "precursor mz": 500.0, "precursor charge": 2}
+    a = SpectraCSR.from_clusters([[spec(40), spec(35), spec(50)], [spec(60)], [dict(empty), dict(empty)]])
+    b = SpectraCSR.from_clusters([[dict(empty), dict(empty)], [dict(empty)]])
+    return a, b
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_zero_peak_tail_all_entry_points(gpu, which):
+    """Regression for the clamp-to-p0 fault class (a load of index n_peaks): every
+    entry point on a batch whose last cluster -- or whole batch -- has no peaks."""
+    import torch
+
+    csr = _zero_tail_batches()[which]
+    b = engine.DeviceBatch.from_host(csr)
+    assert_bin_mean_equal(engine.bin_mean(b).to_host(), c_oracle.bin_mean(csr))
+    ga = engine.gap_average(b).to_host()
+    want = np_oracle.gap_average(csr)
+    np.testing.assert_array_equal(ga["status"], want["status"])
+    rep, tot = engine.medoid(b, with_totals=True).to_host()
+    ref_rep, ref_tot = c_oracle.medoid(csr, with_totals=True)
+    np.testing.assert_array_equal(rep, ref_rep)
+    np.testing.assert_array_equal(tot, ref_tot)
+    # binned cosine with the bin-mean output as representatives (empty ones included)
+    r = engine.bin_mean(b).to_host()
+    dev = lambda x: torch.as_tensor(np.ascontiguousarray(x), device="cuda")  # noqa: E731
+    rm = r["out_mz"] if len(r["out_mz"]) else np.zeros(1)
+    ri = r["out_int"] if len(r["out_int"]) else np.zeros(1)
+    cos, avg, st = engine.binned_cosine(b, dev(r["out_off"]), dev(rm), dev(ri)).to_host()
+    wcos, wavg, wst = np_oracle.binned_cosine(csr, r["out_off"], r["out_mz"], r["out_int"])
+    np.testing.assert_array_equal(st[:csr.n_clusters], wst)
+    torch.cuda.synchronize()

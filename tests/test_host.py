@@ -37,7 +37,7 @@ def test_hip_library_exports_every_declared_symbol():
     missing = [s for s in _declared() if not hasattr(L, s)]
     assert not missing, missing
     L.spx_abi_version.restype = ctypes.c_int
-    assert L.spx_abi_version() == 1
+    assert L.spx_abi_version() == _lib.SPX_ABI_VERSION == 2
 
 
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):

@@ -43,7 +43,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
     for _ in range(args.reps):
-        engine.medoid(batch, out=md)
+        engine.medoid(batch, out=md, check=False)
     ev[1].record()
     torch.cuda.synchronize()
     ms = ev[0].elapsed_time(ev[1]) / args.reps
