@@ -29,6 +29,8 @@
 // HBM traffic per cluster: mz + inten once from HBM (16 B/peak; phase 3 re-reads
 // the m/z that phase 1 pulled into L2/MALL), 16 B per output peak, offsets.
 #pragma once
+#include <utility>
+
 #include "spx_device.hpp"
 
 namespace spx {
@@ -56,7 +58,10 @@ struct BinMeanState {
 };
 
 #ifndef SPX_BM_MINW
-#define SPX_BM_MINW 5  // __launch_bounds__ minimum waves per SIMD for bin_mean_lds_kernel (LDS allows 5)
+#define SPX_BM_MINW 4  // __launch_bounds__ minimum waves per SIMD for bin_mean_lds_kernel (the leftovers)
+#endif
+#ifndef SPX_BR_MINW
+#define SPX_BR_MINW 5  // the same for bin_mean_reg_kernel (48 register codes)
 #endif
 #ifndef SPX_BM_PF
 #define SPX_BM_PF 10  // spectra in flight per thread in the fast path's register ring
@@ -128,8 +133,56 @@ __device__ __forceinline__ void sorted_lane(const BinMeanState<PrefixT, CountT>&
   accumulate(S, bitmap_rank(S.bitmap, S.wprefix, b), L.m, L.it);
 }
 
+// Phase 4 of the LDS paths: slots with cnt >= quorum and a non-NaN mean, written
+// in slot (= bin) order as mz = f64(M)/cnt, int = f64(I)/cnt (binning.py:209-222).
+// Slots are striped over the block (slot j*256 + tid): conflict-free LDS reads and
+// coalesced stores.  A slot's output position = kept slots before it = kept in
+// earlier stripes + kept in earlier waves of its stripe + earlier lanes of its wave
+// (ballot).  Per-(stripe, wave) counts go to `wcnt` (the dead bitmap): one barrier.
+// Returns the number of peaks written.
+template <class CountT, class AccI, class AccM>
+__device__ __forceinline__ int emit_striped(const CountT* cnt, const AccI& acc_i, const AccM& acc_m, int* wcnt,
+                                            int D, uint32_t quorum, double* __restrict__ omz,
+                                            double* __restrict__ oint) {
+  constexpr int NW = BM_BLOCK / kWave;
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const int per = (D + BM_BLOCK - 1) / BM_BLOCK;  // <= BM_DCAP / BM_BLOCK
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t keep = 0u;  // bit j: slot j*256 + tid is emitted
+  for (int j = 0; j < per; ++j) {
+    const int d = j * BM_BLOCK + tid;
+    const bool k = d < D && (uint32_t)cnt[d] >= quorum && !isnan(acc_i(d));  // cnt >= 1: mean NaN iff sum NaN
+    const unsigned long long b = __ballot(k);
+    if (lane == 0) wcnt[j * NW + wid] = __popcll(b);
+    keep |= (uint32_t)k << j;
+  }
+  lds_barrier();
+  int base = 0;
+  for (int j = 0; j < per; ++j) {
+    int tot = 0, before = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int x = wcnt[j * NW + w];
+      tot += x;
+      before += w < wid ? x : 0;
+    }
+    const bool k = (keep >> j) & 1u;
+    const unsigned long long b = __ballot(k);
+    if (k) {
+      const int d = j * BM_BLOCK + tid;
+      const int o = base + before + __popcll(b & below);
+      const double cn = (double)cnt[d];
+      const float si = acc_i(d), sm = acc_m(d);
+      oint[o] = (double)si / cn;
+      omz[o] = sm == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)sm / cn;
+    }
+    base += tot;
+  }
+  return base;
+}
+
 template <bool kSmall, class PrefixT, class CountT>
-__device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const BinMeanState<PrefixT, CountT>& S,
+__device__ __forceinline__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const BinMeanState<PrefixT, CountT>& S,
                                  int64_t c, const PeaksOut& out, double* prec_out, int32_t* charge_out,
                                  int* tmp, int* flag) {
   const int tid = threadIdx.x;
@@ -354,44 +407,9 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   const int per = (D + BM_BLOCK - 1) / BM_BLOCK;
   int total;
   if constexpr (kSmall) {
-    // Slots striped over the block (slot j*256 + tid): conflict-free LDS reads and
-    // coalesced stores.  A slot's output position = kept slots before it = kept in
-    // earlier stripes + kept in earlier waves of its stripe + earlier lanes of its
-    // wave (ballot).  Per-(stripe, wave) counts go to the dead bitmap: one barrier.
-    constexpr int NW = BM_BLOCK / kWave;
-    int* wcnt = reinterpret_cast<int*>(S.bitmap);  // [per][NW], per <= BM_DCAP / BM_BLOCK
-    const int lane = lane_id(), wid = wave_id();
-    const unsigned long long below = (1ull << lane) - 1ull;
-    uint32_t keep = 0u;  // bit j: slot j*256 + tid is emitted
-    for (int j = 0; j < per; ++j) {
-      const int d = j * BM_BLOCK + tid;
-      const bool k = d < D && S.cnt[d] >= quorum && !isnan(S.acc_i[d]);  // cnt >= 1: mean NaN iff sum NaN
-      const unsigned long long b = __ballot(k);
-      if (lane == 0) wcnt[j * NW + wid] = __popcll(b);
-      keep |= (uint32_t)k << j;
-    }
-    lds_barrier();
-    int base = 0;
-    for (int j = 0; j < per; ++j) {
-      int tot = 0, before = 0;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const int x = wcnt[j * NW + w];
-        tot += x;
-        before += w < wid ? x : 0;
-      }
-      const bool k = (keep >> j) & 1u;
-      const unsigned long long b = __ballot(k);
-      if (k) {
-        const int d = j * BM_BLOCK + tid;
-        const int o = base + before + __popcll(b & below);
-        const double cn = (double)S.cnt[d];
-        out.inten[p0 + o] = (double)S.acc_i[d] / cn;
-        out.mz[p0 + o] = S.acc_m[d] == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)S.acc_m[d] / cn;
-      }
-      base += tot;
-    }
-    total = base;
+    total = emit_striped(S.cnt, [&](int d) { return S.acc_i[d]; }, [&](int d) { return S.acc_m[d]; },
+                         reinterpret_cast<int*>(S.bitmap), D, quorum, out.mz + p0,
+                         out.inten + p0);
   } else {
     const int d0 = tid * per;
     int mine = 0;
@@ -424,18 +442,267 @@ __device__ int32_t bin_mean_body(const CsrView& v, const BinMeanParams& P, const
   return kOk;
 }
 
+// ------------------------------------------------------------------------
+// Register-code fast path (clusters of <= BR_NMAX m/z-sorted spectra of <= 252
+// peaks: every U{2..50} cluster of the configs).  Lane mapping as the body's
+// fast path: wave w's lanes 0..62 own peaks 63w..63w+62 of each spectrum, lane
+// 63 loads peak 63w+63 only to hand lane 62 its neighbour key.  Each peak's
+// bin, its "last in bin" flag and its slot are computed ONCE and kept in
+// registers (one u32 per spectrum per lane), so the spectrum-serial fold is
+// only the read-modify-write itself:
+//   A  spectra in order, no barriers (waves stream independently): m/z, exact
+//      bin, DPP neighbour key -> last-in-bin (numpy fancy-index "+=" keeps the
+//      last, binning.py:197-199), occupancy bitmap (32-bit LDS atomics), and
+//      code[j] = bin of the contribution (-1: none)
+//   B  popcount prefix -> slot per bin in ascending order; codes -> slots, the
+//      per-slot contribution count by LDS atomics (integer: order-free)
+//   C  spectra in order: I = f32(f64(I) + inten), M = f32(f64(M) + mz) of each
+//      contribution's slot -- the reference's float32 accumulation order
+//      (binning.py:198-199); one LDS-only barrier per spectrum
+//   D  quorum + ordered output (emit_striped), precursor mean
+// A key inversion or NaN inside a spectrum sends the cluster to the generic
+// kernel.  Returns kNotHere when the cluster does not fit this path.
+#ifndef SPX_BR_NMAX
+#define SPX_BR_NMAX 48
+#endif
+constexpr int BR_NMAX = SPX_BR_NMAX;  // spectra per cluster: one code VGPR each
+constexpr int BR_PFA = 8;             // phase-A m/z loads in flight per lane
+constexpr int BR_PFC = 4;             // phase-C (m/z, intensity) loads in flight per lane
+constexpr int BR_W32 = 2 * BM_WMAX;   // 32-bit occupancy words
+
+// LDS of the register path.  The occupancy bitmap (32-bit words + per-word rank
+// prefix) is dead once every code is a slot, so the accumulators overlay it.
+struct BinRegSmem {
+  union {
+    struct {
+      uint32_t bits[BR_W32];
+      uint16_t pre[BR_W32];
+    } b;                         // phases A-B
+    float2 acc[BM_DCAP + kWave];  // phases C-D: (intensity, m/z) sums; [BM_DCAP + lane]: dummies
+  } u;
+  uint32_t cnt[BM_DCAP + kWave];  // contributions per slot; [BM_DCAP + lane]: dummies
+  double prec[BR_NMAX];
+  int wcnt[(BM_DCAP / BM_BLOCK) * (BM_BLOCK / kWave)];  // emit: kept slots per (stripe, wave)
+  int votes[2 * (BM_BLOCK / kWave)];
+  int tmp[BM_BLOCK / kWave + 1];
+};
+constexpr int32_t kNotHere = -1;
+
+// f(integral_constant<int, J>) for J = 0, 1, ... while J < n (n <= sizeof...(Js)):
+// a compile-time-unrolled loop with a uniform early exit.  Register arrays are
+// indexed by the constant J, and after the exit nothing is merged back (a
+// prefetch ring read inside f never becomes a phi of a fresh load and an old
+// value, which would compile to a wait for the load right after issuing it).
+template <class F, int... Js>
+__device__ __forceinline__ void unrolled_while(int n, F&& f, std::integer_sequence<int, Js...>) {
+  // each step re-reads n through an empty asm: the compiler cannot evaluate the
+  // 64 uniform guards up front (64 live SGPR pairs, which spill)
+  int nn = __builtin_amdgcn_readfirstlane(n);
+  auto more = [&](int j) __attribute__((always_inline)) {
+    asm volatile("" : "+s"(nn));
+    return j < nn;
+  };
+  (void)((more(Js) ? (f(std::integral_constant<int, Js>{}), true) : false) && ...);
+}
+
+__device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const BinMeanParams& P, BinRegSmem& L,
+                                                     int64_t c, const PeaksOut& out, double* prec_out,
+                                                     int32_t* charge_out) {
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1], n64 = s1 - s0;
+  if (n64 < 1 || n64 > BR_NMAX || P.n_words > BM_WMAX) return kNotHere;
+  const int n = (int)n64;
+  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
+  if (p1 == p0 || p1 - p0 >= (int64_t(1) << 28)) return kNotHere;
+  // lane j of every wave: spectrum j's [lo, hi) relative to p0, charge, precursor
+  const int jl = lane < n ? lane : n - 1;
+  const int32_t rlo = (int32_t)(v.spec_off[s0 + jl] - p0), rhi = (int32_t)(v.spec_off[s0 + jl + 1] - p0);
+  const int32_t z0 = v.charge[s0];
+  const bool mine = lane < n;
+  const int32_t zl = v.charge[s0 + jl];
+  const double pl = v.prec_mz[s0 + jl];
+  if (__ballot(mine & ((rhi - rlo) > BM_FASTLEN)) != 0ull) return kNotHere;  // uniform (same in every wave)
+  if (__ballot(mine & (zl != z0)) != 0ull) {  // binning.py:205-206: nothing emitted
+    if (tid == 0) { out.count[c] = 0; prec_out[c] = __longlong_as_double(0x7ff8000000000000ll); charge_out[c] = 0; }
+    return kMixedCharge;
+  }
+  if (wid == 0 && mine) L.prec[lane] = pl;
+  const int nw32 = 2 * P.n_words;
+  for (int w = tid; w < nw32; w += BM_BLOCK) L.u.b.bits[w] = 0u;
+  lds_barrier();
+  SPX_STAMP(1);
+
+  const int fpos = wid * (kWave - 1) + lane;  // this lane's peak in every spectrum
+  const bool owner = lane < kWave - 1;
+  const char* __restrict__ mzb = reinterpret_cast<const char*>(v.mz + p0);
+  const char* __restrict__ itb = reinterpret_cast<const char*>(v.inten + p0);
+  // cluster-relative byte offset of this lane's peak of spectrum j (0 past its
+  // end: the cluster's first peak, in bounds since the cluster has peaks)
+  // Spectra past the cluster's last (j >= n, a ring's tail prefetch) map every
+  // lane to byte 0: one cache line per wave, so the ring's loads are unconditional
+  // (a conditional load makes its ring register a merge of two values, which
+  // compiles to a wait for the load right after issuing it).
+  auto boff = [&](int j) -> uint32_t {
+    const int jj = j < n ? j : n - 1;
+    const int a = __builtin_amdgcn_readlane(rlo, jj), e = __builtin_amdgcn_readlane(rhi, jj);
+    const int k = a + fpos;
+    return (j < n && k < e) ? (uint32_t)k * 8u : 0u;
+  };
+  auto ld = [&](const char* base, uint32_t bo) -> double { return *reinterpret_cast<const double*>(base + bo); };
+
+  // ---- A: bins, last-in-bin, occupancy, codes (branch-free per lane)
+  int32_t code[BR_NMAX];
+  uint32_t* bm32 = L.u.b.bits;
+  int bad = 0;
+  {
+    // ring slot: this lane's m/z of spectrum j and the spectrum's length (read
+    // once, when the load is issued)
+    double ra[BR_PFA];
+    int rl[BR_PFA];
+    auto fetch = [&](int j, double& m, int& len) __attribute__((always_inline)) {
+      const int jj = j < n ? j : n - 1;
+      const int a = __builtin_amdgcn_readlane(rlo, jj), e = __builtin_amdgcn_readlane(rhi, jj);
+      const int k = a + fpos;
+      len = j < n ? e - a : 0;
+      m = ld(mzb, (j < n && k < e) ? (uint32_t)k * 8u : 0u);
+    };
+#pragma unroll
+    for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
+#pragma unroll
+    for (int j = 0; j < BR_NMAX; ++j) code[j] = -1;
+    unrolled_while(n, [&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      const double m = ra[j % BR_PFA];
+      const int len = rl[j % BR_PFA];
+      fetch(j + BR_PFA, ra[j % BR_PFA], rl[j % BR_PFA]);
+      const bool act = fpos < len;
+      const bool inr = act & (m >= P.minimum) & (m < P.maximum);
+      const int32_t kb = bin_small(inr ? m : P.minimum, P);
+      // inactive lanes (past the spectrum's end) carry INT_MAX: the last active
+      // peak's neighbour then always differs from it, and never sorts below it
+      const int32_t key = inr ? kb : ((act & (m < P.minimum)) ? -1 : 0x7fffffff);
+      const int32_t kn = wave_next(key, 0x7fffffff);
+      bad |= (int)(owner & act & ((m != m) | (key > kn)));
+      const bool valid = owner & inr & (kn != key);  // the last peak of its bin (binning.py:197-199)
+      // a lane without a contribution ORs 0 into a word of its own (same-address
+      // LDS atomics serialise; distinct words do not)
+      atomicOr(&bm32[valid ? key >> 5 : lane], valid ? 1u << (key & 31) : 0u);
+      code[j] = valid ? key : -1;
+    }, std::make_integer_sequence<int, BR_NMAX>{});
+  }
+  // phase C's first (m/z, intensity) loads go out now and land during phase B
+  // (whose barriers are LDS-only, so they stay in flight)
+  double rm[BR_PFC], ri[BR_PFC];
+#pragma unroll
+  for (int j = 0; j < BR_PFC; ++j) {
+    const uint32_t bo = boff(j);
+    rm[j] = ld(mzb, bo);
+    ri[j] = ld(itb, bo);
+  }
+  if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
+  SPX_STAMP(2);
+
+  // ---- B: slots in bin order, codes -> slots, contribution counts
+  const int D = bitmap_prefix32<BM_BLOCK>(L.u.b.bits, L.u.b.pre, nw32, L.tmp);
+  if (D > BM_DCAP) return kDeferred;
+  for (int d = tid; d < D; d += BM_BLOCK) L.cnt[d] = 0u;
+  if (tid < kWave) L.cnt[BM_DCAP + tid] = 0u;
+  lds_barrier();
+  unrolled_while(n, [&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    const bool valid = code[j] >= 0;
+    const uint32_t b = (uint32_t)(valid ? code[j] : 0);
+    const uint32_t w = b >> 5;
+    const int slot = (int)L.u.b.pre[w] + __popc(L.u.b.bits[w] & ((1u << (b & 31)) - 1u));
+    code[j] = valid ? slot : BM_DCAP + lane;  // a dummy slot of its own, never read
+    atomicAdd(&L.cnt[code[j]], valid ? 1u : 0u);
+  }, std::make_integer_sequence<int, BR_NMAX>{});
+  lds_barrier();  // the bitmap is dead: the accumulators take its place
+  for (int d = tid; d < D; d += BM_BLOCK) L.u.acc[d] = make_float2(0.0f, 0.0f);
+  lds_barrier();
+  SPX_STAMP(3);
+
+  // ---- C: the ordered fold (spectrum order per slot = the reference's order)
+  unrolled_while(n, [&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    const double m = rm[j % BR_PFC], it = ri[j % BR_PFC];
+    const uint32_t bo = boff(j + BR_PFC);
+    rm[j % BR_PFC] = ld(mzb, bo);
+    ri[j % BR_PFC] = ld(itb, bo);
+    const int slot = code[j];
+    float2 a = L.u.acc[slot];
+    a.x = (float)((double)a.x + it);
+    a.y = (float)((double)a.y + m);
+    L.u.acc[slot] = a;
+    lds_barrier();
+  }, std::make_integer_sequence<int, BR_NMAX>{});
+  SPX_STAMP(4);
+
+  // ---- D: quorum filter and ordered output (binning.py:181-183, 209-222)
+  const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
+  const int total = emit_striped(L.cnt, [&](int d) { return L.u.acc[d].x; }, [&](int d) { return L.u.acc[d].y; },
+                                 L.wcnt, D, quorum, out.mz + p0, out.inten + p0);
+  if (tid == 0) {
+    out.count[c] = total;
+    charge_out[c] = z0;
+    prec_out[c] = pw_sum_small([&](int64_t j) { return L.prec[j]; }, n) / (double)n;  // np.mean (binning.py:224)
+  }
+  return kOk;
+}
+
+// Register-code kernel: one workgroup per cluster.  Clusters this path does not
+// take (kNotHere) go to `rest` for bin_mean_lds_kernel; kDeferred ones (unsorted,
+// NaN, too many distinct bins) straight to the global kernel's list.
+__global__ __launch_bounds__(BM_BLOCK, SPX_BR_MINW) void bin_mean_reg_kernel(CsrView v, BinMeanParams P, PeaksOut out,
+                                                                             double* prec_out, int32_t* charge_out,
+                                                                             int32_t* status, int32_t* rest,
+                                                                             int32_t* n_rest, int32_t* deferred,
+                                                                             int32_t* n_deferred) {
+  __shared__ BinRegSmem L;
+  const int64_t c = blockIdx.x;
+  SPX_STAMP(0);
+  const int32_t st = bin_mean_reg_path(v, P, L, c, out, prec_out, charge_out);
+  SPX_STAMP(5);
+  if (threadIdx.x == 0) {
+    if (st == kNotHere) {
+      rest[atomicAdd(n_rest, 1)] = (int32_t)c;
+    } else {
+      status[c] = st;
+      if (st == kDeferred) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    }
+  }
+}
+
+// The LDS body (bin_mean_body<true>: its own fast path for <= 128 spectra) over
+// the clusters the register kernel left, grid-stride over the list.
 __global__ __launch_bounds__(BM_BLOCK, SPX_BM_MINW) void bin_mean_lds_kernel(CsrView v, BinMeanParams P, PeaksOut out,
                                                                 double* prec_out, int32_t* charge_out,
-                                                                int32_t* status, int32_t* deferred,
+                                                                int32_t* status, const int32_t* list,
+                                                                const int32_t* n_list, int32_t* deferred,
                                                                 int32_t* n_deferred) {
   __shared__ BinMeanSmem L;
-  const int64_t c = blockIdx.x;
-  BinMeanState<uint16_t, uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.acc_i, L.acc_m, nullptr, L.soff, L.prec, L.votes, nullptr,
-                           BM_DCAP, BM_NMAX};
-  const int32_t st = bin_mean_body<true>(v, P, S, c, out, prec_out, charge_out, L.tmp, &L.flag);
-  if (threadIdx.x == 0) {
-    status[c] = st;
-    if (st == kDeferred) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+  BinMeanState<uint16_t, uint16_t> S;
+  S.bitmap = L.bitmap;
+  S.wprefix = L.wprefix;
+  S.cnt = L.cnt;
+  S.acc_i = L.acc_i;
+  S.acc_m = L.acc_m;
+  S.owner = nullptr;
+  S.soff = L.soff;
+  S.prec = L.prec;
+  S.votes = L.votes;
+  S.xch = nullptr;
+  S.dcap = BM_DCAP;
+  S.nmax = BM_NMAX;
+  const int32_t nl = *n_list;
+  for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    const int64_t c = list[i];
+    const int32_t st = bin_mean_body<true>(v, P, S, c, out, prec_out, charge_out, L.tmp, &L.flag);
+    if (threadIdx.x == 0) {
+      status[c] = st;
+      if (st == kDeferred) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+    }
+    __syncthreads();
   }
 }
 

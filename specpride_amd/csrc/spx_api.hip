@@ -81,6 +81,13 @@ int gap_wcap(const spx_gap_params* p, const spx_batch_info* info) {
 extern "C" {
 
 int spx_abi_version(void) { return SPX_ABI_VERSION; }
+
+#ifdef SPX_STAMPS
+// diagnostic builds only: where the phase stamps go (nullptr: off)
+int spx_debug_stamps(void* dev_ptr) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(spx::g_spx_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : SPX_EHIP;
+}
+#endif
 const char* spx_last_error(void) { return g_err; }
 
 // ------------------------------------------------------------------ bin-mean
@@ -88,7 +95,7 @@ size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* par
   if (!csr || !params || !info) return 0;
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
-  return align256(sizeof(int32_t)) + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
+  return 2 * align256(sizeof(int32_t) * 2) + 2 * align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
          (size_t)fallback_grid(C) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
@@ -106,8 +113,11 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   if (C == 0) return SPX_SUCCESS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
-  int32_t* n_def = w.take<int32_t>(1);
+  int32_t* counters = w.take<int32_t>(2);  // [0] deferred to the global kernel, [1] left to the LDS kernel
+  int32_t* n_def = counters;
+  int32_t* n_rest = counters + 1;
   int32_t* def = w.take<int32_t>((size_t)C);
+  int32_t* rest = w.take<int32_t>((size_t)C);
   char* scratch = w.base + w.used;
 
   spx::BinMeanParams P;
@@ -121,9 +131,12 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const spx::CsrView V = view(csr);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
-  if (hipMemsetAsync(n_def, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
-  hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                     charge_out, status, def, n_def);
+  if (hipMemsetAsync(counters, 0, 2 * sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
+  hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                     charge_out, status, rest, n_rest, def, n_def);
+  if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),
+                     dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
   if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)fallback_grid(C)), dim3(spx::BM_BLOCK), 0, s, V, P,
                      O, prec_out, charge_out, status, def, n_def, scratch,

@@ -25,6 +25,22 @@ namespace spx {
 
 constexpr int kWave = 64;
 
+// Diagnostic builds only (-DSPX_STAMPS, tools/stamps.py): thread 0 of each
+// workgroup records the shader clock at phase boundaries, stamps[block * 8 + k].
+// Product builds compile SPX_STAMP to nothing.
+#ifdef SPX_STAMPS
+__device__ unsigned long long* g_spx_stamps;
+#define SPX_STAMP(k)                                                                           \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && g_spx_stamps)                                                      \
+      g_spx_stamps[(size_t)blockIdx.x * 8 + (k)] = (unsigned long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define SPX_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 // ----------------------------------------------------------------- CSR views
 struct CsrView {
   int64_t n_clusters, n_spectra, n_peaks;
@@ -116,27 +132,6 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
   return __longlong_as_double(readlane64(__double_as_longlong(x), l));
 }
 
-// Block exclusive scan of one int per thread.  `tmp` holds BLOCK/64 + 1 ints
-// in LDS.  Returns the exclusive prefix; `total` receives the block sum.
-template <int BLOCK, class T>
-__device__ __forceinline__ T block_exclusive_scan(T v, T* tmp, T& total) {
-  static_assert(BLOCK % kWave == 0, "block must be whole waves");
-  constexpr int NW = BLOCK / kWave;
-  T inc = wave_inclusive_sum(v);
-  if (lane_id() == kWave - 1) tmp[wave_id()] = inc;
-  __syncthreads();
-  T base = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) {
-    T t = tmp[w];
-    base += (w < wave_id()) ? t : T(0);
-    tot += t;
-  }
-  __syncthreads();
-  total = tot;
-  return base + inc - v;
-}
-
 // Workgroup barrier that orders LDS only.  __syncthreads() is a release/acquire
 // fence on ALL address spaces: its release waits for every outstanding global
 // load (vmcnt), which drains any prefetch in flight.  Steps that exchange data
@@ -149,6 +144,30 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: vmcnt/expcnt left alone
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Block exclusive scan of one int per thread.  `tmp` holds BLOCK/64 + 1 ints
+// in LDS.  Returns the exclusive prefix; `total` receives the block sum.
+// kLdsOnly: LDS-only barriers (register prefetches in flight survive them).
+template <int BLOCK, class T, bool kLdsOnly = false>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* tmp, T& total) {
+  static_assert(BLOCK % kWave == 0, "block must be whole waves");
+  constexpr int NW = BLOCK / kWave;
+  T inc = wave_inclusive_sum(v);
+  if (lane_id() == kWave - 1) tmp[wave_id()] = inc;
+  if constexpr (kLdsOnly) lds_barrier();
+  else __syncthreads();
+  T base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    T t = tmp[w];
+    base += (w < wave_id()) ? t : T(0);
+    tot += t;
+  }
+  if constexpr (kLdsOnly) lds_barrier();
+  else __syncthreads();
+  total = tot;
+  return base + inc - v;
 }
 
 // Block-wide OR with ONE barrier: wave ballot, one LDS word per wave, barrier,
@@ -315,9 +334,32 @@ __device__ __forceinline__ int bitmap_rank(const unsigned long long* bm, const P
   return (int)pref[w] + __popcll(bm[w] & mask);
 }
 
+// The same over 32-bit words, LDS-only barriers.
+template <int BLOCK, class PrefixT>
+__device__ int bitmap_prefix32(const uint32_t* bm, PrefixT* pref, int nw, int* tmp) {
+  const int per = (nw + BLOCK - 1) / BLOCK;
+  const int w0 = threadIdx.x * per;
+  int local = 0;
+  for (int k = 0; k < per; ++k) {
+    const int w = w0 + k;
+    if (w < nw) local += __popc(bm[w]);
+  }
+  int total;
+  int base = block_exclusive_scan<BLOCK, int, true>(local, tmp, total);
+  for (int k = 0; k < per; ++k) {
+    const int w = w0 + k;
+    if (w < nw) {
+      pref[w] = (PrefixT)base;
+      base += __popc(bm[w]);
+    }
+  }
+  lds_barrier();
+  return total;
+}
+
 // Exclusive popcount prefix over `nw` bitmap words, in place into `pref`;
 // returns the total number of set bits.  Whole block participates.
-template <int BLOCK, class PrefixT>
+template <int BLOCK, class PrefixT, bool kLdsOnly = false>
 __device__ int bitmap_prefix(const unsigned long long* bm, PrefixT* pref, int nw, int* tmp) {
   const int per = (nw + BLOCK - 1) / BLOCK;
   const int w0 = threadIdx.x * per;
@@ -327,7 +369,7 @@ __device__ int bitmap_prefix(const unsigned long long* bm, PrefixT* pref, int nw
     if (w < nw) local += __popcll(bm[w]);
   }
   int total;
-  int base = block_exclusive_scan<BLOCK>(local, tmp, total);
+  int base = block_exclusive_scan<BLOCK, int, kLdsOnly>(local, tmp, total);
   for (int k = 0; k < per; ++k) {
     int w = w0 + k;
     if (w < nw) {
@@ -335,7 +377,8 @@ __device__ int bitmap_prefix(const unsigned long long* bm, PrefixT* pref, int nw
       base += __popcll(bm[w]);
     }
   }
-  __syncthreads();
+  if constexpr (kLdsOnly) lds_barrier();
+  else __syncthreads();
   return total;
 }
 

@@ -1,12 +1,14 @@
 #!/bin/bash
-# GPU quick loop: parity tests then bench (no CPU baseline).
+# Iteration loop: GPU parity tests (TESTS, default all) -> bench headline only.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/gpu_tests.log 2>&1
-echo "pytest rc=$?" >> gpurun_out/gpu_tests.log
+export TMPDIR=/tmp
+TESTS=${TESTS:-tests}
+timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?
 tail -3 gpurun_out/gpu_tests.log
-grep -q "pytest rc=0" gpurun_out/gpu_tests.log || exit 1
-timeout -k 10 600 python bench.py --no-cpu-baseline "$@" > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
-tail -1 gpurun_out/bench.log
+[ $rc -eq 0 ] || { grep -E "^(FAILED|E  )" gpurun_out/gpu_tests.log | head -30; exit 1; }
+timeout -k 10 600 python bench.py --no-extras --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('value', d['value'], 'ms/step', d['ms_per_step'], d['kernels'], 'bm frac', d['roofline']['frac'], 'md frac', d['roofline_medoid']['frac'])"

@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Kernel timing / diagnostics driver (profiling aid, not the product bench).
+
+    python tools/profile_kernels.py [--clusters 100000] [--reps 5] [--which bm,md,ga] [--stamps]
+
+Times each entry point on a synthetic configs[4]-law batch with HIP events and
+prints one JSON line.  Under ``rocprofv3 --pmc`` it is the program the counter
+passes run (tools/gpu/pmc.sh).  With --stamps it loads the diagnostic build
+(specpride_amd/lib/libspecpride_hip_stamps.so, -DSPX_STAMPS: build it with
+``python tools/profile_kernels.py --build-stamps`` on the CPU) and reports the
+mean shader-clock cycles per bin-mean phase (SPX_STAMP(k) in the kernels),
+overall and per cluster-size band.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+STAMPS_LIB = os.path.join(REPO, "specpride_amd", "lib", "libspecpride_hip_stamps.so")
+
+
+def build_stamps():
+    from specpride_amd import _lib
+
+    cmd = [_lib.HIPCC, *_lib.HIP_FLAGS, "-DSPX_STAMPS", "-o", STAMPS_LIB, os.path.join(_lib.CSRC, "spx_api.hip")]
+    subprocess.run(cmd, check=True)
+    print(STAMPS_LIB)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clusters", type=int, default=100_000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--which", default="bm,md,ga")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--build-stamps", action="store_true")
+    a = ap.parse_args()
+    if a.build_stamps:
+        build_stamps()
+        return
+    if a.stamps:
+        os.environ["SPX_LIB"] = STAMPS_LIB
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    from specpride_amd import _lib, engine
+    from specpride_amd.synthetic import make_clusters_torch
+
+    t = make_clusters_torch(a.clusters, seed=a.seed)
+    b = engine.DeviceBatch.from_device(t)
+    which = a.which.split(",")
+    res = {"clusters": b.n_clusters, "spectra": b.n_spectra, "peaks": b.n_peaks}
+    st = torch.cuda.current_stream()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(a.reps):
+            fn()
+        e1.record(st)
+        torch.cuda.synchronize()
+        return round(e0.elapsed_time(e1) / a.reps, 4)
+
+    if "bm" in which:
+        bm = engine.bin_mean(b)
+        res["bin_mean_ms"] = timed(lambda: engine.bin_mean(b, out=bm))
+    if "md" in which:
+        md = engine.medoid(b)
+        res["medoid_ms"] = timed(lambda: engine.medoid(b, out=md, check=False))
+    if "ga" in which:
+        ga = engine.gap_average(b)
+        res["gap_average_ms"] = timed(lambda: engine.gap_average(b, out=ga))
+    if a.stamps:
+        L = _lib.lib()
+        L.spx_debug_stamps.argtypes = [ctypes.c_void_p]
+        buf = torch.zeros(b.n_clusters * 8, dtype=torch.int64, device="cuda")
+        assert L.spx_debug_stamps(buf.data_ptr()) == 0
+        engine.bin_mean(b, out=bm)
+        torch.cuda.synchronize()
+        L.spx_debug_stamps(None)
+        s = buf.view(-1, 8).cpu().numpy().astype(np.float64)
+        sizes = np.diff(b.host_cluster_off)
+        ph = {}
+        for k in range(1, 6):
+            ok = (s[:, k] > 0) & (s[:, k - 1] > 0)
+            if ok.any():
+                ph[f"p{k - 1}->p{k}"] = round(float(np.mean(s[ok, k] - s[ok, k - 1])), 1)
+        ok = (s[:, 5] > 0) & (s[:, 0] > 0)
+        ph["lifetime"] = round(float(np.mean(s[ok, 5] - s[ok, 0])), 1)
+        bands = {}
+        for lo, hi in ((2, 10), (11, 25), (26, 40), (41, 50)):
+            m = ok & (sizes >= lo) & (sizes <= hi) & (s[:, 4] > 0)
+            if m.any():
+                bands[f"n{lo}-{hi}"] = {f"p{k - 1}->p{k}": round(float(np.mean(s[m, k] - s[m, k - 1])), 1)
+                                        for k in range(1, 6)}
+        span = (s[ok, 5].max() - s[ok, 0].min())
+        res["stamps"] = {"phases_cycles": ph, "by_size": bands, "span_cycles": span,
+                         "cycles_per_cluster_per_cu": round(span * 256 / ok.sum(), 1)}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
