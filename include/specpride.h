@@ -172,11 +172,14 @@ typedef struct spx_cosine_params {
  * members are the cluster's spectra in csr.  cos_out [n_spectra] = cos_dist per
  * member, avg_out [n_clusters] = average_cos_dist (0.0 for no members).
  * status[c]: SPX_EMPTY if the representative or a member has no peaks (the
- * reference's mz[-1] raises IndexError; NaN outputs), SPX_UNRESOLVED if the
- * representative has more than 1,024 peaks. */
+ * reference's mz[-1] raises IndexError; NaN outputs).  Representatives of up to
+ * 1,024 peaks are sorted in LDS; longer ones (max_rep_peaks = an upper bound on
+ * every representative's length) in a global workspace slice, so any length is
+ * evaluated; SPX_UNRESOLVED only if a representative exceeds max_rep_peaks. */
+size_t spx_binned_cosine_workspace_size(int64_t n_clusters, int64_t max_rep_peaks);
 int spx_binned_cosine(const spx_csr *csr, const int64_t *rep_off, const double *rep_mz, const double *rep_inten,
                       const spx_cosine_params *params, double *cos_out, double *avg_out, int32_t *status,
-                      void *stream);
+                      int64_t max_rep_peaks, void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---- best spectrum: best_spectrum.get_best_representative(cluster, scores) for every
  *      cluster: scores.idxmax() over the cluster's members (best_spectrum.py:97-100) ---- */

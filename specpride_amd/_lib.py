@@ -65,7 +65,7 @@ class SpxCosineParams(ctypes.Structure):
 
 # every symbol include/specpride.h declares (checked by tests/test_host.py)
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_gap_average_workspace_size", "spx_gap_average",
-            "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine", "spx_best_score",
+            "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
             "spx_compact_peaks",
             "spx_abi_version", "spx_last_error"]
 
@@ -136,7 +136,9 @@ def lib():
     L.spx_medoid.argtypes = [_p, _p, _p, _p, _p, _sz, _p]
     L.spx_compact_peaks.argtypes = [_p, _p, _p, _p, _p, _p]
     L.spx_xcorr_distance.argtypes = [_p, _p, _p, _i64, _p, _p]
-    L.spx_binned_cosine.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _p]
+    L.spx_binned_cosine_workspace_size.restype = _sz
+    L.spx_binned_cosine_workspace_size.argtypes = [_i64, _i64]
+    L.spx_binned_cosine.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _p, _sz, _p]
     L.spx_best_score.argtypes = [_p, _p, _p, _p, _p, _p]
     if L.spx_abi_version() != SPX_ABI_VERSION:
         raise RuntimeError(f"libspecpride_hip ABI {L.spx_abi_version()} != {SPX_ABI_VERSION}")

@@ -48,7 +48,7 @@ def average_cos_dist_batch(representatives, clusters, mz_space=mz_space, device=
         if st == engine.STATUS_EMPTY:
             raise IndexError("index -1 is out of bounds for axis 0 with size 0")  # benchmark.py:20 mz[-1]
         if st != engine.STATUS_OK:
-            raise RuntimeError(f"cluster {c}: representative beyond the engine's 1,024-peak limit")
+            raise RuntimeError(f"cluster {c}: binned cosine unresolved (status {st})")
     return avg[:csr.n_clusters], [cos[csr.cluster_off[c]:csr.cluster_off[c + 1]] for c in range(csr.n_clusters)]
 
 

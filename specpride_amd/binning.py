@@ -83,7 +83,8 @@ class RepresentativeSpectrumCreator:
         if self.verbose >= 1:
             eprint(f"INFO: Reading {len(scan_list)} scans from mzML file {mzml_file}")
         spectra = []
-        rd = reader if reader is not None else mzml.read(mzml_file)
+        ids = [f"controllerType=0 controllerNumber=1 scan={scan}" for scan in scan_list]
+        rd = reader if reader is not None else mzml.read(mzml_file, ids=ids)
         for scan in scan_list:
             spectrum = rd.get_by_id(f"controllerType=0 controllerNumber=1 scan={scan}")
             if spectrum["ms level"] == 2 and "m/z array" in spectrum:
@@ -107,7 +108,8 @@ class RepresentativeSpectrumCreator:
         """read_spectra for several scan lists with ONE parse of the mzML file."""
         from . import mzml
 
-        rd = mzml.read(mzml_file)
+        ids = [f"controllerType=0 controllerNumber=1 scan={scan}" for scans in clusters for scan in scans]
+        rd = mzml.read(mzml_file, ids=ids)  # only the listed scans are kept (and decoded lazily)
         return [self.read_spectra(mzml_file, scans, reader=rd) for scans in clusters]
 
     # ------------------------------------------------------------- MGF input

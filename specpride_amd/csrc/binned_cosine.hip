@@ -39,21 +39,34 @@ constexpr int CS_NW = CS_BLOCK / kWave;
 constexpr int CS_BSH = 8;      // run-index buckets of 256 bins (~1.28 Da)
 constexpr int CS_BMAX = 2048;  // buckets held in LDS: bins < 524,288 (m/z < ~2,620)
 
-struct CosSmem {
-  int32_t sk[CS_RCAP];       // representative peak bins, input order (rank sort input)
-  int32_t pk[CS_RCAP];       // ... sorted by (bin, index)
-  double pI[CS_RCAP];        //     their intensities
-  int16_t pidx[CS_RCAP];     //     their input index
-  int32_t rb[CS_RCAP];       // runs of equal bins: bin,
-  int16_t rs[CS_RCAP + 1];   //   first sorted position,
-  double rA[CS_RCAP];        //   A_b (summed in input order),
-  double rA2[CS_RCAP + 1];   //   exclusive prefix of A_b^2
-  uint16_t bst[CS_BMAX];     // first run with a bin >= t << CS_BSH, per bucket t
-  int32_t wk[CS_NW][kWave];  // per-wave member scratch: bins,
-  double wI[CS_NW][kWave];   //   intensities
+// Representative state: LDS arrays (cap = CS_RCAP) in the main kernel, a
+// per-workgroup global scratch slice (cap = the largest deferred
+// representative) in binned_cosine_global_kernel.
+struct CosState {
+  int32_t* sk;    // representative peak bins, input order (rank sort input)
+  int32_t* pk;    // ... sorted by (bin, index)
+  double* pI;     //     their intensities
+  int32_t* pidx;  //     their input index
+  int32_t* rb;    // runs of equal bins: bin,
+  int32_t* rs;    //   first sorted position [cap + 1],
+  double* rA;     //   A_b (summed in input order),
+  double* rA2;    //   exclusive prefix of A_b^2 [cap + 1]
+  int cap;
+};
+
+struct CosShared {               // LDS of both kernels
+  int32_t bst[CS_BMAX];          // first run with a bin >= t << CS_BSH, per bucket t
+  int32_t wk[CS_NW][kWave];      // per-wave member scratch: bins,
+  double wI[CS_NW][kWave];       //   intensities
   double tmpd[CS_NW + 1];
   int tmp[CS_NW + 1];
   int nruns;
+};
+
+struct CosSmem {
+  int32_t sk[CS_RCAP], pk[CS_RCAP], pidx[CS_RCAP], rb[CS_RCAP], rs[CS_RCAP + 1];
+  double pI[CS_RCAP], rA[CS_RCAP], rA2[CS_RCAP + 1];
+  CosShared sh;
 };
 
 __device__ __forceinline__ double cs_edge(const CosParams& P, int64_t i) {
@@ -91,12 +104,12 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
-__global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosParams P, const int64_t* rep_off,
-                                                                 const double* rep_mz, const double* rep_int,
-                                                                 double* cos_out, double* avg_out, int32_t* status) {
-  __shared__ CosSmem L;
+// One cluster: the representative's runs, then one wave per member.  Returns
+// false (nothing written) if the representative exceeds S.cap.
+__device__ bool cos_body(const CsrView& v, const CosParams& P, const CosState& S, CosShared& L, int64_t c,
+                         const int64_t* rep_off, const double* rep_mz, const double* rep_int, double* cos_out,
+                         double* avg_out, int32_t* status) {
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
-  const int64_t c = blockIdx.x;
   const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
   const int n = (int)(s1 - s0);
   const int64_t r0 = rep_off[c];
@@ -104,95 +117,93 @@ __global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosP
   const double nan = __longlong_as_double(0x7ff8000000000000ll);
   if (n == 0) {  // average_cos_dist of no members (benchmark.py:36-38)
     if (tid == 0) { avg_out[c] = 0.0; status[c] = kOk; }
-    return;
+    return true;
   }
   // an empty spectrum: the reference's mz[-1] raises IndexError (benchmark.py:20)
   int empty = R == 0;
   for (int j = tid; j < n; j += CS_BLOCK) empty |= v.spec_off[s0 + j + 1] == v.spec_off[s0 + j];
   const bool any_empty = __syncthreads_or(empty);
-  if (any_empty || R > CS_RCAP) {
+  if (any_empty) {
     for (int j = tid; j < n; j += CS_BLOCK) cos_out[s0 + j] = nan;
-    if (tid == 0) { avg_out[c] = nan; status[c] = any_empty ? kEmpty : kDeferred; }
-    return;
+    if (tid == 0) { avg_out[c] = nan; status[c] = kEmpty; }
+    return true;
   }
+  if (R > S.cap) return false;
 
   // representative: bins, stable rank sort by (bin, index), runs, prefix of A^2
   for (int i = tid; i < R; i += CS_BLOCK) {
     const int64_t k = cs_bin(P, rep_mz[r0 + i]);
-    L.sk[i] = k > 0x7ffffffe ? 0x7ffffffe : (int32_t)k;
+    S.sk[i] = k > 0x7ffffffe ? 0x7ffffffe : (int32_t)k;
   }
   __syncthreads();
   // an m/z-sorted representative (the consensus outputs are) is already in
   // (bin, index) order: the stable rank sort is the identity
   int inv = 0;
-  for (int i = tid + 1; i < R; i += CS_BLOCK) inv |= L.sk[i] < L.sk[i - 1];
+  for (int i = tid + 1; i < R; i += CS_BLOCK) inv |= S.sk[i] < S.sk[i - 1];
   const bool sorted = !__syncthreads_or(inv);
   for (int i = tid; i < R; i += CS_BLOCK) {
-    const int32_t k = L.sk[i];
+    const int32_t k = S.sk[i];
     int rank = i;
     if (!sorted) {
       rank = 0;
       for (int j = 0; j < R; ++j) {
-        const int32_t kj = L.sk[j];
+        const int32_t kj = S.sk[j];
         rank += kj < k || (kj == k && j < i);
       }
     }
-    L.pk[rank] = k;
-    L.pI[rank] = rep_int[r0 + i];
-    L.pidx[rank] = (int16_t)i;
+    S.pk[rank] = k;
+    S.pI[rank] = rep_int[r0 + i];
+    S.pidx[rank] = i;
   }
   __syncthreads();
   {
-    constexpr int PER = CS_RCAP / CS_BLOCK;
+    const int PER = (R + CS_BLOCK - 1) / CS_BLOCK;  // contiguous chunk per thread: runs in order
     int heads = 0;
-#pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int r = PER * tid + u;
-      heads += r < R && (r == 0 || L.pk[r] != L.pk[r - 1]);
+      heads += r < R && (r == 0 || S.pk[r] != S.pk[r - 1]);
     }
     int nr;
     int id = block_exclusive_scan<CS_BLOCK>(heads, L.tmp, nr);
-#pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int r = PER * tid + u;
-      if (r < R && (r == 0 || L.pk[r] != L.pk[r - 1])) {
+      if (r < R && (r == 0 || S.pk[r] != S.pk[r - 1])) {
         double A = 0.0;  // np.bincount: out[bin] = 0.0, then += w in input order
-        for (int q = r; q < R && L.pk[q] == L.pk[r]; ++q) A += L.pI[q];
-        L.rb[id] = L.pk[r];
-        L.rs[id] = (int16_t)r;
-        L.rA[id] = A;
+        for (int q = r; q < R && S.pk[q] == S.pk[r]; ++q) A += S.pI[q];
+        S.rb[id] = S.pk[r];
+        S.rs[id] = r;
+        S.rA[id] = A;
         ++id;
       }
     }
-    if (tid == 0) { L.nruns = nr; L.rs[nr] = (int16_t)R; }
+    if (tid == 0) { L.nruns = nr; S.rs[nr] = R; }
     __syncthreads();
+    const int PR = (nr + CS_BLOCK - 1) / CS_BLOCK;
     double sq = 0.0;
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int r = PER * tid + u;
-      if (r < nr && L.rb[r] >= 0) sq += L.rA[r] * L.rA[r];
+    for (int u = 0; u < PR; ++u) {
+      const int r = PR * tid + u;
+      if (r < nr && S.rb[r] >= 0) sq += S.rA[r] * S.rA[r];
     }
     double tot;
     double pre = block_exclusive_scan<CS_BLOCK>(sq, L.tmpd, tot);
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int r = PER * tid + u;
+    for (int u = 0; u < PR; ++u) {
+      const int r = PR * tid + u;
       if (r < nr) {
-        L.rA2[r] = pre;
-        if (L.rb[r] >= 0) pre += L.rA[r] * L.rA[r];
+        S.rA2[r] = pre;
+        if (S.rb[r] >= 0) pre += S.rA[r] * S.rA[r];
       }
     }
-    if (tid == 0) L.rA2[nr] = tot;
+    if (tid == 0) S.rA2[nr] = tot;
     // bucket t: the first run with a bin >= t << CS_BSH (runs are sorted by bin)
     for (int t = tid; t < CS_BMAX; t += CS_BLOCK) {
       const int64_t b0 = (int64_t)t << CS_BSH;
       int lo = 0, hi = nr;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if ((int64_t)L.rb[mid] < b0) lo = mid + 1;
+        if ((int64_t)S.rb[mid] < b0) lo = mid + 1;
         else hi = mid;
       }
-      L.bst[t] = (uint16_t)lo;
+      L.bst[t] = lo;
     }
     __syncthreads();
   }
@@ -208,31 +219,31 @@ __global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosP
     const int64_t kc = Lc - 2;                                          // the last bin
     const double e_last = cs_edge(P, Lc - 1), rl = np_around(e_last, P.p10);
     // representative under this pair's cut: A.A and the on-edge extra of bin kc
-    const int ic = runs_upper(L.rb, NR, kc);  // runs with a bin <= kc
+    const int ic = runs_upper(S.rb, NR, kc);  // runs with a bin <= kc
     double extra = 0.0;
     bool has_extra = false;
-    if (ic < NR && (int64_t)L.rb[ic] == kc + 1) {
-      for (int q = L.rs[ic]; q < L.rs[ic + 1]; ++q) {
-        const double x = rep_mz[r0 + L.pidx[q]];
+    if (ic < NR && (int64_t)S.rb[ic] == kc + 1) {
+      for (int q = S.rs[ic]; q < S.rs[ic + 1]; ++q) {
+        const double x = rep_mz[r0 + S.pidx[q]];
         if (x >= e_last && np_around(x, P.p10) == rl) {
-          extra += L.pI[q];
+          extra += S.pI[q];
           has_extra = true;
         }
       }
     }
-    const bool kc_run = ic > 0 && (int64_t)L.rb[ic - 1] == kc;
-    const double A_kc = (kc_run ? L.rA[ic - 1] : 0.0) + extra;  // A'_{kc}
-    double aa = L.rA2[ic];
-    if (has_extra) aa = L.rA2[kc_run ? ic - 1 : ic] + A_kc * A_kc;
+    const bool kc_run = ic > 0 && (int64_t)S.rb[ic - 1] == kc;
+    const double A_kc = (kc_run ? S.rA[ic - 1] : 0.0) + extra;  // A'_{kc}
+    double aa = S.rA2[ic];
+    if (has_extra) aa = S.rA2[kc_run ? ic - 1 : ic] + A_kc * A_kc;
     auto lookup = [&](int64_t b) -> double {
       if (b == kc) return A_kc;
       if ((b >> CS_BSH) < CS_BMAX) {  // bucket start, then a short forward walk
         int u = L.bst[b >> CS_BSH];
-        while (u < NR && (int64_t)L.rb[u] < b) ++u;
-        return (u < NR && (int64_t)L.rb[u] == b) ? L.rA[u] : 0.0;
+        while (u < NR && (int64_t)S.rb[u] < b) ++u;
+        return (u < NR && (int64_t)S.rb[u] == b) ? S.rA[u] : 0.0;
       }
-      const int u = runs_upper(L.rb, NR, b);
-      return (u > 0 && (int64_t)L.rb[u - 1] == b) ? L.rA[u - 1] : 0.0;
+      const int u = runs_upper(S.rb, NR, b);
+      return (u > 0 && (int64_t)S.rb[u - 1] == b) ? S.rA[u - 1] : 0.0;
     };
     auto mem_bin = [&](double x) -> int64_t {
       const int64_t k = cs_bin(P, x);
@@ -332,6 +343,55 @@ __global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosP
     for (int j = 0; j < n; ++j) sum += cos_out[s0 + j];
     avg_out[c] = sum / (double)n;
     status[c] = kOk;
+  }
+  return true;
+}
+
+// Clusters whose representative fits LDS; larger ones go to `deferred`.
+__global__ __launch_bounds__(CS_BLOCK) void binned_cosine_kernel(CsrView v, CosParams P, const int64_t* rep_off,
+                                                                 const double* rep_mz, const double* rep_int,
+                                                                 double* cos_out, double* avg_out, int32_t* status,
+                                                                 int32_t* deferred, int32_t* n_deferred) {
+  __shared__ CosSmem L;
+  CosState S;
+  S.sk = L.sk; S.pk = L.pk; S.pI = L.pI; S.pidx = L.pidx; S.rb = L.rb; S.rs = L.rs; S.rA = L.rA; S.rA2 = L.rA2;
+  S.cap = CS_RCAP;
+  const int64_t c = blockIdx.x;
+  if (!cos_body(v, P, S, L.sh, c, rep_off, rep_mz, rep_int, cos_out, avg_out, status) && threadIdx.x == 0) {
+    status[c] = kDeferred;
+    deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+  }
+}
+
+// Bytes of one scratch slice for representatives of up to `cap` peaks.
+__host__ __device__ inline int64_t cos_slice_bytes(int64_t cap) {
+  return 5 * ((4 * (cap + 1) + 255) & ~int64_t(255)) + 3 * ((8 * (cap + 1) + 255) & ~int64_t(255));
+}
+
+// The deferred clusters (representative > CS_RCAP peaks): the same body with the
+// representative's arrays in a per-workgroup global scratch slice.
+__global__ __launch_bounds__(CS_BLOCK) void binned_cosine_global_kernel(
+    CsrView v, CosParams P, const int64_t* rep_off, const double* rep_mz, const double* rep_int, double* cos_out,
+    double* avg_out, int32_t* status, const int32_t* deferred, const int32_t* n_deferred, char* scratch, int cap) {
+  __shared__ CosShared L;
+  char* base = scratch + (int64_t)blockIdx.x * cos_slice_bytes(cap);
+  const int64_t s4 = (4 * ((int64_t)cap + 1) + 255) & ~int64_t(255), s8 = (8 * ((int64_t)cap + 1) + 255) & ~int64_t(255);
+  CosState S;
+  S.sk = reinterpret_cast<int32_t*>(base);
+  S.pk = reinterpret_cast<int32_t*>(base + s4);
+  S.pidx = reinterpret_cast<int32_t*>(base + 2 * s4);
+  S.rb = reinterpret_cast<int32_t*>(base + 3 * s4);
+  S.rs = reinterpret_cast<int32_t*>(base + 4 * s4);
+  S.pI = reinterpret_cast<double*>(base + 5 * s4);
+  S.rA = reinterpret_cast<double*>(base + 5 * s4 + s8);
+  S.rA2 = reinterpret_cast<double*>(base + 5 * s4 + 2 * s8);
+  S.cap = cap;
+  const int32_t nd = *n_deferred;
+  for (int32_t i = blockIdx.x; i < nd; i += gridDim.x) {
+    const int64_t c = deferred[i];
+    if (!cos_body(v, P, S, L, c, rep_off, rep_mz, rep_int, cos_out, avg_out, status) && threadIdx.x == 0)
+      status[c] = kDeferred;  // longer than the workspace was sized for
+    __syncthreads();
   }
 }
 

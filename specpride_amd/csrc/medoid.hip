@@ -174,6 +174,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   __shared__ MedoidRegSmem L;
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
   const int64_t c = blockIdx.x;
+  SPX_STAMP(0);
   const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
   const int n = (int)(s1 - s0);
   if (s1 - s0 > MD_NMAX) {
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     }
   }
 
+  SPX_STAMP(1);
   // P1: one read of every m/z; bins packed two per register.  Batches of 8
   // loads per thread, double-buffered (batch b+1 in flight while b is binned).
   // The batch count is a compile-time constant per size class, so every load
@@ -287,6 +289,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     return;
   }
   const int nw = np > 0 ? (int)(L.red[0] >> 6) + 1 : 0;
+  SPX_STAMP(2);
   // P2: compact columns (exclusive popcount prefix into the records)
   int K;
   {
@@ -309,6 +312,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
     return;
   }
+  SPX_STAMP(3);
   // P3: bit-packed rows from the register bins
   for (int w = tid; w < n * KW; w += MD_BLOCK) L.u.a.rows[w] = 0ull;
   // start-bit word 4u + wid and its prefix for slice u, lane u holds them
@@ -341,6 +345,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     }
   }
   __syncthreads();
+  SPX_STAMP(4);
 
   // P4: every pair i <= j of the row-major upper triangle (row i starts at
   // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
@@ -381,6 +386,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   // diagonal, zeros below (most_similar_representative.py:91-93)
   auto dval = [&](int a, int b) -> double { return b >= a ? L.u.d[row_start(a) + b - a] : 0.0; };
 
+  SPX_STAMP(5);
   // P5: totals, 16 lanes per spectrum (8 row accumulators, 8 column ones)
   const int k = lane & 7;
   const bool colside = (lane & 8) != 0;
@@ -412,6 +418,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     }
   }
   __syncthreads();
+  SPX_STAMP(6);
   // P6: first index of the minimum (:103-110)
   if (tid < kWave) {
     double t = tid < n ? L.totals[tid] : __longlong_as_double(0x7ff0000000000000ll);
@@ -424,6 +431,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     }
     if (tid == 0) rep[c] = s0 + idx;
   }
+  SPX_STAMP(7);
 }
 
 // ------------------------------------------------------------ large path

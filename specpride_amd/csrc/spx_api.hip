@@ -71,9 +71,15 @@ int32_t bin_words(const spx_bin_params* p) {
   return (int32_t)((nb + 63.0) / 64.0);
 }
 
+// Bitmap words of the gap-average global slice: the batch's m/z span in
+// half-accuracy buckets.  A non-finite or absurd span (a caller's bad info) is
+// clamped: clusters past the slice report SPX_UNRESOLVED, they are never read
+// out of bounds.
 int gap_wcap(const spx_gap_params* p, const spx_batch_info* info) {
-  const double span = (info && info->max_mz_span > 0) ? info->max_mz_span : 5000.0;
-  return (int)std::ceil((span / (p->mz_accuracy * 0.5) + 3.0) / 64.0);
+  double span = (info && info->max_mz_span > 0) ? info->max_mz_span : 5000.0;
+  if (!std::isfinite(span)) span = 5000.0;
+  const double w = std::ceil((span / (p->mz_accuracy * 0.5) + 3.0) / 64.0);
+  return (int)std::min(w, (double)(1 << 24));
 }
 
 }  // namespace
@@ -319,14 +325,29 @@ extern "C" int spx_xcorr_distance(const spx_csr* csr, const spx_medoid_params* p
 }
 
 // ------------------------------------------------------------ binned cosine
+extern "C" size_t spx_binned_cosine_workspace_size(int64_t n_clusters, int64_t max_rep_peaks) {
+  if (n_clusters < 0 || max_rep_peaks < 0) return 0;
+  const int64_t cap = std::max<int64_t>(max_rep_peaks, 1);
+  return align256(sizeof(int32_t)) + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(n_clusters, 1)) +
+         (max_rep_peaks > spx::CS_RCAP ? (size_t)fallback_grid(n_clusters) * (size_t)spx::cos_slice_bytes(cap) : 0);
+}
+
 extern "C" int spx_binned_cosine(const spx_csr* csr, const int64_t* rep_off, const double* rep_mz,
                                  const double* rep_inten, const spx_cosine_params* params, double* cos_out,
-                                 double* avg_out, int32_t* status, void* stream) {
+                                 double* avg_out, int32_t* status, int64_t max_rep_peaks, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
   if (!csr_ok(csr) || !rep_off || !params || !avg_out || !status || (csr->n_spectra && !cos_out))
     return fail(SPX_EINVAL, "spx_binned_cosine: null argument");
   if (!(params->mz_space > 0)) return fail(SPX_EINVAL, "spx_binned_cosine: mz_space must be > 0");
   const int64_t C = csr->n_clusters;
+  const size_t need = spx_binned_cosine_workspace_size(C, max_rep_peaks);
+  if (need == 0 || !workspace || workspace_bytes < need) return fail(SPX_ENOSPACE, "spx_binned_cosine: workspace too small");
   if (C == 0) return SPX_SUCCESS;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
+  int32_t* n_def = w.take<int32_t>(1);
+  int32_t* def = w.take<int32_t>((size_t)C);
+  char* scratch = w.base + w.used;
   // np.arange(-s/2, stop, s): e0 = start, e1 = start + s, e_i = start + i * (e1 - e0)
   // (numpy DOUBLE_fill); scipy's on-edge rounding keeps int(-log10(min edge gap)) + 6 decimals
   spx::CosParams P;
@@ -337,10 +358,15 @@ extern "C" int spx_binned_cosine(const spx_csr* csr, const int64_t* rep_off, con
   P.inv_d = 1.0 / P.d;
   const int dec = (int)(-std::log10(std::min(P.d, P.s))) + 6;
   P.p10 = std::pow(10.0, (double)dec);
-  hipLaunchKernelGGL(spx::binned_cosine_kernel, dim3((unsigned)C), dim3(spx::CS_BLOCK), 0,
-                     reinterpret_cast<hipStream_t>(stream), view(csr), P, rep_off, rep_mz, rep_inten, cos_out, avg_out,
-                     status);
-  return check_launch("binned_cosine_kernel");
+  if (hipMemsetAsync(n_def, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_binned_cosine memset");
+  hipLaunchKernelGGL(spx::binned_cosine_kernel, dim3((unsigned)C), dim3(spx::CS_BLOCK), 0, s, view(csr), P, rep_off,
+                     rep_mz, rep_inten, cos_out, avg_out, status, def, n_def);
+  if (int rc = check_launch("binned_cosine_kernel")) return rc;
+  if (max_rep_peaks <= spx::CS_RCAP) return SPX_SUCCESS;  // nothing can be deferred
+  hipLaunchKernelGGL(spx::binned_cosine_global_kernel, dim3((unsigned)fallback_grid(C)), dim3(spx::CS_BLOCK), 0, s,
+                     view(csr), P, rep_off, rep_mz, rep_inten, cos_out, avg_out, status, def, n_def, scratch,
+                     (int)std::min<int64_t>(max_rep_peaks, INT32_MAX - 1));
+  return check_launch("binned_cosine_global_kernel");
 }
 
 // --------------------------------------------------------- best spectrum

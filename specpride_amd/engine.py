@@ -64,17 +64,26 @@ class DeviceBatch:
 
     @classmethod
     def from_host(cls, csr: SpectraCSR, device="cuda") -> "DeviceBatch":
-        span = 0.0
-        if csr.n_peaks:
-            span = float(np.nanmax(csr.mz) - np.nanmin(csr.mz)) if np.isfinite(csr.mz).any() else 0.0
+        # the m/z span over FINITE values only: a NaN/inf peak makes its cluster
+        # SPX_NON_FINITE, it must not blow up the workspace sizing of the others
+        fin = csr.mz[np.isfinite(csr.mz)] if csr.n_peaks else csr.mz
+        span = float(fin.max() - fin.min()) if len(fin) else 0.0
         return cls(csr.to_device(device), csr.cluster_off, csr.spec_off, span,
                    cluster_ids=csr.cluster_ids, titles=csr.titles)
 
     @classmethod
     def from_device(cls, tensors: dict) -> "DeviceBatch":
         """Wrap tensors already in HBM (e.g. synthetic.make_clusters_torch)."""
+        import torch
+
         mz = tensors["mz"]
-        span = float((mz.max() - mz.min()).item()) if mz.numel() else 0.0
+        span = 0.0
+        if mz.numel():
+            fin = torch.isfinite(mz)
+            inf = torch.tensor(float("inf"), dtype=mz.dtype, device=mz.device)
+            hi = torch.where(fin, mz, -inf).max()
+            lo = torch.where(fin, mz, inf).min()
+            span = float((hi - lo).clamp(min=0.0).item()) if bool(fin.any().item()) else 0.0
         return cls(tensors, tensors["cluster_off"].cpu().numpy(), tensors["spec_off"].cpu().numpy(), span)
 
     def workspace(self, key: str, nbytes: int):
@@ -282,28 +291,38 @@ MZ_SPACE = 1.000508 * .005  # benchmark.py:7-8 (mz_unit * .005)
 class CosineResult:
     cos: object     # [S] f64: cos_dist(representative, member) per member spectrum
     avg: object     # [C] f64: average_cos_dist per cluster
-    status: object  # [C] i32 (STATUS_EMPTY: an empty spectrum; STATUS_UNRESOLVED: > 1,024 representative peaks)
+    status: object  # [C] i32 (STATUS_EMPTY: an empty spectrum)
 
     def to_host(self):
         return self.cos.cpu().numpy(), self.avg.cpu().numpy(), self.status.cpu().numpy()
 
 
 def binned_cosine(batch: DeviceBatch, rep_off, rep_mz, rep_int, mz_space=MZ_SPACE,
-                  out: Optional[CosineResult] = None, stream=None) -> CosineResult:
+                  out: Optional[CosineResult] = None, stream=None, max_rep_peaks: Optional[int] = None) -> CosineResult:
     """cos_dist / average_cos_dist (benchmark.py:19-38) for every cluster of the
     batch: cluster c's representative is the device peak list
-    [rep_off[c], rep_off[c+1]) of rep_mz / rep_int, its members are its spectra."""
+    [rep_off[c], rep_off[c+1]) of rep_mz / rep_int, its members are its spectra.
+    ``max_rep_peaks`` (an upper bound on the representatives' lengths) sizes the
+    workspace for representatives past the LDS path's 1,024 peaks; if omitted it
+    is read from ``rep_off`` (one small device reduction and host read)."""
     import torch
 
     dev = batch.device
+    C = batch.n_clusters
     if out is None:
         out = CosineResult(torch.empty(max(batch.n_spectra, 1), dtype=torch.float64, device=dev),
-                           torch.empty(max(batch.n_clusters, 1), dtype=torch.float64, device=dev),
-                           torch.empty(max(batch.n_clusters, 1), dtype=torch.int32, device=dev))
+                           torch.empty(max(C, 1), dtype=torch.float64, device=dev),
+                           torch.empty(max(C, 1), dtype=torch.int32, device=dev))
+    if max_rep_peaks is None:
+        max_rep_peaks = int((rep_off[1:C + 1] - rep_off[:C]).max().item()) if C else 0
+    L = _lib.lib()
+    need = L.spx_binned_cosine_workspace_size(C, int(max_rep_peaks))
+    ws = batch.workspace("binned_cosine", need)
     prm = _lib.SpxCosineParams(float(mz_space))
-    _lib.check(_lib.lib().spx_binned_cosine(ctypes.byref(batch.csr), _ptr(rep_off), _ptr(rep_mz), _ptr(rep_int),
-                                            ctypes.byref(prm), _ptr(out.cos), _ptr(out.avg), _ptr(out.status),
-                                            _stream_handle(stream)), "spx_binned_cosine")
+    _lib.check(L.spx_binned_cosine(ctypes.byref(batch.csr), _ptr(rep_off), _ptr(rep_mz), _ptr(rep_int),
+                                   ctypes.byref(prm), _ptr(out.cos), _ptr(out.avg), _ptr(out.status),
+                                   int(max_rep_peaks), _ptr(ws), ws.numel(), _stream_handle(stream)),
+               "spx_binned_cosine")
     return out
 
 

@@ -64,23 +64,30 @@ def _accessions(elem) -> set:
 
 
 def _binary_array(bda):
+    """(name, accessions, raw base64 text) of a binaryDataArray: decoded later."""
     acc = _accessions(bda)
-    dtype = np.float32 if _F32 in acc else np.float64
     raw = ""
     for ch in bda:
         if _local(ch.tag) == "binary":
             raw = ch.text or ""
-    data = base64.b64decode(raw.strip()) if raw.strip() else b""
+    name = "m/z array" if _MZ_ARRAY in acc else ("intensity array" if _INT_ARRAY in acc else None)
+    return name, acc, raw.strip()
+
+
+def _decode(acc, raw: str):
+    dtype = np.float32 if _F32 in acc else np.float64
+    data = base64.b64decode(raw) if raw else b""
     if _ZLIB in acc and data:
         data = zlib.decompress(data)
-    arr = np.frombuffer(data, dtype=dtype).copy()
-    name = "m/z array" if _MZ_ARRAY in acc else ("intensity array" if _INT_ARRAY in acc else None)
-    return name, arr
+    return np.frombuffer(data, dtype=dtype).copy()
 
 
 def _spectrum(elem) -> dict:
+    """The spectrum's metadata; its binary arrays stay encoded under '_raw' until
+    :meth:`MzML.get_by_id` decodes them."""
     sp = {"id": elem.get("id"), "index": int(elem.get("index", -1))}
     sp.update(_cv(elem))
+    raw = {}
     for ch in elem:
         t = _local(ch.tag)
         if t == "precursorList":
@@ -100,29 +107,36 @@ def _spectrum(elem) -> dict:
         elif t == "binaryDataArrayList":
             for bda in ch:
                 if _local(bda.tag) == "binaryDataArray":
-                    name, arr = _binary_array(bda)
+                    name, acc, text = _binary_array(bda)
                     if name:
-                        sp[name] = arr
+                        raw[name] = (acc, text)
+    sp["_raw"] = raw
     return sp
 
 
 class MzML:
     """``with MzML(fh) as reader: reader.get_by_id(id)`` over an mzML byte stream
-    (path, file object, or ``.gz`` path).  The spectra are indexed by id on open."""
+    (path, file object, or ``.gz`` path).  One streaming pass indexes the spectra
+    by id; binary arrays are base64/zlib-decoded only when a spectrum is fetched
+    (pyteomics' get_by_id is lazy too).  ``ids`` (optional): keep only these
+    spectra -- the caller's MaRaCluster scan list -- so a multi-GB run with MS1
+    scans costs memory for the wanted spectra alone."""
 
-    def __init__(self, source):
+    def __init__(self, source, ids=None):
         own = False
         if isinstance(source, str):
             source = gzip.open(source) if re.search(r"\.gz$", source) else open(source, "rb")
             own = True
+        keep = None if ids is None else set(ids)
         self._spectra = {}
         self._order = []
         try:
             for _, elem in ET.iterparse(source, events=("end",)):
                 if _local(elem.tag) == "spectrum":
-                    sp = _spectrum(elem)
-                    self._spectra[sp["id"]] = sp
-                    self._order.append(sp["id"])
+                    if keep is None or elem.get("id") in keep:
+                        sp = _spectrum(elem)
+                        self._spectra[sp["id"]] = sp
+                        self._order.append(sp["id"])
                     elem.clear()
         finally:
             if own:
@@ -135,19 +149,24 @@ class MzML:
         return False
 
     def __iter__(self):
-        return (self._spectra[i] for i in self._order)
+        return (self.get_by_id(i) for i in self._order)
 
     def __len__(self):
         return len(self._order)
 
     def get_by_id(self, spectrum_id: str) -> dict:
         """KeyError for an unknown id (pyteomics raises KeyError too)."""
-        return self._spectra[spectrum_id]
+        sp = self._spectra[spectrum_id]
+        raw = sp.pop("_raw", None)
+        if raw:
+            for name, (acc, text) in raw.items():
+                sp[name] = _decode(acc, text)
+        return sp
 
 
-def read(source) -> MzML:
+def read(source, ids=None) -> MzML:
     """``pyteomics.mzml.read`` stand-in (the reference uses it as a context manager)."""
-    return MzML(source)
+    return MzML(source, ids=ids)
 
 
 # ---------------------------------------------------------------- writer (tests, synthetic inputs)

@@ -109,3 +109,27 @@ def test_benchmark_shim_names(gpu):
     assert benchmark.average_cos_dist(a, [a, b]) == pytest.approx((1.0 + want) / 2, rel=RTOL)
     with pytest.raises(IndexError):
         benchmark.cos_dist(a, SimpleNamespace(mz=np.zeros(0), intensity=np.zeros(0)))
+
+
+def test_binned_cosine_representatives_past_lds(gpu):
+    """Representatives of 1,025-5,000 peaks (the global-scratch path), mixed with
+    ordinary ones in one call; one of them unsorted (the rank sort), one sharing
+    bins with every member (runs of several peaks)."""
+    rng = np.random.default_rng(41)
+    clusters, reps = [], []
+    for k, R in enumerate((300, 1025, 2048, 5000, 900, 1500)):
+        base = np.sort(rng.uniform(100, 1900, 60))
+        members = [{"m/z array": np.round(np.sort(base + rng.normal(0, 0.002, 60)), 5),
+                    "intensity array": rng.lognormal(5, 1, 60)} for _ in range(3 + k)]
+        clusters.append(members)
+        rm = np.concatenate([np.repeat(base, 3) + rng.normal(0, 0.0005, 180), rng.uniform(100, 1990, R - 180)])
+        rm = np.round(rm, 5)
+        if k != 5:
+            rm = np.sort(rm)  # cluster 5: an unsorted representative
+        reps.append((rm, rng.lognormal(4, 1, len(rm))))
+    csr = SpectraCSR.from_clusters(clusters)
+    rep_off = np.concatenate([[0], np.cumsum([len(r[0]) for r in reps])])
+    rep_mz, rep_int = np.concatenate([r[0] for r in reps]), np.concatenate([r[1] for r in reps])
+    got = _run(csr, rep_off, rep_mz, rep_int)
+    assert np.all(got[2][:csr.n_clusters] == 0)
+    _check(got, np_oracle.binned_cosine(csr, rep_off, rep_mz, rep_int), csr.n_clusters, csr.n_spectra)

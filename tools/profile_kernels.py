@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--which", default="bm,md,ga")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--stamps-kernel", default="bm", choices=["bm", "md"])
     ap.add_argument("--build-stamps", action="store_true")
     a = ap.parse_args()
     if a.build_stamps:
@@ -83,25 +84,29 @@ def main():
         L.spx_debug_stamps.argtypes = [ctypes.c_void_p]
         buf = torch.zeros(b.n_clusters * 8, dtype=torch.int64, device="cuda")
         assert L.spx_debug_stamps(buf.data_ptr()) == 0
-        engine.bin_mean(b, out=bm)
+        if a.stamps_kernel == "bm":
+            engine.bin_mean(b, out=bm)
+        else:
+            engine.medoid(b, out=md, check=False)
         torch.cuda.synchronize()
         L.spx_debug_stamps(None)
         s = buf.view(-1, 8).cpu().numpy().astype(np.float64)
         sizes = np.diff(b.host_cluster_off)
         ph = {}
-        for k in range(1, 6):
+        last = 5 if a.stamps_kernel == "bm" else 7
+        for k in range(1, last + 1):
             ok = (s[:, k] > 0) & (s[:, k - 1] > 0)
             if ok.any():
                 ph[f"p{k - 1}->p{k}"] = round(float(np.mean(s[ok, k] - s[ok, k - 1])), 1)
-        ok = (s[:, 5] > 0) & (s[:, 0] > 0)
-        ph["lifetime"] = round(float(np.mean(s[ok, 5] - s[ok, 0])), 1)
+        ok = (s[:, last] > 0) & (s[:, 0] > 0)
+        ph["lifetime"] = round(float(np.mean(s[ok, last] - s[ok, 0])), 1)
         bands = {}
         for lo, hi in ((2, 10), (11, 25), (26, 40), (41, 50)):
-            m = ok & (sizes >= lo) & (sizes <= hi) & (s[:, 4] > 0)
+            m = ok & (sizes >= lo) & (sizes <= hi) & (s[:, last - 1] > 0)
             if m.any():
                 bands[f"n{lo}-{hi}"] = {f"p{k - 1}->p{k}": round(float(np.mean(s[m, k] - s[m, k - 1])), 1)
-                                        for k in range(1, 6)}
-        span = (s[ok, 5].max() - s[ok, 0].min())
+                                        for k in range(1, last + 1)}
+        span = (s[ok, last].max() - s[ok, 0].min())
         res["stamps"] = {"phases_cycles": ph, "by_size": bands, "span_cycles": span,
                          "cycles_per_cluster_per_cu": round(span * 256 / ok.sum(), 1)}
     print(json.dumps(res), flush=True)
