@@ -138,31 +138,71 @@ def median_rt(spectra):
 # ------------------------------------------------------------ batch driver
 def process_maracluster_mgf(fname, get_cluster=get_cluster_id, get_pepmass=naive_average_mass_and_charge,
                             get_rt=median_rt, **kwargs):
-    """Average every consecutive-title cluster of an MGF (:151-165) in one GPU pass."""
-    spectra = read_mgf(fname)
-    runs = []
-    for cluster_id, grp in groupby(spectra, lambda s: get_cluster(s["params"]["title"])):
-        runs.append((cluster_id, list(grp)))
+    """Average every consecutive-title cluster of an MGF (:151-165) in one GPU pass.
+
+    With the standard helpers the file goes through the native parser straight
+    into the CSR (no per-spectrum Python objects); custom callables, or a file
+    outside the native subset, take the dict path."""
     # the standard helpers run on the device in the same pass; custom callables on the host
     pm_mode = {lower_median_mass: "lower_median", naive_average_mass_and_charge: "naive_average",
                neutral_average_mass_and_charge: "neutral_average"}.get(get_pepmass)
     rt_mode = {median_rt: "median", lower_median_mass_rt: "mass_lower_median"}.get(get_rt)
     on_device = pm_mode is not None and rt_mode is not None
-    r = _average_batch([sp for _cid, sp in runs], kwargs.get("mz_accuracy", DIFF_THRESH),
-                       kwargs.get("dyn_range", DYN_RANGE), kwargs.get("min_fraction", MIN_FRACTION),
+    acc = kwargs.get("mz_accuracy", DIFF_THRESH)
+    dyn = kwargs.get("dyn_range", DYN_RANGE)
+    frac = kwargs.get("min_fraction", MIN_FRACTION)
+    if on_device and get_cluster is get_cluster_id:
+        native = _native_runs(fname)
+        if native is not None:
+            ids, csr = native
+            r = engine.gap_average(engine.DeviceBatch.from_host(csr), acc, dyn, frac, pepmass=pm_mode,
+                                   rt=rt_mode).to_host()
+            return _outputs(r, ids)
+    spectra = read_mgf(fname)
+    runs = []
+    for cluster_id, grp in groupby(spectra, lambda s: get_cluster(s["params"]["title"])):
+        runs.append((cluster_id, list(grp)))
+    r = _average_batch([sp for _cid, sp in runs], acc, dyn, frac,
                        pepmass=pm_mode or "lower_median", rt=rt_mode or "mass_lower_median")
+    if on_device:
+        return _outputs(r, [cid for cid, _sp in runs])
     outputs = []
     for c, (cluster_id, sp) in enumerate(runs):
-        if on_device:
-            mz, ch, rt = float(r["prec"][c]), int(r["charge"][c]), float(r["rt"][c])
-        else:
-            (mz, ch), rt = get_pepmass(sp), get_rt(sp)
+        (mz, ch), rt = get_pepmass(sp), get_rt(sp)
         if r["status"][c] != engine.STATUS_OK:
             _raise_for(r["status"][c])
         a, b = r["out_off"][c], r["out_off"][c + 1]
         outputs.append({"params": {"title": cluster_id, "pepmass": mz, "rtinseconds": rt, "charge": ch},
                         "m/z array": r["out_mz"][a:b].copy(), "intensity array": r["out_int"][a:b].copy()})
     return outputs
+
+
+def _outputs(r, ids):
+    """Output spectra of a device pass whose precursor fields came from the device."""
+    outputs = []
+    for c, cluster_id in enumerate(ids):
+        if r["status"][c] != engine.STATUS_OK:
+            _raise_for(r["status"][c])
+        a, b = r["out_off"][c], r["out_off"][c + 1]
+        outputs.append({"params": {"title": cluster_id, "pepmass": float(r["prec"][c]),
+                                   "rtinseconds": float(r["rt"][c]), "charge": int(r["charge"][c])},
+                        "m/z array": r["out_mz"][a:b].copy(), "intensity array": r["out_int"][a:b].copy()})
+    return outputs
+
+
+def _native_runs(fname):
+    """Native parse -> (run ids, CSR of the consecutive-title runs), or None when
+    the file is outside the native subset or a record has no TITLE."""
+    from . import ingest, mgf_native
+
+    try:
+        flat = mgf_native.parse_general(fname)
+    except ValueError:
+        return None
+    if flat is None or not flat["has_title"].all():
+        return None
+    ids, records, sizes = ingest.gap_average_groups(flat["titles"])
+    return ids, ingest.csr_from_flat(flat, sizes)
 
 
 def main(argv=None):
@@ -199,8 +239,17 @@ def main(argv=None):
         write_pyteomics_style([average_spectrum(spectra, title=args.output, pepmass=mz, charge=c, rtinseconds=rt,
                                                 **kwargs)], args.output, file_mode=mode)
     elif args.encodedclusters:
-        write_pyteomics_style(process_maracluster_mgf(args.input, get_pepmass=get_pepmass, get_rt=get_rt, **kwargs),
-                              args.output, file_mode=mode)
+        def single():
+            write_pyteomics_style(process_maracluster_mgf(args.input, get_pepmass=get_pepmass, get_rt=get_rt,
+                                                          **kwargs), args.output, file_mode=mode)
+
+        from . import sharded_cli
+
+        if sharded_cli.launched_distributed():  # torchrun: rank-local ingest, one GPU per rank
+            sharded_cli.run_cli(sharded_cli.gap_average, single, args.input, args.output, pepmass=args.pepmass,
+                                rt=args.rt, file_mode=mode, **kwargs)
+        else:
+            single()
     else:
         raise NotImplementedError("This mode is not implemented yet.")
 

@@ -235,22 +235,33 @@ def main(argv=None):
         print("Example: representative_spectrum_creator.py --mgf_file=../data/clustered_mgf.mgf")
         print("Or use --help for additional usage information")
         sys.exit(10)
+    from . import sharded_cli
+
+    if sharded_cli.launched_distributed():  # torchrun: rank-local ingest, one GPU per rank
+        sharded_cli.run_cli(sharded_cli.binning, lambda: _main_mgf(params.mgf_file, params.out, verbose),
+                            params.mgf_file, params.out)
+        return
+    _main_mgf(params.mgf_file, params.out, verbose)
+
+
+def _main_mgf(mgf_file, out, verbose):
+    """The single-process ``--mgf_file`` CLI body (binning.py:286-302)."""
     rsc = RepresentativeSpectrumCreator(verbose=verbose)
     print("Reading spectra...")
-    flat = _flat_clusters(params.mgf_file)
+    flat = _flat_clusters(mgf_file)
     if flat is not None:  # native parse straight to the cluster-segmented CSR
         ids, csr = flat
         print("Clustering...")
         merged = rsc._combine_csr(csr, [None] * len(ids), minimum=100, maximum=2000, binsize=0.02)
     else:  # the reference's own line loop decides (malformed or unusual input)
-        clusters = rsc.read_spectra_clustered_mgf(params.mgf_file)
+        clusters = rsc.read_spectra_clustered_mgf(mgf_file)
         print("Clustering...")
         ids = list(clusters.keys())
         merged = rsc.combine_bin_mean_batch([clusters[k] for k in ids], minimum=100, maximum=2000, binsize=0.02)
     for cid, spec in zip(ids, merged):
         spec["cluster_id"] = cid
-    with open(params.out, "wt") as mgf_file:
-        rsc.write_spectrum(merged, mgf_file)
+    with open(out, "wt") as fh:
+        rsc.write_spectrum(merged, fh)
 
 
 if __name__ == "__main__":

@@ -33,6 +33,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 namespace {
@@ -48,7 +49,7 @@ struct Chunk {
 
 struct Result {
   std::vector<int64_t> spec_off;
-  std::vector<double> mz, it, prec;
+  std::vector<double> mz, it, prec, rt;
   std::vector<int64_t> charge;
   std::vector<int32_t> flags;
   std::string titles, error;
@@ -244,6 +245,151 @@ void parse_range(const char* b, const char* e, Chunk& C) {
   C.it.resize(mark);
 }
 
+// ---------------------------------------------------- general MGF (pyteomics shape)
+// The subset of specpride_amd.mgf.iter_mgf (the gap-average and medoid CLIs'
+// reader, pyteomics-shaped) whose meaning is unambiguous: stripped lines;
+// BEGIN IONS / END IONS blocks; inside, a line starting with a digit (or +-.
+// then a digit) is "mz [intensity]" split on spaces/tabs; KEY=value params with
+// TITLE (string), PEPMASS (mz [intensity]), CHARGE (one charge, "2+", "3-", "2"),
+// RTINSECONDS (float); other params are ignored (the writers do not emit them).
+// Anything else (several charges, non-decimal numbers, non-ASCII) -> fallback.
+struct GenChunk {
+  std::vector<int64_t> npk;
+  std::vector<double> mz, it, prec, rt;
+  std::vector<int64_t> charge;
+  std::vector<int32_t> flags;  // bit0 PEPMASS, bit1 CHARGE, bit2 RTINSECONDS, bit3 TITLE
+  std::string titles;
+  std::string error;
+};
+
+inline bool is_ws(unsigned char c) { return c == ' ' || c == '\t'; }
+
+bool parse_one_charge(const char* b, const char* e, int64_t& out) {
+  strip(b, e);
+  if (b == e) return false;
+  int sign = 1;
+  if (e[-1] == '+') --e;
+  else if (e[-1] == '-') { sign = -1; --e; }
+  while (b < e && *b == '+') ++b;
+  if (b == e || e - b > 17) return false;
+  int64_t v = 0;
+  for (const char* p = b; p < e; ++p) {
+    if (*p < '0' || *p > '9') return false;  // "2+ and 3+", "2,3": several charges
+    v = v * 10 + (*p - '0');
+  }
+  out = sign * v;
+  return true;
+}
+
+void parse_range_general(const char* b, const char* e, GenChunk& C) {
+  bool inside = false;
+  int64_t cur_np = 0;
+  double cur_prec = 0.0, cur_rt = 0.0;
+  int64_t cur_z = 0;
+  int32_t cur_f = 0;
+  std::string cur_title;
+  size_t mark = 0;
+  const char* p = b;
+  auto fail = [&](const char* why) { if (C.error.empty()) C.error = std::string("fallback: ") + why; };
+  while (p < e && C.error.empty()) {
+    const char* ls = p;
+    const char* le = p;
+    while (le < e && *le != '\n' && *le != '\r') ++le;
+    p = le;
+    if (p < e) {
+      if (*p == '\r') { ++p; if (p < e && *p == '\n') ++p; }
+      else ++p;
+    }
+    for (const char* q = ls; q < le; ++q)
+      if ((unsigned char)*q >= 0x80) { fail("non-ASCII text"); break; }
+    if (!C.error.empty()) break;
+    const char *sb = ls, *se = le;
+    strip(sb, se);
+    const size_t n = (size_t)(se - sb);
+    if (n == 0) continue;
+    if (n == 10 && std::memcmp(sb, "BEGIN IONS", 10) == 0) {
+      C.mz.resize(mark);
+      C.it.resize(mark);
+      inside = true;
+      cur_np = 0;
+      cur_f = 0;
+      cur_z = 0;
+      cur_title.clear();
+      continue;
+    }
+    if (n == 8 && std::memcmp(sb, "END IONS", 8) == 0) {
+      if (!inside) { fail("END IONS outside a block"); break; }
+      C.npk.push_back(cur_np);
+      C.prec.push_back((cur_f & 1) ? cur_prec : std::nan(""));
+      C.rt.push_back((cur_f & 4) ? cur_rt : std::nan(""));
+      C.charge.push_back(cur_z);
+      C.flags.push_back(cur_f);
+      C.titles += cur_title;
+      C.titles += '\n';
+      mark = C.mz.size();
+      inside = false;
+      continue;
+    }
+    if (!inside) continue;
+    const unsigned char c0 = (unsigned char)sb[0];
+    const bool digit0 = c0 >= '0' && c0 <= '9';
+    const bool signed0 = (c0 == '+' || c0 == '-' || c0 == '.') && n > 1 && sb[1] >= '0' && sb[1] <= '9';
+    if (digit0 || signed0) {
+      const char* t0 = sb;
+      const char* t0e = t0;
+      while (t0e < se && !is_ws((unsigned char)*t0e)) ++t0e;
+      const char* t1 = t0e;
+      while (t1 < se && is_ws((unsigned char)*t1)) ++t1;
+      const char* t1e = t1;
+      while (t1e < se && !is_ws((unsigned char)*t1e)) ++t1e;
+      double a, v = 0.0;
+      if (!parse_float(t0, t0e, a) || (t1 < t1e && !parse_float(t1, t1e, v))) { fail("peak value"); break; }
+      C.mz.push_back(a);
+      C.it.push_back(v);
+      ++cur_np;
+      continue;
+    }
+    const char* eq = (const char*)std::memchr(sb, '=', n);
+    if (!eq) continue;  // iter_mgf ignores lines that are neither peaks nor params
+    const size_t kl = (size_t)(eq - sb);
+    auto key_is = [&](const char* k) {
+      const size_t m = std::strlen(k);
+      if (m != kl) return false;
+      for (size_t i = 0; i < m; ++i)
+        if (std::tolower((unsigned char)sb[i]) != k[i]) return false;
+      return true;
+    };
+    const char *vb = eq + 1, *ve = se;
+    if (key_is("title")) {
+      cur_title.assign(vb, ve);
+      cur_f |= 8;
+    } else if (key_is("pepmass")) {
+      const char* a = vb;
+      while (a < ve && is_ws((unsigned char)*a)) ++a;
+      const char* ae = a;
+      while (ae < ve && !is_ws((unsigned char)*ae)) ++ae;
+      if (!parse_float(a, ae, cur_prec)) { fail("PEPMASS value"); break; }
+      const char* b2 = ae;
+      while (b2 < ve && is_ws((unsigned char)*b2)) ++b2;
+      const char* b2e = b2;
+      while (b2e < ve && !is_ws((unsigned char)*b2e)) ++b2e;
+      double pint;
+      if (b2 < b2e && !parse_float(b2, b2e, pint)) { fail("PEPMASS intensity"); break; }
+      cur_f |= 1;
+    } else if (key_is("charge")) {
+      if (!parse_one_charge(vb, ve, cur_z)) { fail("CHARGE value"); break; }
+      cur_f |= 2;
+    } else if (key_is("rtinseconds")) {
+      const char *a = vb, *ae = ve;
+      strip(a, ae);
+      if (!parse_float(a, ae, cur_rt)) { fail("RTINSECONDS value"); break; }
+      cur_f |= 4;
+    }
+  }
+  C.mz.resize(mark);
+  C.it.resize(mark);
+}
+
 bool read_file(const char* path, std::string& data, std::string& err) {
   FILE* f = std::fopen(path, "rb");
   if (!f) { err = std::string("cannot open ") + path; return false; }
@@ -340,6 +486,71 @@ int64_t format_binning(char* buf, int64_t cap, const char* cid, const char* char
   return (int64_t)(o - buf);
 }
 
+// Spectrum record start lines: "TITLE=" (binning.py's parser starts a peaklist
+// there) or a stripped "BEGIN IONS" (general MGF).
+inline bool record_start(const char* q, const char* e, int general) {
+  if (!general) return e - q >= 6 && std::memcmp(q, "TITLE=", 6) == 0;
+  const char* a = q;
+  const char* le = (const char*)std::memchr(q, '\n', (size_t)(e - q));
+  const char* b = le ? le : e;
+  strip(a, b);
+  return b - a == 10 && std::memcmp(a, "BEGIN IONS", 10) == 0;
+}
+
+// Per-thread byte ranges of [b, e) that begin at record starts.
+std::vector<const char*> split_records(const char* b, const char* e, int T, int general) {
+  std::vector<const char*> cuts{b};
+  const size_t size = (size_t)(e - b);
+  for (int t = 1; t < T; ++t) {
+    const char* q = b + size * (size_t)t / (size_t)T;
+    if (q <= cuts.back()) continue;
+    while (q < e) {
+      const char* nl = (const char*)std::memchr(q, '\n', (size_t)(e - q));
+      if (!nl) { q = e; break; }
+      q = nl + 1;
+      if (record_start(q, e, general)) break;
+    }
+    if (q < e && q > cuts.back()) cuts.push_back(q);
+  }
+  cuts.push_back(e);
+  return cuts;
+}
+
+template <class ChunkT>
+void merge_chunks(std::vector<ChunkT>& chunks, Result* R, bool with_rt) {
+  size_t S = 0, P = 0;
+  for (auto& c : chunks) {
+    if (!c.error.empty()) { R->error = c.error; return; }
+    S += c.npk.size();
+    P += c.mz.size();
+  }
+  R->spec_off.assign(S + 1, 0);
+  R->mz.reserve(P);
+  R->it.reserve(P);
+  size_t s = 0;
+  for (auto& c : chunks) {
+    for (size_t k = 0; k < c.npk.size(); ++k, ++s) R->spec_off[s + 1] = R->spec_off[s] + c.npk[k];
+    R->mz.insert(R->mz.end(), c.mz.begin(), c.mz.end());
+    R->it.insert(R->it.end(), c.it.begin(), c.it.end());
+    R->prec.insert(R->prec.end(), c.prec.begin(), c.prec.end());
+    R->charge.insert(R->charge.end(), c.charge.begin(), c.charge.end());
+    R->flags.insert(R->flags.end(), c.flags.begin(), c.flags.end());
+    if constexpr (std::is_same<ChunkT, GenChunk>::value) R->rt.insert(R->rt.end(), c.rt.begin(), c.rt.end());
+    R->titles += c.titles;
+  }
+  if (!with_rt) R->rt.assign(S, std::nan(""));
+}
+
+int default_threads(int threads) {
+  return threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+// Record index: where each spectrum record starts and ends, its title, peaks.
+struct Index {
+  std::vector<int64_t> begin, end, npk;
+  std::string titles, error;
+};
+
 }  // namespace
 
 extern "C" {
@@ -371,26 +582,7 @@ void* spx_mgf_parse(const char* path, int threads) {
   std::vector<std::thread> pool;
   for (int i = 0; i < nc; ++i) pool.emplace_back(parse_range, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
   for (auto& th : pool) th.join();
-  size_t S = 0, P = 0;
-  for (auto& c : chunks) {
-    if (!c.error.empty()) { R->error = c.error; return R; }
-    S += c.npk.size();
-    P += c.mz.size();
-  }
-  R->spec_off.resize(S + 1);
-  R->mz.reserve(P);
-  R->it.reserve(P);
-  R->spec_off[0] = 0;
-  size_t s = 0;
-  for (auto& c : chunks) {
-    for (size_t k = 0; k < c.npk.size(); ++k, ++s) R->spec_off[s + 1] = R->spec_off[s] + c.npk[k];
-    R->mz.insert(R->mz.end(), c.mz.begin(), c.mz.end());
-    R->it.insert(R->it.end(), c.it.begin(), c.it.end());
-    R->prec.insert(R->prec.end(), c.prec.begin(), c.prec.end());
-    R->charge.insert(R->charge.end(), c.charge.begin(), c.charge.end());
-    R->flags.insert(R->flags.end(), c.flags.begin(), c.flags.end());
-    R->titles += c.titles;
-  }
+  merge_chunks(chunks, R, false);
   return R;
 }
 
@@ -411,6 +603,162 @@ void spx_mgf_copy(void* h, int64_t* spec_off, double* mz, double* it, double* pr
 }
 const char* spx_mgf_titles(void* h) { return static_cast<Result*>(h)->titles.c_str(); }
 void spx_mgf_free(void* h) { delete static_cast<Result*>(h); }
+void spx_mgf_copy_rt(void* h, double* rt) {
+  Result* R = static_cast<Result*>(h);
+  std::copy(R->rt.begin(), R->rt.end(), rt);
+}
+
+// General MGF (pyteomics-shaped subset, see parse_range_general): same result
+// accessors as spx_mgf_parse, plus spx_mgf_copy_rt (NaN where absent); prec is
+// NaN without PEPMASS; flags bit0 PEPMASS, bit1 CHARGE, bit2 RTINSECONDS, bit3 TITLE.
+void* spx_mgf_parse_general(const char* path, int threads) {
+  Result* R = new Result();
+  std::string data;
+  if (!read_file(path, data, R->error)) return R;
+  const char* b = data.data();
+  const char* e = b + data.size();
+  int T = default_threads(threads);
+  if (data.size() < (1u << 20)) T = 1;
+  const std::vector<const char*> cuts = split_records(b, e, T, 1);
+  const int nc = (int)cuts.size() - 1;
+  std::vector<GenChunk> chunks((size_t)nc);
+  std::vector<std::thread> pool;
+  for (int i = 0; i < nc; ++i)
+    pool.emplace_back(parse_range_general, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
+  for (auto& th : pool) th.join();
+  merge_chunks(chunks, R, true);
+  return R;
+}
+
+// Record index of an MGF without parsing numbers (the sharded CLIs' planning
+// pass): record r = bytes [begin[r], end[r]) from its start line ("TITLE=" for
+// general == 0, binning.py's reader; "BEGIN IONS" for general == 1) to the next
+// record's start, its title (the TITLE= value, stripped) and its peak-line count.
+// Only records holding an END IONS line are listed (the ones a parser stores).
+void* spx_mgf_index(const char* path, int general) {
+  Index* X = new Index();
+  std::string data;
+  if (!read_file(path, data, X->error)) return X;
+  const char* b = data.data();
+  const char* e = b + data.size();
+  const char* p = b;
+  int64_t rb = -1, np = 0;
+  bool has_end = false;
+  std::string title;
+  auto close = [&](int64_t at) {
+    if (rb >= 0 && has_end) {
+      X->begin.push_back(rb);
+      X->end.push_back(at);
+      X->npk.push_back(np);
+      X->titles += title;
+      X->titles += '\n';
+    }
+  };
+  while (p < e) {
+    const char* ls = p;
+    const char* le = p;
+    while (le < e && *le != '\n' && *le != '\r') ++le;
+    p = le;
+    if (p < e) {
+      if (*p == '\r') { ++p; if (p < e && *p == '\n') ++p; }
+      else ++p;
+    }
+    if (record_start(ls, le, general)) {
+      close(ls - b);
+      rb = ls - b;
+      np = 0;
+      has_end = false;
+      title.clear();
+    }
+    const char *sb = ls, *se = le;
+    strip(sb, se);
+    if (rb >= 0 && !has_end && se - sb >= 6 && (general ? (std::tolower((unsigned char)sb[0]) == 't' && std::tolower((unsigned char)sb[1]) == 'i' &&
+                                    std::tolower((unsigned char)sb[2]) == 't' && std::tolower((unsigned char)sb[3]) == 'l' &&
+                                    std::tolower((unsigned char)sb[4]) == 'e' && sb[5] == '=')
+                                 : std::memcmp(ls, "TITLE=", 6) == 0)) {
+      const char *tb = (general ? sb : ls) + 6, *te = general ? se : le;
+      if (!general) strip(tb, te);
+      title.assign(tb, te);
+    } else if (se - sb == 8 && std::memcmp(sb, "END IONS", 8) == 0) {
+      has_end = true;
+    } else if (se > sb && ((*(general ? sb : ls) >= '0' && *(general ? sb : ls) <= '9') ||
+                           (general && (*sb == '+' || *sb == '-' || *sb == '.') && se - sb > 1 && sb[1] >= '0' &&
+                            sb[1] <= '9'))) {
+      ++np;
+    }
+  }
+  close(e - b);
+  return X;
+}
+
+const char* spx_mgf_index_error(void* h) {
+  Index* X = static_cast<Index*>(h);
+  return X->error.empty() ? nullptr : X->error.c_str();
+}
+int64_t spx_mgf_index_n(void* h) { return (int64_t)static_cast<Index*>(h)->begin.size(); }
+void spx_mgf_index_copy(void* h, int64_t* begin, int64_t* end, int64_t* npk) {
+  Index* X = static_cast<Index*>(h);
+  std::copy(X->begin.begin(), X->begin.end(), begin);
+  std::copy(X->end.begin(), X->end.end(), end);
+  std::copy(X->npk.begin(), X->npk.end(), npk);
+}
+const char* spx_mgf_index_titles(void* h) { return static_cast<Index*>(h)->titles.c_str(); }
+void spx_mgf_index_free(void* h) { delete static_cast<Index*>(h); }
+
+// Parse only the records [begin[r], end[r]) (any order: the result follows it),
+// with the binning (general == 0) or the general parser.  A rank of a sharded CLI
+// reads its own clusters' spectra this way and nothing else.
+void* spx_mgf_parse_ranges(const char* path, const int64_t* begin, const int64_t* end, int64_t n, int general,
+                           int threads) {
+  Result* R = new Result();
+  FILE* f = std::fopen(path, "rb");
+  if (!f) { R->error = std::string("cannot open ") + path; return R; }
+  // read the records into one buffer (in the requested order)
+  std::vector<int64_t> at((size_t)n + 1, 0);
+  for (int64_t r = 0; r < n; ++r) {
+    if (begin[r] < 0 || end[r] < begin[r]) { std::fclose(f); R->error = "bad record range"; return R; }
+    at[(size_t)r + 1] = at[(size_t)r] + (end[r] - begin[r]);
+  }
+  std::string data((size_t)at[(size_t)n], '\0');
+  for (int64_t r = 0; r < n && R->error.empty();) {
+    int64_t q = r + 1;  // coalesce records adjacent in the file into one read
+    while (q < n && begin[q] == end[q - 1]) ++q;
+    const int64_t len = end[q - 1] - begin[r];
+    if (len > 0 && (std::fseek(f, (long)begin[r], SEEK_SET) != 0 ||
+                    std::fread(&data[(size_t)at[(size_t)r]], 1, (size_t)len, f) != (size_t)len))
+      R->error = "short read";
+    r = q;
+  }
+  std::fclose(f);
+  if (!R->error.empty()) return R;
+  int T = default_threads(threads);
+  if (data.size() < (1u << 20)) T = 1;
+  T = (int)std::min<int64_t>(T, std::max<int64_t>(n, 1));
+  // thread t parses whole records [rs[t], rs[t+1])
+  std::vector<const char*> cuts{data.data()};
+  for (int t = 1; t < T; ++t) {
+    const int64_t r = n * t / T;
+    const char* q = data.data() + at[(size_t)r];
+    if (q > cuts.back()) cuts.push_back(q);
+  }
+  cuts.push_back(data.data() + data.size());
+  const int nc = (int)cuts.size() - 1;
+  std::vector<std::thread> pool;
+  if (general) {
+    std::vector<GenChunk> chunks((size_t)nc);
+    for (int i = 0; i < nc; ++i)
+      pool.emplace_back(parse_range_general, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
+    for (auto& th : pool) th.join();
+    merge_chunks(chunks, R, true);
+  } else {
+    std::vector<Chunk> chunks((size_t)nc);
+    for (int i = 0; i < nc; ++i) pool.emplace_back(parse_range, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
+    for (auto& th : pool) th.join();
+    merge_chunks(chunks, R, false);
+  }
+  if (R->error.empty() && (int64_t)R->prec.size() != n) R->error = "fallback: records and parsed spectra differ";
+  return R;
+}
 
 int64_t spx_mgf_format_binning(char* buf, int64_t cap, const char* cid, const char* charge_str, double prec,
                                const double* mz, const double* it, int64_t n, int skip_nan) {

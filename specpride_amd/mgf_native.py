@@ -1,4 +1,4 @@
-"""MGF ingest/emit for the bin-mean CLI path.
+"""MGF ingest/emit for the three CLIs.
 
 ``read_binning_mgf`` reproduces the reference's line parser
 (src/binning.py:122-167) and ``write_binning_mgf`` its f-string writer
@@ -40,8 +40,56 @@ def _native():
         L.spx_mgf_format_binning.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
                                              ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_int]
+        L.spx_mgf_parse_general.restype = ctypes.c_void_p
+        L.spx_mgf_parse_general.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        L.spx_mgf_copy_rt.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.spx_mgf_index.restype = ctypes.c_void_p
+        L.spx_mgf_index.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        L.spx_mgf_index_error.restype = ctypes.c_char_p
+        L.spx_mgf_index_error.argtypes = [ctypes.c_void_p]
+        L.spx_mgf_index_n.restype = ctypes.c_int64
+        L.spx_mgf_index_n.argtypes = [ctypes.c_void_p]
+        L.spx_mgf_index_copy.argtypes = [ctypes.c_void_p] * 4
+        L.spx_mgf_index_titles.restype = ctypes.c_char_p
+        L.spx_mgf_index_titles.argtypes = [ctypes.c_void_p]
+        L.spx_mgf_index_free.argtypes = [ctypes.c_void_p]
+        L.spx_mgf_parse_ranges.restype = ctypes.c_void_p
+        L.spx_mgf_parse_ranges.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                           ctypes.c_int, ctypes.c_int]
         _mgf = L
     return _mgf
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _split_titles(raw, n):
+    return raw.decode("utf-8", errors="surrogateescape").split("\n")[:n] if n else []
+
+
+def _take_result(L, h, general):
+    """Copy a parse handle's arrays out and free it (ValueError on an error/fallback)."""
+    try:
+        err = L.spx_mgf_error(h)
+        if err:
+            raise ValueError(err.decode(errors="replace"))
+        S, P = L.spx_mgf_n_spectra(h), L.spx_mgf_n_peaks(h)
+        spec_off = np.zeros(S + 1, np.int64)
+        mz, inten = np.empty(P), np.empty(P)
+        prec, rt = np.empty(S), np.empty(S)
+        charge = np.empty(S, np.int64)
+        flags = np.empty(S, np.int32)
+        L.spx_mgf_copy(h, _ptr(spec_off), _ptr(mz), _ptr(inten), _ptr(prec), _ptr(charge), _ptr(flags))
+        L.spx_mgf_copy_rt(h, _ptr(rt))
+        titles = _split_titles(L.spx_mgf_titles(h), S)
+    finally:
+        L.spx_mgf_free(h)
+    d = dict(spec_off=spec_off, mz=mz, inten=inten, prec_mz=prec, charge=charge,
+             has_prec=(flags & 1) != 0, has_charge=(flags & 2) != 0, titles=titles)
+    if general:
+        d.update(rt=rt, has_rt=(flags & 4) != 0, has_title=(flags & 8) != 0)
+    return d
 
 
 # ------------------------------------------------------------------ reading
@@ -74,24 +122,57 @@ def parse_native(path, threads: int = 0):
     L = _native()
     if L is None:
         return None
-    h = L.spx_mgf_parse(os.fsencode(path), int(threads))
+    return _take_result(L, L.spx_mgf_parse(os.fsencode(path), int(threads)), False)
+
+
+def parse_general(path, threads: int = 0):
+    """Native parse of a general (pyteomics-shaped) MGF -- the subset of
+    :func:`specpride_amd.mgf.iter_mgf` whose meaning is unambiguous -- into flat
+    arrays: dict(spec_off, mz, inten, prec_mz (NaN if absent), charge (0 if
+    absent), rt (NaN if absent), has_prec, has_charge, has_rt, has_title, titles).
+    None when the library is absent; ValueError("fallback: ...") outside the subset
+    (the caller then reads with iter_mgf, which behaves or raises as before)."""
+    L = _native()
+    if L is None:
+        return None
+    return _take_result(L, L.spx_mgf_parse_general(os.fsencode(path), int(threads)), True)
+
+
+def index(path, general: bool):
+    """Record index of an MGF without parsing any number: dict(begin, end, npk,
+    titles) -- record r is bytes [begin[r], end[r]) (from its TITLE= line for the
+    binning reader, from BEGIN IONS for the general one, to the next record's
+    start), npk its peak-line count.  Only records with an END IONS are listed.
+    None when the library is absent."""
+    L = _native()
+    if L is None:
+        return None
+    h = L.spx_mgf_index(os.fsencode(path), int(bool(general)))
     try:
-        err = L.spx_mgf_error(h)
+        err = L.spx_mgf_index_error(h)
         if err:
             raise ValueError(err.decode(errors="replace"))
-        S, P = L.spx_mgf_n_spectra(h), L.spx_mgf_n_peaks(h)
-        spec_off = np.zeros(S + 1, np.int64)
-        mz, inten = np.empty(P), np.empty(P)
-        prec = np.empty(S)
-        charge = np.empty(S, np.int64)
-        flags = np.empty(S, np.int32)
-        p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-        L.spx_mgf_copy(h, p(spec_off), p(mz), p(inten), p(prec), p(charge), p(flags))
-        titles = L.spx_mgf_titles(h).decode("utf-8", errors="surrogateescape").split("\n")[:S] if S else []
+        n = L.spx_mgf_index_n(h)
+        begin, end, npk = (np.empty(n, np.int64) for _ in range(3))
+        L.spx_mgf_index_copy(h, _ptr(begin), _ptr(end), _ptr(npk))
+        titles = _split_titles(L.spx_mgf_index_titles(h), n)
     finally:
-        L.spx_mgf_free(h)
-    return dict(spec_off=spec_off, mz=mz, inten=inten, prec_mz=prec, charge=charge,
-                has_prec=(flags & 1) != 0, has_charge=(flags & 2) != 0, titles=titles)
+        L.spx_mgf_index_free(h)
+    return dict(begin=begin, end=end, npk=npk, titles=titles)
+
+
+def parse_ranges(path, begin, end, general: bool, threads: int = 0):
+    """Parse only the records [begin[r], end[r]) of :func:`index` (result in the
+    given order) with the binning (general=False) or the general parser; the
+    same flat dict as :func:`parse_native` / :func:`parse_general`."""
+    L = _native()
+    if L is None:
+        raise RuntimeError(f"native MGF library missing ({MGF_LIB}); run __graft_entry__.build()")
+    begin = np.ascontiguousarray(begin, np.int64)
+    end = np.ascontiguousarray(end, np.int64)
+    h = L.spx_mgf_parse_ranges(os.fsencode(path), _ptr(begin), _ptr(end), len(begin), int(bool(general)),
+                               int(threads))
+    return _take_result(L, h, general)
 
 
 def read_binning_mgf(path):

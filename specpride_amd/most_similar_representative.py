@@ -73,27 +73,40 @@ def _first_runs(names):
     return runs
 
 
+def write_record(fh, title, pepmass, charge, rt, mz, inten):
+    """One output spectrum (fields that are None are omitted)."""
+    parts = ["BEGIN IONS\n"]
+    if title is not None:
+        parts.append(f"TITLE={title}\n")
+    if pepmass is not None:
+        parts.append(f"PEPMASS={float(pepmass)!r}\n")
+    if charge is not None:
+        parts.append(f"CHARGE={format_charge(charge)}\n")
+    if rt is not None:
+        parts.append(f"RTINSECONDS={float(rt)!r}\n")
+    parts.extend(f"{float(a)!r} {float(b)!r}\n" for a, b in zip(mz, inten))
+    parts.append("END IONS\n\n")
+    fh.write("".join(parts))
+
+
 def _write_spectra(spectra, path):
     with open(path, "w") as fh:
         for sp in spectra:
             p = sp["params"]
-            fh.write("BEGIN IONS\n")
-            if "title" in p:
-                fh.write(f"TITLE={p['title']}\n")
-            if "pepmass" in p:
-                fh.write(f"PEPMASS={float(p['pepmass'][0])!r}\n")
-            if "charge" in p and len(p["charge"]):
-                fh.write(f"CHARGE={format_charge(p['charge'])}\n")
-            if "rtinseconds" in p:
-                fh.write(f"RTINSECONDS={float(p['rtinseconds'])!r}\n")
-            fh.write("".join(f"{float(a)!r} {float(b)!r}\n" for a, b in zip(sp["m/z array"], sp["intensity array"])))
-            fh.write("END IONS\n\n")
+            ch = p.get("charge")
+            write_record(fh, p.get("title"), p["pepmass"][0] if "pepmass" in p else None,
+                         ch if ch is not None and len(ch) else None, p.get("rtinseconds"),
+                         sp["m/z array"], sp["intensity array"])
 
 
 def representatives(spectra, names):
     """Indices (into ``spectra``) of the representative of every cluster run."""
     runs = [(cl, m) for cl, m in _first_runs(names) if m]
     csr = SpectraCSR.from_clusters([[spectra[i] for i in members] for _cl, members in runs])
+    return _choose(csr, runs)
+
+
+def _choose(csr, runs):
     rep, _ = engine.medoid(engine.DeviceBatch.from_host(csr), TOLERANCE).to_host()
     if np.any(rep < 0):
         raise RuntimeError("medoid engine could not resolve a cluster (see DESIGN.md limits)")
@@ -101,6 +114,53 @@ def representatives(spectra, names):
     for c, (cl, members) in enumerate(runs):
         out.append((cl, members, members[int(rep[c] - csr.cluster_off[c])]))
     return out
+
+
+def _main_native(inputfile, outputfile):
+    """main() over the native parse: records straight into the CSR, the chosen
+    records written from the flat arrays.  False when the file is outside the
+    native subset or a record has no TITLE (the dict path then decides)."""
+    from . import ingest, mgf_native
+
+    try:
+        flat = mgf_native.parse_general(inputfile)
+    except ValueError:
+        return False
+    if flat is None or not flat["has_title"].all():
+        return False
+    titles = flat["titles"]
+    runs = [(cl, m) for cl, m in _first_runs([t.split(";")[0] for t in titles]) if m]
+    records = np.asarray([i for _cl, m in runs for i in m], np.int64)
+    csr = ingest.csr_from_flat(flat, [len(m) for _cl, m in runs], records)
+    so = flat["spec_off"]
+    chosen = []
+    for cl, members, best in _choose(csr, runs):
+        print(cl)
+        print(len(members))
+        chosen.append(best)
+    print(len(chosen))
+    with open(outputfile, "w") as fh:
+        for s in chosen:
+            write_record(fh, titles[s], flat["prec_mz"][s] if flat["has_prec"][s] else None,
+                         int(flat["charge"][s]) if flat["has_charge"][s] else None,
+                         flat["rt"][s] if flat["has_rt"][s] else None,
+                         flat["mz"][so[s]:so[s + 1]], flat["inten"][so[s]:so[s + 1]])
+    return True
+
+
+def _main_dicts(inputfile, outputfile):
+    from . import sharded_cli
+
+    if sharded_cli.launched_distributed():  # torchrun: rank-local ingest, one GPU per rank
+        sharded_cli.run_cli(sharded_cli.medoid, lambda: main_single(inputfile, outputfile), inputfile, outputfile)
+        return
+    main_single(inputfile, outputfile)
+
+
+def main_single(inputfile, outputfile):
+    """The single-process CLI body: native ingest, else the dict path."""
+    if not _main_native(inputfile, outputfile):
+        _main_dicts(inputfile, outputfile)
 
 
 def main(argv):
@@ -118,15 +178,18 @@ def main(argv):
             inputfile = arg
         elif opt in ("-o",):
             outputfile = arg
-    spectra = read_mgf(inputfile)
-    names = [s["params"]["title"].split(";")[0] for s in spectra]
-    chosen = []
-    for cl, members, best in representatives(spectra, names):
-        print(cl)
-        print(len(members))
-        chosen.append(spectra[best])
-    print(len(chosen))
-    _write_spectra(chosen, outputfile)
+    from . import sharded_cli
+
+    if sharded_cli.launched_distributed():  # torchrun: rank-local ingest, one GPU per rank
+        sharded_cli.run_cli(sharded_cli.medoid, lambda: main_single(inputfile, outputfile), inputfile, outputfile)
+        return
+    main_single(inputfile, outputfile)
+
+
+def main_single(inputfile, outputfile):
+    """The single-process CLI body: native ingest, else the dict path."""
+    if not _main_native(inputfile, outputfile):
+        _main_dicts(inputfile, outputfile)
 
 
 if __name__ == "__main__":

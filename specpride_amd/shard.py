@@ -30,9 +30,11 @@ CONSENSUS_KEYS = ("count", "status", "prec", "charge", "rt")
 
 
 # ------------------------------------------------------------------ planning
-def cluster_costs(csr: SpectraCSR, method: str) -> np.ndarray:
-    peaks = csr.cluster_peaks().astype(np.float64)
-    n = csr.cluster_sizes().astype(np.float64)
+def costs_from_sizes(sizes, peaks, method: str) -> np.ndarray:
+    """Per-cluster cost from spectrum and peak counts (what an MGF index gives
+    before any number is parsed)."""
+    peaks = np.asarray(peaks, np.float64)
+    n = np.asarray(sizes, np.float64)
     if method in ("bin_mean", "gap_average"):
         return peaks + 1.0
     if method == "medoid":
@@ -42,19 +44,50 @@ def cluster_costs(csr: SpectraCSR, method: str) -> np.ndarray:
     raise ValueError(f"unknown method {method!r}")
 
 
-def plan(csr: SpectraCSR, world: int, method: str = "bin_mean") -> list:
-    """LPT greedy assignment: rank -> ascending array of global cluster ids."""
+def cluster_costs(csr: SpectraCSR, method: str) -> np.ndarray:
+    return costs_from_sizes(csr.cluster_sizes(), csr.cluster_peaks(), method)
+
+
+def plan_costs(cost, world: int) -> list:
+    """LPT greedy assignment: rank -> ascending array of cluster ids."""
     if world < 1:
         raise ValueError("world must be >= 1")
-    cost = cluster_costs(csr, method)
+    cost = np.asarray(cost, np.float64)
     order = np.argsort(-cost, kind="stable")
     heap = [(0.0, r) for r in range(world)]
-    owner = np.empty(csr.n_clusters, np.int64)
+    owner = np.empty(len(cost), np.int64)
     for c in order:
         load, r = heapq.heappop(heap)
         owner[c] = r
         heapq.heappush(heap, (load + float(cost[c]), r))
     return [np.flatnonzero(owner == r) for r in range(world)]
+
+
+def plan(csr: SpectraCSR, world: int, method: str = "bin_mean") -> list:
+    """LPT greedy assignment of ``csr``'s clusters: rank -> ascending global cluster ids."""
+    return plan_costs(cluster_costs(csr, method), world)
+
+
+def world_rank(group=None):
+    """(world size, rank) of ``group``; (1, 0) without an initialised process group."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+def all_true(flag: bool, group=None) -> bool:
+    """Logical AND of ``flag`` over the ranks (a tensor on the backend's device)."""
+    import torch
+    import torch.distributed as dist
+
+    if world_rank(group)[0] == 1:
+        return bool(flag)
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
 
 
 # ---------------------------------------------------------------- collectives
@@ -65,7 +98,9 @@ def gatherv(tensors: list, root: int = 0, group=None) -> Optional[list]:
     import torch
     import torch.distributed as dist
 
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    world, rank = world_rank(group)
+    if world == 1:
+        return [list(tensors)]
     dev = tensors[0].device if tensors else torch.device("cpu")
     lens = torch.tensor([t.numel() for t in tensors], dtype=torch.int64, device=dev)
     all_lens = [torch.empty_like(lens) for _ in range(world)]
@@ -106,6 +141,7 @@ def _engine_consensus(method: str, params: dict, device):
 
 
 def _engine_medoid(params: dict, device):
+    """Per-rank medoid compute; ``member`` = representative index within its cluster."""
     def run(sub: SpectraCSR) -> dict:
         import torch
 
@@ -125,26 +161,18 @@ def _engine_medoid(params: dict, device):
 
 # ----------------------------------------------------------------- drivers
 def _my_shard(csr: SpectraCSR, method: str, group):
-    import torch.distributed as dist
-
-    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    world, rank = world_rank(group)
     parts = plan(csr, world, method)
     return parts, rank, csr.select(parts[rank])
 
 
-def consensus_sharded(csr: SpectraCSR, method: str = "bin_mean", params: Optional[dict] = None,
-                      device=None, group=None, compute: Optional[Callable] = None) -> Optional[dict]:
-    """Run ``engine.bin_mean`` / ``engine.gap_average`` over the ranks of ``group``;
-    rank 0 returns the host dict of :meth:`engine.PeaksResult.to_host` for the
-    WHOLE batch in global cluster order; other ranks return None.  Every rank
-    passes the same ``csr`` (e.g. each parsed the same file, or rank-local
-    ingest wrote the full index)."""
+def gather_consensus(res: dict, parts: list, n_clusters: int, group=None) -> Optional[dict]:
+    """Gather every rank's consensus result (``res``: count/status/prec/charge[/rt]
+    per local cluster + dense mz/inten) to rank 0 and reorder it into global
+    cluster order; rank 0 returns the host dict of :meth:`engine.PeaksResult.to_host`,
+    other ranks None."""
     import torch
 
-    params = params or {}
-    parts, rank, sub = _my_shard(csr, method, group)
-    run = compute or _engine_consensus(method, params, device)
-    res = run(sub)
     with_rt = "rt" in res
     keys = [k for k in CONSENSUS_KEYS if k in res]
     dev = res["count"].device
@@ -152,65 +180,77 @@ def consensus_sharded(csr: SpectraCSR, method: str = "bin_mean", params: Optiona
     got = gatherv(payload, group=group)
     if got is None:
         return None
-    C = csr.n_clusters
+    C = n_clusters
     full = {}
     for i, k in enumerate(keys):
         t0 = got[0][i]
         buf = torch.zeros(C, dtype=t0.dtype, device=dev)
         for r, ids in enumerate(parts):
             if len(ids):
-                buf[torch.from_numpy(ids).to(dev)] = got[r][i]
+                buf[torch.from_numpy(ids).to(dev)] = got[r][i].to(dev)
         full[k] = buf
-    count = full["count"].to(torch.int64)
-    out_off = torch.zeros(C + 1, dtype=torch.int64, device=dev)
-    if C:
-        torch.cumsum(count, 0, out=out_off[1:])
-    total = int(out_off[-1].item()) if C else 0
-    mz = torch.empty(total, dtype=torch.float64, device=dev)
-    inten = torch.empty(total, dtype=torch.float64, device=dev)
+    count = full["count"].to(torch.int64).cpu().numpy()
+    out_off = np.zeros(C + 1, np.int64)
+    np.cumsum(count, out=out_off[1:])
+    total = int(out_off[-1])
+    mz = np.empty(total, np.float64)
+    inten = np.empty(total, np.float64)
     for r, ids in enumerate(parts):
         if not len(ids):
             continue
         ids_np = np.asarray(ids, np.int64)
-        cnt = count[torch.from_numpy(ids_np).to(dev)].cpu().numpy()
-        dst = concat_ranges(out_off.cpu().numpy()[ids_np], cnt)
+        dst = concat_ranges(out_off[ids_np], count[ids_np])
         if len(dst):
-            dst_t = torch.from_numpy(dst).to(dev)
-            mz[dst_t] = got[r][len(keys)]
-            inten[dst_t] = got[r][len(keys) + 1]
-    out = dict(out_off=out_off.cpu().numpy(), out_mz=mz.cpu().numpy(), out_int=inten.cpu().numpy(),
-               status=full["status"].cpu().numpy(), prec=full["prec"].cpu().numpy(),
-               charge=full["charge"].cpu().numpy())
+            mz[dst] = got[r][len(keys)].cpu().numpy()
+            inten[dst] = got[r][len(keys) + 1].cpu().numpy()
+    out = dict(out_off=out_off, out_mz=mz, out_int=inten, status=full["status"].cpu().numpy(),
+               prec=full["prec"].cpu().numpy(), charge=full["charge"].cpu().numpy())
     if with_rt:
         out["rt"] = full["rt"].cpu().numpy()
     return out
 
 
-def medoid_sharded(csr: SpectraCSR, params: Optional[dict] = None, device=None, group=None,
-                   compute: Optional[Callable] = None):
-    """Sharded ``engine.medoid``: rank 0 returns ``(rep [C] global spectrum index,
-    totals [S] or None)`` in global order; other ranks return None."""
-    import torch
-
+def consensus_sharded(csr: SpectraCSR, method: str = "bin_mean", params: Optional[dict] = None,
+                      device=None, group=None, compute: Optional[Callable] = None) -> Optional[dict]:
+    """Run ``engine.bin_mean`` / ``engine.gap_average`` over the ranks of ``group``;
+    rank 0 returns the host dict of :meth:`engine.PeaksResult.to_host` for the
+    WHOLE batch in global cluster order; other ranks return None.  Every rank
+    passes the same ``csr`` (the CLIs' rank-local ingest instead packs only the
+    rank's own clusters and calls :func:`gather_consensus`)."""
     params = params or {}
-    parts, rank, sub = _my_shard(csr, "medoid", group)
-    run = compute or _engine_medoid(params, device)
-    res = run(sub)
+    parts, rank, sub = _my_shard(csr, method, group)
+    run = compute or _engine_consensus(method, params, device)
+    return gather_consensus(run(sub), parts, csr.n_clusters, group)
+
+
+def gather_medoid(res: dict, parts: list, cluster_off: np.ndarray, group=None):
+    """Rank 0: ``(rep [C] global spectrum index, totals [S] or None)`` from every
+    rank's ``member`` (index within its cluster, <0 = failure code) [+ totals]."""
     with_totals = "totals" in res
     payload = [res["member"].contiguous()] + ([res["totals"].contiguous()] if with_totals else [])
     got = gatherv(payload, group=group)
     if got is None:
         return None
-    C, S = csr.n_clusters, csr.n_spectra
+    C, S = len(cluster_off) - 1, int(cluster_off[-1])
     rep = np.full(C, -1, np.int64)
     totals = np.full(S, np.nan) if with_totals else None
     for r, ids in enumerate(parts):
         if not len(ids):
             continue
         member = got[r][0].cpu().numpy()
-        first = csr.cluster_off[ids]
+        first = cluster_off[ids]
         rep[ids] = np.where(member >= 0, first + member, member)
         if with_totals:
-            sizes = csr.cluster_off[ids + 1] - first
+            sizes = cluster_off[ids + 1] - first
             totals[concat_ranges(first, sizes)] = got[r][1].cpu().numpy()
     return rep, totals
+
+
+def medoid_sharded(csr: SpectraCSR, params: Optional[dict] = None, device=None, group=None,
+                   compute: Optional[Callable] = None):
+    """Sharded ``engine.medoid``: rank 0 returns ``(rep [C] global spectrum index,
+    totals [S] or None)`` in global order; other ranks return None."""
+    params = params or {}
+    parts, rank, sub = _my_shard(csr, "medoid", group)
+    run = compute or _engine_medoid(params, device)
+    return gather_medoid(run(sub), parts, csr.cluster_off, group)
