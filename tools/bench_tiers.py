@@ -2,9 +2,12 @@
 """The two host-inclusive measurement tiers of SURVEY.md §8(d) (never `value`):
 
 * tier 2 -- a packed host CSR (configs[1] law) -> H2D -> spx_bin_mean + spx_medoid
-  -> compaction + D2H of the consensus peaks and representatives;
-* tier 3 -- the binning.py CLI end to end (binning.py:250-302): MGF text in
-  (native parser) -> device -> MGF text out, on a synthetic clustered MGF.
+  -> compaction + D2H of the consensus peaks and representatives; and the same
+  for each method alone (bin-mean, gap-average, medoid);
+* tier 3 -- each CLI end to end on one synthetic clustered MGF: binning.py
+  (binning.py:250-302), average_spectrum_clustering.py --encodedclusters
+  (:168-210) and most_similar_representative.py (:22-115): MGF text in (native
+  parser straight to the CSR) -> device -> MGF text out.
 
 Prints one JSON line.  The reference's own CLI is timed on the same file shape by
 tools/time_reference_cli.py in the build container (the reference never reaches the
@@ -57,21 +60,40 @@ def main():
                     "clusters_per_s": round(csr.n_clusters / (t3 - t0), 1),
                     "h2d_GBs": round(16.0 * csr.n_peaks / (t1 - t0) / 1e9, 1),
                     "kept_peaks": int(r["out_off"][-1]), "reps_ok": bool((rep_idx >= 0).all())}
+    per = {}
+    for name, fn in (("bin_mean", lambda b: engine.bin_mean(b).to_host()),
+                     ("gap_average", lambda b: engine.gap_average(b).to_host()),
+                     ("medoid", lambda b: engine.medoid(b).to_host())):
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn(engine.DeviceBatch.from_host(csr))
+            t1 = time.perf_counter()
+        per[name] = {"s": round(t1 - t0, 4), "clusters_per_s": round(csr.n_clusters / (t1 - t0), 1)}
+    out["tier2_per_method"] = per
     # ---------------------------------------------------------------- tier 3
+    from specpride_amd import average_spectrum_clustering as asc
+    from specpride_amd import most_similar_representative as msr
+
     small = make_clusters_np(args.t3_clusters, seed=args.seed + 1)
+    clis = {"binning": lambda i, o: binning.main(["--mgf_file", i, "--out", o]),
+            "average_spectrum_clustering": lambda i, o: asc.main([i, o, "--encodedclusters"]),
+            "most_similar_representative": lambda i, o: msr.main(["-i", i, "-o", o])}
     with tempfile.TemporaryDirectory() as td:
         mgf_in, mgf_out = os.path.join(td, "in.mgf"), os.path.join(td, "out.mgf")
         write_csr_mgf(small, mgf_in)
         size = os.path.getsize(mgf_in)
-        with contextlib.redirect_stdout(io.StringIO()):
-            binning.main(["--mgf_file", mgf_in, "--out", mgf_out])  # warm
-            t0 = time.perf_counter()
-            binning.main(["--mgf_file", mgf_in, "--out", mgf_out])
-            t1 = time.perf_counter()
-        out["tier3"] = {"clusters": int(small.n_clusters), "peaks": int(small.n_peaks),
-                        "mgf_MB": round(size / 1e6, 1), "cli_s": round(t1 - t0, 3),
-                        "clusters_per_s": round(small.n_clusters / (t1 - t0), 1),
+        t3 = {"clusters": int(small.n_clusters), "spectra": int(small.n_spectra), "peaks": int(small.n_peaks),
+              "mgf_MB": round(size / 1e6, 1)}
+        for name, cli in clis.items():
+            with contextlib.redirect_stdout(io.StringIO()):
+                cli(mgf_in, mgf_out)  # warm
+                t0 = time.perf_counter()
+                cli(mgf_in, mgf_out)
+                t1 = time.perf_counter()
+            t3[name] = {"cli_s": round(t1 - t0, 3), "clusters_per_s": round(small.n_clusters / (t1 - t0), 1),
                         "out_MB": round(os.path.getsize(mgf_out) / 1e6, 2)}
+        out["tier3"] = t3
     print(json.dumps(out), flush=True)
 
 
