@@ -305,6 +305,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     }
   }
   if (early && pl && wid == 0 && n <= kWave) *early = precursor_summary_wave(*pl, (int)n, P);
+  SPX_STAMP(1);
   // f(m, it, tag) over every peak; kInten false passes it = 0 and loads none
   auto peaks_g = [&](auto inten_c, auto tagout_c, auto f) __attribute__((always_inline)) {
     constexpr bool kInten = decltype(inten_c)::value;
@@ -357,6 +358,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     imax = fmax(imax, fabs(it));
   });
   if (__syncthreads_or(bad)) return kNonFinite;
+  SPX_STAMP(2);
 
   if (n == 1) {
     // passthrough + dynamic-range filter on the raw spectrum (:88-98)
@@ -413,6 +415,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   __syncthreads();
   const int D = bitmap_prefix<GA_BLOCK>(S.bitmap, S.wprefix, (int)nw, tmp);
   if (D > S.dcap) return kDeferred;
+  SPX_STAMP(3);
   for (int d = tid; d < D; d += GA_BLOCK) {
     S.cnt[d] = 0u;
     S.gcnt[d] = 0u;
@@ -433,6 +436,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   });
   __syncthreads();
 
+  SPX_STAMP(4);
   // 4: gaps between consecutive occupied buckets -> emitted group per slot
   const int per = (D + GA_BLOCK - 1) / GA_BLOCK;
   const int d0 = tid * per;
@@ -463,6 +467,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
   __syncthreads();
 
+  SPX_STAMP(5);
   // 5: fixed-point group sums (exact integer adds: order-independent)
   int ex_m, ex_i;
   frexp(fmax(fabs(lo), fabs(hi)) * (double)N, &ex_m);
@@ -478,6 +483,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   });
   __syncthreads();
 
+  SPX_STAMP(6);
   // 6: min_fraction filter, dynamic range, ordered output
   const double min_len = P.min_fraction * (double)n;
   const int gper = (E + GA_BLOCK - 1) / GA_BLOCK;
@@ -546,6 +552,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
                                                                    int32_t* deferred, int32_t* n_deferred) {
   __shared__ GapSmem L;
   const int64_t c = blockIdx.x;
+  SPX_STAMP(0);
   GapState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.gcnt, L.kmin, L.kmax, GA_WMAX, GA_DCAP};
   const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
   PrecLanes pl{0, 0.0, 0.0};
@@ -560,6 +567,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
     return;
   }
   gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, nullptr, &early);
+  SPX_STAMP(7);
 }
 
 // Scratch slice of the deferred path: every array starts 256-B aligned (the

@@ -133,8 +133,8 @@ def make_clusters_torch(n_clusters: int, seed: int = 0, *, device="cuda", min_si
         jit = t + JITTER_SD * torch.randn(t.shape, generator=g, device=device, dtype=f64)
         keep = torch.rand(t.shape, generator=g, device=device) >= DROPOUT
         jit = torch.where(keep, jit, torch.full_like(jit, float("inf")))
-        n_noise = torch.distributions.Binomial(
-            n_template, torch.full((m,), NOISE_FRAC, device=device)).sample().to(torch.int64)
+        n_noise = torch.binomial(torch.full((m,), float(n_template), device=device),
+                                 torch.full((m,), NOISE_FRAC, device=device), generator=g).to(torch.int64)
         n_noise = torch.clamp(n_noise, max=n_noise_max)
         noise = MZ_LO + (MZ_HI - MZ_LO) * torch.rand((m, n_noise_max), generator=g, device=device, dtype=f64)
         col = torch.arange(n_noise_max, device=device)[None, :]

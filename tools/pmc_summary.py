@@ -44,6 +44,8 @@ def main():
     ap.add_argument("root")
     ap.add_argument("--json")
     ap.add_argument("--only", help="only counter files whose name starts with this prefix")
+    ap.add_argument("--peaks-from", help="log whose last JSON line holds the profiled batch's 'peaks' "
+                                         "(stored as '_peaks' so bench.py can rescale)")
     a = ap.parse_args()
     acc = load(a.root, a.only)
     traffic = {}
@@ -64,6 +66,11 @@ def main():
             traffic[k] = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
             print(f"   hbm_bytes (fetch+write)      {traffic[k]:16.0f}")
     if a.json:
+        if a.peaks_from:
+            for line in reversed(open(a.peaks_from).read().splitlines()):
+                if line.startswith("{"):
+                    traffic["_peaks"] = json.loads(line)["peaks"]
+                    break
         with open(a.json, "w") as fh:
             json.dump(traffic, fh, indent=1)
 

@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--which", default="bm,md,ga")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--stamps", action="store_true")
-    ap.add_argument("--stamps-kernel", default="bm", choices=["bm", "md"])
+    ap.add_argument("--stamps-kernel", default="bm", choices=["bm", "md", "ga"])
     ap.add_argument("--build-stamps", action="store_true")
     a = ap.parse_args()
     if a.build_stamps:
@@ -70,15 +70,28 @@ def main():
         torch.cuda.synchronize()
         return round(e0.elapsed_time(e1) / a.reps, 4)
 
+    def digest(*arrays):  # order-sensitive checksum of result arrays (variants must agree)
+        import hashlib
+
+        h = hashlib.sha1()
+        for x in arrays:
+            h.update(x.detach().cpu().numpy().tobytes())
+        return h.hexdigest()[:16]
+
     if "bm" in which:
         bm = engine.bin_mean(b)
         res["bin_mean_ms"] = timed(lambda: engine.bin_mean(b, out=bm))
+        off, mz, it = bm.compact()
+        res["bin_mean_digest"] = digest(off, mz, it, bm.status, bm.prec, bm.charge)
     if "md" in which:
         md = engine.medoid(b)
         res["medoid_ms"] = timed(lambda: engine.medoid(b, out=md, check=False))
+        res["medoid_digest"] = digest(md.rep)
     if "ga" in which:
         ga = engine.gap_average(b)
         res["gap_average_ms"] = timed(lambda: engine.gap_average(b, out=ga))
+        off, mz, it = ga.compact()
+        res["gap_average_digest"] = digest(off, mz, it, ga.status, ga.prec, ga.charge)
     if a.stamps:
         L = _lib.lib()
         L.spx_debug_stamps.argtypes = [ctypes.c_void_p]
@@ -86,6 +99,8 @@ def main():
         assert L.spx_debug_stamps(buf.data_ptr()) == 0
         if a.stamps_kernel == "bm":
             engine.bin_mean(b, out=bm)
+        elif a.stamps_kernel == "ga":
+            engine.gap_average(b, out=ga)
         else:
             engine.medoid(b, out=md, check=False)
         torch.cuda.synchronize()
