@@ -349,8 +349,8 @@ def headline(args, rank, world, local, out):
                    "gather": ("per-step RCCL gather of reps + compacted consensus peaks to rank 0, "
                               "overlapped with the next step" if world > 1 else "none (1 GPU: results stay in HBM)"),
                    "medoid_large_path": bool(large)},
-        "roofline": roofline("spx_bin_mean", "bin_mean_lds_kernel", bm_bytes, bm_ms,
-                             load_pmc_traffic("bin_mean_lds_kernel", batch)),
+        "roofline": roofline("spx_bin_mean", "bin_mean_reg_kernel", bm_bytes, bm_ms,
+                             load_pmc_traffic("bin_mean_reg_kernel", batch)),
         "roofline_medoid": roofline("spx_medoid", "medoid_reg_kernel", medoid_bytes(batch), md_ms,
                                     load_pmc_traffic("medoid_reg_kernel", batch)),
         "kernels": {"spx_bin_mean_ms": round(bm_ms, 4), "spx_medoid_ms": round(md_ms, 4)},
@@ -429,6 +429,37 @@ def config3(args, out):
     torch.cuda.empty_cache()
 
 
+def bin_mean_shapes(args, out):
+    """Bin-mean off the headline's shape: the configs[3]
+    skewed size law (clusters up to n = 5,000: the LDS and global-scratch paths)
+    and spectra longer than the register path's 252 peaks (600-peak templates)."""
+    import torch
+
+    from specpride_amd import engine
+    from specpride_amd.synthetic import make_clusters_torch
+
+    res = {}
+    for name, kw in (("skewed_config3", dict(n_clusters=20000, seed=4, skewed=True, forced_large=4, large_size=5000)),
+                     ("long_spectra_600", dict(n_clusters=20000, seed=6, n_template=600))):
+        t = make_clusters_torch(**kw)
+        batch = engine.DeviceBatch.from_device(t)
+        bm = engine.bin_mean(batch)
+        torch.cuda.synchronize()
+        st = bm.status.cpu().numpy()[:batch.n_clusters]
+        kept = int(bm.count[:batch.n_clusters].sum().item())
+        ms = time_launches(lambda: engine.bin_mean(batch, out=bm), 5, torch.cuda.current_stream())
+        sizes = np.diff(batch.host_cluster_off)
+        so = batch.host_spec_off
+        res[name] = {"clusters": batch.n_clusters, "spectra": batch.n_spectra, "peaks": batch.n_peaks,
+                     "max_n": int(sizes.max()), "max_spectrum_peaks": int(np.diff(so).max()),
+                     "ms": round(ms, 3), "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1),
+                     "all_ok": bool(np.all(st == 0)),
+                     "roofline": roofline("spx_bin_mean", "all bin-mean kernels", consensus_bytes(batch, kept), ms)}
+        del bm, batch, t
+        torch.cuda.empty_cache()
+    out["bin_mean_shapes"] = res
+
+
 def main():
     args = parse()
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
@@ -439,6 +470,7 @@ def main():
     headline(args, rank, world, local, out)
     if rank == 0 and world == 1 and not args.no_extras:
         config3(args, out)
+        bin_mean_shapes(args, out)
         if args.ns_clusters > 0:
             north_star(args, out)
     if rank == 0 and want_cpu:

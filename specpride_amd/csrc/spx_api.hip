@@ -66,6 +66,17 @@ constexpr int kFallbackBlocks = 64;
 
 int64_t fallback_grid(int64_t C) { return std::max<int64_t>(1, std::min<int64_t>(C, kFallbackBlocks)); }
 
+// Grid of a global-scratch fallback kernel whose workgroups each own a slice of
+// `slice_bytes`: as many as a 1 GiB scratch budget allows (>= 64, <= 4,096, <= C),
+// so a batch whose clusters all defer (long spectra, many distinct bins) still
+// fills the device.  Workspace sizing and the launch use the same value.
+int64_t fallback_grid_sized(int64_t C, int64_t slice_bytes) {
+  constexpr int64_t kBudget = int64_t(1) << 30;
+  int64_t g = slice_bytes > 0 ? kBudget / slice_bytes : kFallbackBlocks;
+  g = std::max<int64_t>(kFallbackBlocks, std::min<int64_t>(g, 4096));
+  return std::max<int64_t>(1, std::min<int64_t>(C, g));
+}
+
 int32_t bin_words(const spx_bin_params* p) {
   const double nb = std::trunc((p->maximum - p->minimum) / p->binsize) + 1.0;  // binning.py:172
   return (int32_t)((nb + 63.0) / 64.0);
@@ -80,6 +91,15 @@ int gap_wcap(const spx_gap_params* p, const spx_batch_info* info) {
   if (!std::isfinite(span)) span = 5000.0;
   const double w = std::ceil((span / (p->mz_accuracy * 0.5) + 3.0) / 64.0);
   return (int)std::min(w, (double)(1 << 24));
+}
+
+int64_t bin_mean_fallback_grid(int64_t C, const spx_bin_params* params, int64_t dcap) {
+  return fallback_grid_sized(C, spx::bin_mean_slice_bytes(bin_words(params), dcap));
+}
+
+int64_t gap_fallback_grid(int64_t C, const spx_gap_params* params, const spx_batch_info* info) {
+  const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
+  return fallback_grid_sized(C, spx::gap_slice_bytes(gap_wcap(params, info), (int)std::min<int64_t>(dcap, INT32_MAX)));
 }
 
 }  // namespace
@@ -102,7 +122,7 @@ size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* par
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   return 2 * align256(sizeof(int32_t) * 2) + 2 * align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
-         (size_t)fallback_grid(C) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
+         (size_t)bin_mean_fallback_grid(C, params, dcap) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
 int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info, spx_peaks_out* out,
@@ -144,7 +164,8 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),
                      dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
   if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)fallback_grid(C)), dim3(spx::BM_BLOCK), 0, s, V, P,
+  hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)bin_mean_fallback_grid(C, params, dcap)),
+                     dim3(spx::BM_BLOCK), 0, s, V, P,
                      O, prec_out, charge_out, status, def, n_def, scratch,
                      spx::bin_mean_slice_bytes(P.n_words, dcap), (int)std::min<int64_t>(dcap, INT32_MAX));
   return check_launch("bin_mean_global_kernel");
@@ -156,7 +177,8 @@ size_t spx_gap_average_workspace_size(const spx_csr* csr, const spx_gap_params* 
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   return align256(sizeof(int32_t)) * 2 + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
-         (size_t)fallback_grid(C) * (size_t)spx::gap_slice_bytes(gap_wcap(params, info), (int)std::min<int64_t>(dcap, INT32_MAX));
+         (size_t)gap_fallback_grid(C, params, info) *
+             (size_t)spx::gap_slice_bytes(gap_wcap(params, info), (int)std::min<int64_t>(dcap, INT32_MAX));
 }
 
 int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_batch_info* info, spx_peaks_out* out,
@@ -198,7 +220,8 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   spx::GapParams P2 = P;  // half-width buckets: no gap can hide inside one
   P2.bucket_w = params->mz_accuracy * 0.5;
   P2.inv_bucket_w = 1.0 / P2.bucket_w;
-  hipLaunchKernelGGL(spx::gap_average_global_kernel, dim3((unsigned)fallback_grid(C)), dim3(spx::GA_BLOCK), 0, s, V,
+  hipLaunchKernelGGL(spx::gap_average_global_kernel, dim3((unsigned)gap_fallback_grid(C, params, info)),
+                     dim3(spx::GA_BLOCK), 0, s, V,
                      P2, O, pepmass_out, charge_out, rt_out, status, def, n_def, scratch,
                      spx::gap_slice_bytes(wcap, dcap), wcap, dcap, unresolved);
   return check_launch("gap_average_global_kernel");
