@@ -72,6 +72,7 @@ struct GapSmem {
   uint64_t kmin[GA_DCAP];
   uint64_t kmax[GA_DCAP];
   int tmp[GA_BLOCK / kWave + 1];
+  int votes[2 * GA_NW];
   double red[GA_BLOCK / kWave * 3];
 };
 
@@ -277,9 +278,19 @@ __device__ __forceinline__ void gap_peaks(const CsrView& v, int64_t p0, int64_t 
 // --------------------------------------------------------------- the body
 template <class PrefixT>
 __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState<PrefixT>& S, int64_t c,
-                            const PeaksOut& out, int* tmp, double* red, const PrecLanes* pl = nullptr,
+                            const PeaksOut& out, int* tmp, double* red, int* votes, const PrecLanes* pl = nullptr,
                             PrecSummary* early = nullptr) {
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  // LDS state (the LDS kernel): barriers order LDS only, so register loads in
+  // flight survive them; global-scratch state (the fallback kernel): full barriers
+  constexpr bool kL = std::is_same<PrefixT, uint16_t>::value;
+  auto bar = [&]() __attribute__((always_inline)) {
+    if constexpr (kL) lds_barrier();
+    else __syncthreads();
+  };
+  auto any = [&](int pred, int parity) __attribute__((always_inline)) {
+    return block_any<GA_BLOCK, kL>(pred, votes, parity);
+  };
   const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1], n = s1 - s0;
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1], N = p1 - p0;
   if (n == 0) return kNoGap;
@@ -357,19 +368,19 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     hi = fmax(hi, m);
     imax = fmax(imax, fabs(it));
   });
-  if (__syncthreads_or(bad)) return kNonFinite;
+  if (any(bad, 0)) return kNonFinite;
   SPX_STAMP(2);
 
   if (n == 1) {
     // passthrough + dynamic-range filter on the raw spectrum (:88-98)
     double mx = -__longlong_as_double(0x7ff0000000000000ll);
     for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) mx = fmax(mx, v.inten[k]);
-    mx = wave_max(mx);
+    mx = wave_max_dpp(mx);
     if (lane == 0) red[wid] = mx;
-    __syncthreads();
+    bar();
     mx = red[0];
     for (int w = 1; w < GA_BLOCK / kWave; ++w) mx = fmax(mx, red[w]);
-    __syncthreads();
+    bar();
     if (N == 0) return kEmpty;
     const double thr = mx / P.dyn_range;
     int64_t base = 0;
@@ -377,7 +388,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       const int64_t k = k0 + tid;
       const int keep = k < p1 && v.inten[k] >= thr;
       int tot;
-      const int o = block_exclusive_scan<GA_BLOCK>(keep, tmp, tot);
+      const int o = block_exclusive_scan<GA_BLOCK, int, kL>(keep, tmp, tot);
       if (keep) {
         out.mz[p0 + base + o] = v.mz[k];
         out.inten[p0 + base + o] = v.inten[k];
@@ -389,11 +400,11 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   }
   if (N < 2) return kNoGap;  // np.diff of < 2 values is empty -> ind_list[0] IndexError
 
-  lo = wave_min_d(lo);
-  hi = -wave_min_d(-hi);
-  imax = -wave_min_d(-imax);
+  lo = wave_min_dpp(lo);
+  hi = wave_max_dpp(hi);
+  imax = wave_max_dpp(imax);
   if (lane == 0) { red[wid] = lo; red[GA_NW + wid] = hi; red[2 * GA_NW + wid] = imax; }
-  __syncthreads();
+  bar();
   for (int w = 0; w < GA_BLOCK / kWave; ++w) {
     lo = fmin(lo, red[w]);
     hi = fmax(hi, red[GA_NW + w]);
@@ -406,14 +417,14 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 
   // 2: occupied buckets
   for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
-  __syncthreads();
+  bar();
   peaks_m([&](double m, double, int32_t& tag) {
     const int64_t b = floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
     SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
     atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
   });
-  __syncthreads();
-  const int D = bitmap_prefix<GA_BLOCK>(S.bitmap, S.wprefix, (int)nw, tmp);
+  bar();
+  const int D = bitmap_prefix<GA_BLOCK, PrefixT, kL>(S.bitmap, S.wprefix, (int)nw, tmp);
   if (D > S.dcap) return kDeferred;
   SPX_STAMP(3);
   for (int d = tid; d < D; d += GA_BLOCK) {
@@ -422,7 +433,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     S.kmin[d] = ~0ull;
     S.kmax[d] = 0ull;
   }
-  __syncthreads();
+  bar();
 
   // 3: per-slot count and m/z extent
   peaks_m_tag([&](double m, double, int32_t& tag) {
@@ -434,7 +445,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)key);
     atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)key);
   });
-  __syncthreads();
+  bar();
 
   SPX_STAMP(4);
   // 4: gaps between consecutive occupied buckets -> emitted group per slot
@@ -448,9 +459,9 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     split |= (mx - mn) >= P.mz_accuracy;  // a gap could hide inside the bucket
     if (d + 1 < D) my_gaps += (f64_from_order_key(S.kmin[d + 1]) - mx) >= P.mz_accuracy;
   }
-  if (__syncthreads_or(split)) return kDeferred;
+  if (any(split, 1)) return kDeferred;
   int m_gaps;
-  int g = block_exclusive_scan<GA_BLOCK>(my_gaps, tmp, m_gaps);
+  int g = block_exclusive_scan<GA_BLOCK, int, kL>(my_gaps, tmp, m_gaps);
   if (m_gaps == 0) return kNoGap;
   const int E = m_gaps >= 2 ? m_gaps : 2;
   for (int j = 0; j < per; ++j) {
@@ -463,9 +474,9 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     S.cnt[d] = (uint32_t)eg;
     g += gap_after;
   }
-  __syncthreads();
+  bar();
   for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
-  __syncthreads();
+  bar();
 
   SPX_STAMP(5);
   // 5: fixed-point group sums (exact integer adds: order-independent)
@@ -481,38 +492,39 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), (unsigned long long)__double2ll_rn(ldexp(m, sc_m)));
     atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[eg]), (unsigned long long)__double2ll_rn(ldexp(it, sc_i)));
   });
-  __syncthreads();
+  bar();
 
   SPX_STAMP(6);
   // 6: min_fraction filter, dynamic range, ordered output
   const double min_len = P.min_fraction * (double)n;
   const int gper = (E + GA_BLOCK - 1) / GA_BLOCK;
   const int e0 = tid * gper;
+  auto isum = [&](int e) -> double { return ldexp((double)(int64_t)S.kmax[e], -sc_i); };
   double gmax = -__longlong_as_double(0x7ff0000000000000ll);
-  int any = 0;
+  int anyg = 0;
   for (int j = 0; j < gper; ++j) {
     const int e = e0 + j;
     if (e < E && (double)S.gcnt[e] >= min_len) {
-      gmax = fmax(gmax, ldexp((double)(int64_t)S.kmax[e], -sc_i) / (double)n);
-      any = 1;
+      gmax = fmax(gmax, isum(e) / (double)n);
+      anyg = 1;
     }
   }
-  gmax = wave_max(gmax);
+  gmax = wave_max_dpp(gmax);
   if (lane == 0) red[wid] = gmax;
-  if (!__syncthreads_or(any)) return kEmpty;
+  if (!any(anyg, 1)) return kEmpty;
   for (int w = 0; w < GA_BLOCK / kWave; ++w) gmax = fmax(gmax, red[w]);
   const double thr = gmax / P.dyn_range;
   int mine = 0;
   for (int j = 0; j < gper; ++j) {
     const int e = e0 + j;
-    if (e < E && (double)S.gcnt[e] >= min_len && ldexp((double)(int64_t)S.kmax[e], -sc_i) / (double)n >= thr) ++mine;
+    if (e < E && (double)S.gcnt[e] >= min_len && isum(e) / (double)n >= thr) ++mine;
   }
   int total;
-  int o = block_exclusive_scan<GA_BLOCK>(mine, tmp, total);
+  int o = block_exclusive_scan<GA_BLOCK, int, kL>(mine, tmp, total);
   for (int j = 0; j < gper; ++j) {
     const int e = e0 + j;
     if (e >= E || (double)S.gcnt[e] < min_len) continue;
-    const double iv = ldexp((double)(int64_t)S.kmax[e], -sc_i) / (double)n;
+    const double iv = isum(e) / (double)n;
     if (!(iv >= thr)) continue;
     SPX_GUARD(o < N, "gap out c=%ld o=%d N=%ld\n", (long)c, o, (long)N)
     out.mz[p0 + o] = ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e];
@@ -558,7 +570,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   PrecLanes pl{0, 0.0, 0.0};
   if (wave_id() == 0 && pn <= kWave) pl = prec_lanes(v, ps0, pn);
   PrecSummary early{0.0, 0.0, 0, kOk};
-  const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, &pl, &early);
+  const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, &early);
   if (st == kDeferred) {
     if (threadIdx.x == 0) {
       status[c] = kDeferred;
@@ -597,6 +609,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
                                                                       int64_t slice_bytes, int wcap, int dcap,
                                                                       int32_t* unresolved) {
   __shared__ int tmp[GA_BLOCK / kWave + 1];
+  __shared__ int votes[2 * GA_NW];
   __shared__ double red[GA_BLOCK / kWave * 3];
   char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
   const GapSliceLayout Lo = gap_slice_layout(wcap, dcap);
@@ -612,7 +625,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
   const int32_t nd = *n_deferred;
   for (int32_t i = blockIdx.x; i < nd; i += gridDim.x) {
     const int64_t c = deferred[i];
-    int32_t st = gap_body(v, P, S, c, out, tmp, red);
+    int32_t st = gap_body(v, P, S, c, out, tmp, red, votes);
     if (st == kDeferred) {
       // bucket range beyond the scratch, or a bucket spanning >= mz_accuracy:
       // reported, never approximated (the host re-runs it through the sort path)

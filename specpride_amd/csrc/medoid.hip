@@ -98,7 +98,7 @@ __device__ __forceinline__ int spectrum_of(const int32_t* soff, int n, int32_t k
 struct MedoidMeta {
   unsigned long long lo_key, hi_key;  // bin range, order-preserving keys (atomicMax; 0 = none)
   int64_t c, s0, blo;
-  int64_t l1_off, l2_off, rows_off, cmat_off, leaf_off, lsum_off, tot_off;  // arena byte offsets
+  int64_t l1_off, l2_off, rows_off, rowsT_off, cmat_off, leaf_off, lsum_off, tot_off;  // arena byte offsets
   int32_t n, nw1, B1, KW, L, tiles, units, ok;
 };
 
@@ -444,16 +444,31 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
 //   l2      (grid)   level-2 occupancy (one bit per occupied bin)
 //   plan2   (WG/cl)  level-2 prefix -> K compact columns; allocates rows, counts,
 //                    numpy's leaf segmentation and leaf sums
-//   scan    (1 WG)   Gram-tile and leaf-unit bases over the deferred clusters
+//   scan    (1 WG)   Gram-tile, leaf-unit and transpose-tile bases over the deferred clusters
 //   fill    (grid)   bit rows, 1 bit per occupied column (the OpenMS binary
 //                    ion table, compacted)
+//   xpose   (grid)   bit rows row-major -> word-major (64 x 64-word LDS tiles)
 //   gram    (MFMA)   c_ij = |B_i ∩ B_j|, v_mfma_i32_32x32x32_i8 on 0/1 bytes
+//                    expanded in registers, one 64 x 64 tile per wave
 //   leaves  (grid)   numpy pairwise-tree leaf sums of row i and column i
 //   combine (WG/cl)  the tree over the leaf sums -> totals, lowest-index argmin
 constexpr int MD_L1WORDS = 1024;  // level-1 bits: 65,536 blocks = 4.2M bins
 constexpr int MD_L2LDS = 4096;    // level-2 words staged in LDS (else global atomics)
-constexpr int MD_GT = 128;        // MFMA Gram tile (rows padded to a multiple)
-constexpr int MD_GROW = 80;       // LDS bytes per expanded row (64 + 16: conflict-free b128)
+constexpr int MD_GT = 128;        // rows padded to a multiple
+constexpr int MD_WT = 64;         // register Gram: one wave's 64-row output tile
+constexpr int MD_GR_NB = 2;  // 32-column MFMA blocks per wave tile (64 x 128 measured: no faster)
+constexpr int MD_WTN = 32 * MD_GR_NB;  // wave tile columns
+
+// Wave tiles of a cluster: 64-row blocks ti against MD_WTN-column blocks tj that
+// reach the upper triangle (tj * MD_WTN + MD_WTN - 1 >= ti * 64).
+__host__ __device__ __forceinline__ int md_gr_first_tj(int ti) { return (ti * MD_WT) / MD_WTN; }
+__host__ __device__ __forceinline__ int64_t md_gr_tiles(int n) {
+  const int T = (n + MD_WT - 1) / MD_WT, TN = (n + MD_WTN - 1) / MD_WTN;
+  int64_t t = 0;
+  for (int ti = 0; ti < T; ++ti) t += TN - md_gr_first_tj(ti);
+  return t;
+}
+
 constexpr int MD_GRIDX = 64;      // blocks per cluster in the grid-parallel passes
 
 __host__ __device__ __forceinline__ int64_t md_align(int64_t b) { return (b + 255) & ~int64_t(255); }
@@ -673,7 +688,8 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
     const int64_t leaf_b = md_align((5 * maxL + 1) * 4);        // starts, leaf nodes, program
     const int64_t lsum_b = md_align(2 * (2 * maxL) * (int64_t)n * 8);  // node values, row and column
     const int64_t tot_b = md_align((int64_t)n * 8);
-    if (tid == 0) base_sh = md_bump(bump, rows_b + cmat_b + leaf_b + lsum_b + tot_b, arena_bytes);
+    const int64_t rowsT_b = rows_b;  // the word-major copy the Gram kernel reads
+    if (tid == 0) base_sh = md_bump(bump, rows_b + rowsT_b + cmat_b + leaf_b + lsum_b + tot_b, arena_bytes);
     __syncthreads();
     const int64_t base = base_sh;
     if (base < 0) {
@@ -685,7 +701,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
       // numpy's recursion over [0, n) as a post-order program: every node gets
       // a value slot when it completes; leaves in order, internal nodes as
       // (left slot, right slot, out slot) with children before parents.
-      int32_t* start = reinterpret_cast<int32_t*>(arena + base + rows_b + cmat_b);  // [maxL + 1]
+      int32_t* start = reinterpret_cast<int32_t*>(arena + base + rows_b + rowsT_b + cmat_b);  // [maxL + 1]
       int32_t* lnode = start + (maxL + 1);                                           // [maxL]
       int32_t* prog = lnode + maxL;                                                  // [3 * maxL]
       int nl = 0, nq = 0, nid = 0, ret = 0;
@@ -725,11 +741,12 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
       M->KW = KW;
       M->L = nl;
       M->rows_off = base;
-      M->cmat_off = base + rows_b;
-      M->leaf_off = base + rows_b + cmat_b;
-      M->lsum_off = base + rows_b + cmat_b + leaf_b;
-      M->tot_off = base + rows_b + cmat_b + leaf_b + lsum_b;
-      M->tiles = T * (T + 1) / 2;
+      M->rowsT_off = base + rows_b;
+      M->cmat_off = base + rows_b + rowsT_b;
+      M->leaf_off = M->cmat_off + cmat_b;
+      M->lsum_off = M->leaf_off + leaf_b;
+      M->tot_off = M->lsum_off + lsum_b;
+      M->tiles = md_gr_tiles(n);
       M->units = ((n + MD_BLOCK - 1) / MD_BLOCK) * nl;
       M->ok = 1;
     }
@@ -738,12 +755,16 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
 }
 
 // Exclusive scans of Gram tiles and leaf units over the deferred clusters (one workgroup).
+__device__ __forceinline__ int64_t md_xpose_tiles(const MedoidMeta& M) {  // 64 x 64-word transpose tiles
+  return (int64_t)((M.n + MD_GT - 1) / MD_GT * MD_GT / 64) * ((M.KW + 63) / 64);
+}
+
 __global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
                                                                int64_t* tile_base, int64_t* unit_base,
-                                                               int64_t* chunk_base) {
+                                                               int64_t* chunk_base, int64_t* xpose_base) {
   __shared__ int64_t tmp[MD_BLOCK / kWave + 1];
   const int32_t nd = *n_deferred;
-  int64_t ct = 0, cu = 0, cc = 0;
+  int64_t ct = 0, cu = 0, cc = 0, cx = 0;
   for (int32_t i0 = 0; i0 < nd; i0 += MD_BLOCK) {
     const int32_t i = i0 + threadIdx.x;
     const bool ok = i < nd && meta[i].ok;
@@ -758,8 +779,11 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta*
         block_exclusive_scan<MD_BLOCK>(ok ? (int64_t)((meta[i].n + MD_BLOCK - 1) / MD_BLOCK) : 0, tmp, tot);
     if (i < nd) chunk_base[i] = cc + ec;
     cc += tot;
+    const int64_t ex = block_exclusive_scan<MD_BLOCK>(ok ? md_xpose_tiles(meta[i]) : int64_t(0), tmp, tot);
+    if (i < nd) xpose_base[i] = cx + ex;
+    cx += tot;
   }
-  if (threadIdx.x == 0) { tile_base[nd] = ct; unit_base[nd] = cu; chunk_base[nd] = cc; }
+  if (threadIdx.x == 0) { tile_base[nd] = ct; unit_base[nd] = cu; chunk_base[nd] = cc; xpose_base[nd] = cx; }
 }
 
 // which deferred cluster owns work item t (base[lo] <= t < base[lo + 1], skipping empties)
@@ -805,112 +829,119 @@ typedef int md_i32x16 __attribute__((ext_vector_type(16)));
 // 64 bins (one u64 row word) -> 64 bytes of 0/1 in 4 x 16 B.  Byte p of dword
 // g (g < 8: low word) holds bin g + 8p -- a fixed permutation of the k axis,
 // identical for the A and B operands, so the dot products are unchanged.
-__device__ __forceinline__ void md_expand_store(unsigned long long w, char* dst) {
-  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-  md_i32x4 out[4];
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    out[g >> 2][g & 3] = (int)((lo >> g) & 0x01010101u);
-    out[2 + (g >> 2)][g & 3] = (int)((hi >> g) & 0x01010101u);
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) *reinterpret_cast<md_i32x4*>(dst + 16 * q) = out[q];
-}
+constexpr int MD_GR_PF = 4;  // words in flight per lane
 
-// c_ij for one 128x128 upper tile (ti <= tj) per iteration, grid-stride over
-// all tiles of all deferred clusters.  4 waves in 2x2, each 64x64 = 2x2 MFMA
-// 32x32 tiles (int32 accumulators, exact).  Thread t streams one row (t < 128:
-// A row t, else B row t-128) through an 8-word register ring (the next 64-byte
-// line is in flight for 8 k-steps), expands one word (64 bins) per k-step into
-// LDS (double-buffered; LDS-only barrier, so the ring is never drained) and
-// each lane reads 16 B per operand per 32-k half (ds_read_b128) for the MFMAs.
-__global__ __launch_bounds__(MD_BLOCK) void medoid_gram_mfma_kernel(const MedoidMeta* meta,
-                                                                    const int32_t* n_deferred,
-                                                                    const int64_t* tile_base, char* arena) {
-  __shared__ __attribute__((aligned(16))) char st[2][2 * MD_GT * MD_GROW];  // [buf][A rows | B rows]
-  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const int wm = wv >> 1, wn = wv & 1;
+// Bit rows, row-major [npad][KW] -> word-major [KW][npad] (64 x 64-word tiles
+// through LDS: both sides coalesced), for the register Gram's loads.
+__global__ __launch_bounds__(MD_BLOCK) void medoid_transpose_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
+                                                                    const int64_t* xpose_base, char* arena) {
+  __shared__ unsigned long long tile[64][65];
+  const int tid = threadIdx.x, x = tid & 63, y0 = tid >> 6;
+  const int32_t nd = *n_deferred;
+  const int64_t total = xpose_base[nd];
+  for (int64_t g = blockIdx.x; g < total; g += gridDim.x) {  // every tile of every cluster, flat
+    const int o = md_owner(xpose_base, nd, g);
+    const MedoidMeta M = meta[o];
+    const int npad = (M.n + MD_GT - 1) / MD_GT * MD_GT, KW = M.KW;
+    const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(arena + M.rows_off);
+    unsigned long long* rowsT = reinterpret_cast<unsigned long long*>(arena + M.rowsT_off);
+    const int tw = (KW + 63) / 64;
+    {
+      const int t = (int)(g - xpose_base[o]);
+      const int r0 = (t / tw) * 64, w0 = (t % tw) * 64;
+      for (int y = y0; y < 64; y += MD_BLOCK / 64)
+        tile[y][x] = w0 + x < KW ? rows[(int64_t)(r0 + y) * KW + w0 + x] : 0ull;
+      __syncthreads();
+      for (int y = y0; y < 64; y += MD_BLOCK / 64)
+        if (w0 + y < KW) rowsT[(int64_t)(w0 + y) * npad + r0 + x] = tile[x][y];
+      __syncthreads();
+    }
+  }
+}
+__global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
+                                                                   const int64_t* tile_base, char* arena) {
+  const int lane = lane_id();
   const int fr = lane & 31, fh = lane >> 5;
   const int32_t nd = *n_deferred;
   const int64_t total = tile_base[nd];
-  for (int64_t t = blockIdx.x; t < total; t += gridDim.x) {
+  const int64_t wstride = (int64_t)gridDim.x * (MD_BLOCK / kWave);
+  for (int64_t t = (int64_t)blockIdx.x * (MD_BLOCK / kWave) + wave_id(); t < total; t += wstride) {
     const int o = md_owner(tile_base, nd, t);
     const MedoidMeta M = meta[o];
     int64_t r = t - tile_base[o];
-    const int T = (M.n + MD_GT - 1) / MD_GT;
+    const int TN = (M.n + MD_WTN - 1) / MD_WTN;
     int ti = 0;
-    while (r >= T - ti) { r -= T - ti; ++ti; }
-    const int tj = ti + (int)r;
-    const int KW = M.KW;  // multiple of 8
-    const int srow = tid < MD_GT ? ti * MD_GT + tid : tj * MD_GT + (tid - MD_GT);
-    const ulonglong2* src = reinterpret_cast<const ulonglong2*>(
-        reinterpret_cast<const unsigned long long*>(arena + M.rows_off) + (int64_t)srow * KW);
-    char* mine[2] = {st[0] + tid * MD_GROW, st[1] + tid * MD_GROW};
+    while (r >= TN - md_gr_first_tj(ti)) { r -= TN - md_gr_first_tj(ti); ++ti; }
+    const int tj = md_gr_first_tj(ti) + (int)r;
+    const int KW = M.KW;
+    const int64_t npad = (int64_t)((M.n + MD_GT - 1) / MD_GT) * MD_GT;
+    const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(arena + M.rowsT_off);
+    // rows this lane loads: A blocks 0/1 (64-row tile), B blocks 0..NB-1 (zero past npad)
+    const unsigned long long* pa = rows + ti * MD_WT + fr;
+    const unsigned long long* pb = rows + (int64_t)tj * MD_WTN + fr;
+    bool bok[MD_GR_NB];
+#pragma unroll
+    for (int b = 0; b < MD_GR_NB; ++b) bok[b] = (int64_t)tj * MD_WTN + b * 32 < npad;
 
-    md_i32x16 acc[2][2];
+    md_i32x16 acc[2][MD_GR_NB];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < MD_GR_NB; ++b)
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[a][b][q] = 0;
 
-    ulonglong2 cur[4], nxt[4];
+    constexpr int NR = 2 + MD_GR_NB;  // rows per lane
+    unsigned long long ring[MD_GR_PF][NR];
+    auto load = [&](int w, unsigned long long* dst) __attribute__((always_inline)) {
+      const int64_t wo = (int64_t)(w < KW ? w : 0) * npad;  // unconditional (clamped)
+      dst[0] = pa[wo];
+      dst[1] = pa[wo + 32];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) cur[q] = src[q];
-    // the ring's first line fully landed: keeps the waitcnt pass from merging
-    // this tile's prologue loads with the in-loop prefetch at the loop header
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    md_expand_store(cur[0].x, mine[0]);
-    lds_barrier();
-    for (int kc = 0; kc < KW; kc += 8) {
-      const bool more = kc + 8 < KW;
-      if (more) {
+      for (int b = 0; b < MD_GR_NB; ++b) dst[2 + b] = pb[wo + (bok[b] ? b * 32 : 0)];
+    };
 #pragma unroll
-        for (int q = 0; q < 4; ++q) nxt[q] = src[(kc + 8) / 2 + q];
-      }
+    for (int q = 0; q < MD_GR_PF; ++q) load(q, ring[q]);
+    // one fragment: 16 bytes of the 32-bin half c, dwords 4h..4h+3
+    auto frag = [&](uint32_t c) __attribute__((always_inline)) {
+      md_i32x4 f;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int buf = u & 1;  // kc is a multiple of 8: (kc + u) & 1 == u & 1
-        const char* A = st[buf] + (wm * 64) * MD_GROW;
-        const char* B = st[buf] + (MD_GT + wn * 64) * MD_GROW;
+      for (int g = 0; g < 4; ++g) f[g] = (int)((c >> (4 * fh + g)) & 0x01010101u);
+      return f;
+    };
+    for (int w0 = 0; w0 < KW; w0 += MD_GR_PF) {  // KW is a multiple of 8
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          md_i32x4 fa[2], fb[2];
+      for (int q = 0; q < MD_GR_PF; ++q) {
+        unsigned long long cur[NR];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) cur[k] = ring[q][k];
+        load(w0 + q + MD_GR_PF, ring[q]);
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          md_i32x4 fa[2], fb[MD_GR_NB];
+#pragma unroll
+          for (int a = 0; a < 2; ++a) fa[a] = frag((uint32_t)(cur[a] >> (32 * hf)));
+#pragma unroll
+          for (int b = 0; b < MD_GR_NB; ++b) fb[b] = frag((uint32_t)(cur[2 + b] >> (32 * hf)));
 #pragma unroll
           for (int a = 0; a < 2; ++a)
-            fa[a] = *reinterpret_cast<const md_i32x4*>(A + (a * 32 + fr) * MD_GROW + 32 * h + 16 * fh);
 #pragma unroll
-          for (int b = 0; b < 2; ++b)
-            fb[b] = *reinterpret_cast<const md_i32x4*>(B + (b * 32 + fr) * MD_GROW + 32 * h + 16 * fh);
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
+            for (int b = 0; b < MD_GR_NB; ++b)
               acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
         }
-        if (u < 7) {
-          const unsigned long long w = (u + 1) & 1 ? cur[(u + 1) >> 1].y : cur[(u + 1) >> 1].x;
-          md_expand_store(w, mine[buf ^ 1]);
-        } else if (more) {
-          md_expand_store(nxt[0].x, mine[buf ^ 1]);
-        }
-        lds_barrier();
       }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
     }
     // C/D layout (32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
     uint32_t* cmat = reinterpret_cast<uint32_t*>(arena + M.cmat_off);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < MD_GR_NB; ++b)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int i = ti * MD_GT + wm * 64 + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
-          const int j = tj * MD_GT + wn * 64 + b * 32 + fr;
-          if (i < M.n && j < M.n) {
+          const int i = ti * MD_WT + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
+          const int j = tj * MD_WTN + b * 32 + fr;
+          if (i < M.n && j < M.n && i <= j) {
             const uint32_t cnt = (uint32_t)acc[a][b][q];
             cmat[(int64_t)i * M.n + j] = cnt;
             cmat[(int64_t)j * M.n + i] = cnt;
@@ -919,9 +950,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_gram_mfma_kernel(const Medoid
   }
 }
 
-// Both pairwise leaf sums of thread i over j in [lo, lo + m) (m <= 128): row i
-// takes d(i, j) for j >= i, column i takes d(j, i) for j <= i (the reference's
-// upper-triangular matrix, most_similar_representative.py:91-100).
 template <class F>
 __device__ __forceinline__ void dual_leaf_at(const F& f, int lo, int m, int i, double& row, double& col) {
   if (m < 8) {

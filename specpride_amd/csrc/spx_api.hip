@@ -238,7 +238,8 @@ size_t medoid_cluster_bytes(int64_t n, int64_t p) {
   const int64_t T = (n + spx::MD_GT - 1) / spx::MD_GT;
   const int64_t B1 = std::min<int64_t>(K, 64 * (int64_t)spx::MD_L1WORDS);
   const int64_t L = spx::md_max_leaves(n);
-  return (size_t)(spx::md_l1_bytes() + spx::md_align(B1 * 12 + 8) + spx::md_align(T * spx::MD_GT * KW * 8) +
+  return (size_t)(spx::md_l1_bytes() + spx::md_align(B1 * 12 + 8) +
+                  2 * spx::md_align(T * spx::MD_GT * KW * 8) +
                   spx::md_align(n * n * 4) + spx::md_align((5 * L + 1) * 4) + spx::md_align(2 * (2 * L) * n * 8) +
                   spx::md_align(n * 8));
 }
@@ -253,7 +254,7 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
   if (C < 0 || (C > 0 && (!hco || !hso)) || n_extra < 0 || (n_extra > 0 && !extra)) return 0;
   const size_t Cm = (size_t)std::max<int64_t>(C, 1);
   size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(sizeof(int32_t) * Cm) +
-                 align256(sizeof(spx::MedoidMeta) * Cm) + 3 * align256(sizeof(int64_t) * (Cm + 1));
+                 align256(sizeof(spx::MedoidMeta) * Cm) + 4 * align256(sizeof(int64_t) * (Cm + 1));
   size_t arena = 0, margin = 0;
   for (int64_t c = 0; c < C; ++c) {
     const int64_t n = hco[c + 1] - hco[c];
@@ -295,6 +296,7 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   int64_t* tile_base = w.take<int64_t>((size_t)C + 1);
   int64_t* unit_base = w.take<int64_t>((size_t)C + 1);
   int64_t* chunk_base = w.take<int64_t>((size_t)C + 1);
+  int64_t* xpose_base = w.take<int64_t>((size_t)C + 1);
   if (w.used >= workspace_bytes) return fail(SPX_ENOSPACE, "spx_medoid: workspace too small");
   char* arena = w.base + w.used;
   const int64_t arena_bytes = (int64_t)(workspace_bytes - w.used);
@@ -319,12 +321,15 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   if (int rc = check_launch("medoid_l2_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_plan2_kernel, dim3(g), blk, 0, s, n_def, meta, arena, bump, arena_bytes, rep);
   if (int rc = check_launch("medoid_plan2_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_scan_kernel, dim3(1), blk, 0, s, meta, n_def, tile_base, unit_base, chunk_base);
+  hipLaunchKernelGGL(spx::medoid_scan_kernel, dim3(1), blk, 0, s, meta, n_def, tile_base, unit_base, chunk_base,
+                     xpose_base);
   if (int rc = check_launch("medoid_scan_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_fill_kernel, grid2, blk, 0, s, V, P, meta, n_def, arena);
   if (int rc = check_launch("medoid_fill_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_gram_mfma_kernel, dim3(2048), blk, 0, s, meta, n_def, tile_base, arena);
-  if (int rc = check_launch("medoid_gram_mfma_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_transpose_kernel, dim3(4096), blk, 0, s, meta, n_def, xpose_base, arena);
+  if (int rc = check_launch("medoid_transpose_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_gram_reg_kernel, dim3(2048), blk, 0, s, meta, n_def, tile_base, arena);
+  if (int rc = check_launch("medoid_gram_reg_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_leaves_kernel, dim3(4096), blk, 0, s, V, meta, n_def, unit_base, arena);
   if (int rc = check_launch("medoid_leaves_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_combine_kernel, dim3(1024), blk, 0, s, meta, n_def, chunk_base, arena, totals);

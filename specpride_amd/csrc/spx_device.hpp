@@ -8,6 +8,8 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 
 #ifdef SPX_DEBUG
@@ -90,14 +92,53 @@ __device__ __forceinline__ int32_t wave_next(int32_t x, int32_t old) {
 }
 __device__ __forceinline__ int wave_id() { return threadIdx.x / kWave; }
 
+// ---- DPP wave reductions / scans (no LDS round trip, unlike __shfl's ds_bpermute).
+// GFX9 DPP controls: row_shr:n = 0x110 + n, row_bcast:15 = 0x142, row_bcast:31 = 0x143.
+// Lanes whose DPP source is outside the row (or whose row is masked off) get `old`
+// (the identity), so each step is x = op(x, shifted) (Hillis-Steele).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROWMASK, 0xF, false);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double old, double x) {
+  const uint64_t o = (uint64_t)__double_as_longlong(old), v = (uint64_t)__double_as_longlong(x);
+  const uint32_t lo = dpp_u32<CTRL, ROWMASK>((uint32_t)o, (uint32_t)v);
+  const uint32_t hi = dpp_u32<CTRL, ROWMASK>((uint32_t)(o >> 32), (uint32_t)(v >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// inclusive scan over the wave (lane 63 holds the total)
+template <class T, class Op>
+__device__ __forceinline__ T wave_scan_dpp(T x, T ident, Op op) {
+  auto step = [&](auto ctrl_c, auto mask_c) __attribute__((always_inline)) {
+    constexpr int C = decltype(ctrl_c)::value, M = decltype(mask_c)::value;
+    if constexpr (sizeof(T) == 8) {
+      x = op(x, dpp_f64<C, M>(ident, x));
+    } else {
+      x = op(x, (T)dpp_u32<C, M>((uint32_t)ident, (uint32_t)x));
+    }
+  };
+  step(std::integral_constant<int, 0x111>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x112>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x114>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x118>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xA>{});
+  step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xC>{});
+  return x;
+}
+
 template <class T>
 __device__ __forceinline__ T wave_inclusive_sum(T x) {
+  if constexpr (std::is_integral<T>::value && sizeof(T) == 4) {
+    return wave_scan_dpp(x, T(0), [](T a, T b) { return a + b; });  // DPP: no LDS round trips
+  } else {
 #pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    T y = __shfl_up(x, o, kWave);
-    if (lane_id() >= o) x += y;
+    for (int o = 1; o < kWave; o <<= 1) {
+      T y = __shfl_up(x, o, kWave);
+      if (lane_id() >= o) x += y;
+    }
+    return x;
   }
-  return x;
 }
 
 template <class T>
@@ -130,6 +171,17 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
 }
 __device__ __forceinline__ double readlane_f64(double x, int l) {
   return __longlong_as_double(readlane64(__double_as_longlong(x), l));
+}
+
+// wave-wide min (fmin: NaN-ignoring) / max (NaN-propagating, like numpy max),
+// broadcast to every lane; DPP, not ds_bpermute
+__device__ __forceinline__ double wave_min_dpp(double x) {
+  return readlane_f64(wave_scan_dpp(x, __longlong_as_double(0x7ff0000000000000ll),
+                                    [](double a, double b) { return fmin(a, b); }), kWave - 1);
+}
+__device__ __forceinline__ double wave_max_dpp(double x) {
+  return readlane_f64(wave_scan_dpp(x, -__longlong_as_double(0x7ff0000000000000ll),
+                                    [](double a, double b) { return (b > a || (b != b)) ? b : a; }), kWave - 1);
 }
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is a release/acquire

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--large", type=int, default=5000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--seed", type=int, default=4)
-    ap.add_argument("--check", action="store_true", help="compare the large clusters with the C oracle")
+    ap.add_argument("--check", action="store_true", help="with totals, and print a digest of reps + totals")
     args = ap.parse_args()
     import torch
 
@@ -62,22 +62,12 @@ def main():
            "large_clusters": int(len(big)), "max_n": int(sizes.max()),
            "spectra_in_large": int(sizes[big].sum()), "medoid_ms": round(ms, 3),
            "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1), "gram_ops": gram_ops}
-    if args.check:
-        from oracle import c_oracle
-        from specpride_amd.csr import SpectraCSR
+    if args.check:  # result digest: variants must agree (oracle parity: tests/test_gpu_configs.py)
+        import hashlib
 
-        csr = SpectraCSR.from_device(t)
-        order = np.argsort(-sizes)[:8]
-        sub = csr.select(order)
-        t0 = time.perf_counter()
-        want_rep, want_tot = c_oracle.medoid(sub, with_totals=True)
-        got_tot = md.totals.cpu().numpy()
-        got_rep = rep[order] - batch.host_cluster_off[order]
-        ok_rep = bool(np.array_equal(got_rep, want_rep - sub.cluster_off[:-1]))
-        sel = np.concatenate([np.arange(batch.host_cluster_off[c], batch.host_cluster_off[c + 1]) for c in order])
-        ok_tot = bool(np.array_equal(got_tot[sel], want_tot))
-        out.update(check_clusters=[int(sizes[c]) for c in order], check_rep=ok_rep, check_totals=ok_tot,
-                   oracle_s=round(time.perf_counter() - t0, 2))
+        h = hashlib.sha1(md.rep.cpu().numpy().tobytes())
+        h.update(md.totals.cpu().numpy().tobytes())
+        out["digest"] = h.hexdigest()[:16]
     print(json.dumps(out), flush=True)
 
 
