@@ -127,10 +127,14 @@ __device__ __forceinline__ T wave_scan_dpp(T x, T ident, Op op) {
   return x;
 }
 
-template <class T>
+// Inclusive wave scan: DPP for 32-bit integers (kDpp), else ds_bpermute shuffles.
+// The register bin-mean kernel measured 1% faster with the shuffle form (its
+// LDS round trips overlap the surrounding VALU work), the others 2-3% faster
+// with DPP (A/B, tools/gpu/ab.sh).
+template <class T, bool kDpp = true>
 __device__ __forceinline__ T wave_inclusive_sum(T x) {
-  if constexpr (std::is_integral<T>::value && sizeof(T) == 4) {
-    return wave_scan_dpp(x, T(0), [](T a, T b) { return a + b; });  // DPP: no LDS round trips
+  if constexpr (kDpp && std::is_integral<T>::value && sizeof(T) == 4) {
+    return wave_scan_dpp(x, T(0), [](T a, T b) { return a + b; });
   } else {
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -201,11 +205,11 @@ __device__ __forceinline__ void lds_barrier() {
 // Block exclusive scan of one int per thread.  `tmp` holds BLOCK/64 + 1 ints
 // in LDS.  Returns the exclusive prefix; `total` receives the block sum.
 // kLdsOnly: LDS-only barriers (register prefetches in flight survive them).
-template <int BLOCK, class T, bool kLdsOnly = false>
+template <int BLOCK, class T, bool kLdsOnly = false, bool kDpp = true>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* tmp, T& total) {
   static_assert(BLOCK % kWave == 0, "block must be whole waves");
   constexpr int NW = BLOCK / kWave;
-  T inc = wave_inclusive_sum(v);
+  T inc = wave_inclusive_sum<T, kDpp>(v);
   if (lane_id() == kWave - 1) tmp[wave_id()] = inc;
   if constexpr (kLdsOnly) lds_barrier();
   else __syncthreads();
@@ -397,7 +401,7 @@ __device__ int bitmap_prefix32(const uint32_t* bm, PrefixT* pref, int nw, int* t
     if (w < nw) local += __popc(bm[w]);
   }
   int total;
-  int base = block_exclusive_scan<BLOCK, int, true>(local, tmp, total);
+  int base = block_exclusive_scan<BLOCK, int, true, false>(local, tmp, total);
   for (int k = 0; k < per; ++k) {
     const int w = w0 + k;
     if (w < nw) {
