@@ -16,6 +16,7 @@
 #include "../../include/specpride.h"
 #include "best_score.hip"
 #include "bin_mean.hip"
+#include "bin_mean_split.hip"
 #include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
@@ -117,11 +118,21 @@ int spx_debug_stamps(void* dev_ptr) {
 const char* spx_last_error(void) { return g_err; }
 
 // ------------------------------------------------------------------ bin-mean
+// range records of the split path: every range holds >= SP_CAPW occupied bins
+// except each cluster's last, so C + P / SP_CAPW bounds them (capped; clusters past
+// the cap take the global kernel)
+int32_t split_range_cap(const spx_csr* csr) {
+  const int64_t r = csr->n_clusters + csr->n_peaks / spx::SP_CAPW + 1;
+  return (int32_t)std::max<int64_t>(1, std::min<int64_t>(r, int64_t(1) << 20));
+}
+
 size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info) {
   if (!csr || !params || !info) return 0;
   const int64_t C = csr->n_clusters;
+  const size_t Cm = (size_t)std::max<int64_t>(C, 1);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
-  return 2 * align256(sizeof(int32_t) * 2) + 2 * align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
+  return align256(sizeof(int32_t) * 5) + 3 * align256(sizeof(int32_t) * Cm) +
+         align256(sizeof(spx::SplitCluster) * Cm) + align256(sizeof(spx::SplitRange) * (size_t)split_range_cap(csr)) +
          (size_t)bin_mean_fallback_grid(C, params, dcap) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
@@ -139,11 +150,20 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   if (C == 0) return SPX_SUCCESS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
-  int32_t* counters = w.take<int32_t>(2);  // [0] deferred to the global kernel, [1] left to the LDS kernel
+  // [0] deferred past the LDS kernel, [1] left to the LDS kernel, [2] planned split
+  // clusters, [3] split ranges, [4] the global kernel's list
+  int32_t* counters = w.take<int32_t>(5);
   int32_t* n_def = counters;
   int32_t* n_rest = counters + 1;
+  int32_t* n_scl = counters + 2;
+  int32_t* n_ranges = counters + 3;
+  int32_t* n_glist = counters + 4;
   int32_t* def = w.take<int32_t>((size_t)C);
   int32_t* rest = w.take<int32_t>((size_t)C);
+  int32_t* glist = w.take<int32_t>((size_t)C);
+  spx::SplitCluster* scl = w.take<spx::SplitCluster>((size_t)C);
+  const int32_t range_cap = split_range_cap(csr);
+  spx::SplitRange* ranges = w.take<spx::SplitRange>((size_t)range_cap);
   char* scratch = w.base + w.used;
 
   spx::BinMeanParams P;
@@ -157,16 +177,26 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const spx::CsrView V = view(csr);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
-  if (hipMemsetAsync(counters, 0, 2 * sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
+  if (hipMemsetAsync(counters, 0, 5 * sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
   hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                      charge_out, status, rest, n_rest, def, n_def);
   if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),
                      dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
   if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
+  const dim3 gsplit((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048)));
+  hipLaunchKernelGGL(spx::bin_mean_split_plan_kernel, gsplit, dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                     charge_out, status, def, n_def, scl, n_scl, ranges, n_ranges, range_cap, glist, n_glist);
+  if (int rc = check_launch("bin_mean_split_plan_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_split_fold_kernel, dim3(4096), dim3(spx::BM_BLOCK), 0, s, V, P, O, scl, ranges,
+                     n_ranges, range_cap);
+  if (int rc = check_launch("bin_mean_split_fold_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_split_emit_kernel, gsplit, dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                     charge_out, status, scl, n_scl, ranges, glist, n_glist);
+  if (int rc = check_launch("bin_mean_split_emit_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)bin_mean_fallback_grid(C, params, dcap)),
                      dim3(spx::BM_BLOCK), 0, s, V, P,
-                     O, prec_out, charge_out, status, def, n_def, scratch,
+                     O, prec_out, charge_out, status, glist, n_glist, scratch,
                      spx::bin_mean_slice_bytes(P.n_words, dcap), (int)std::min<int64_t>(dcap, INT32_MAX));
   return check_launch("bin_mean_global_kernel");
 }

@@ -118,3 +118,19 @@ def test_config2_gap_average_shard_125k(gpu):
     sub = SpectraCSR.select_from_device(t, pick)
     got = _subset_host(t, ga, pick)
     assert_gap_close(got, np_oracle.gap_average(sub), 1000.0, rtol=GAP_RTOL)
+
+
+def test_config3_skewed_bin_mean_vs_oracle(gpu):
+    """Bin-mean on the configs[3] size law (up to n = 5,000 spectra, ~1.1M peaks per
+    giant cluster: the bin-range split path): every cluster with n > 48 plus 2,000
+    random small ones against the C oracle, bit-exact incl. values."""
+    t = make_clusters_torch(20000, seed=4, skewed=True, forced_large=4, large_size=5000)
+    batch = engine.DeviceBatch.from_device(t)
+    sizes = np.diff(batch.host_cluster_off)
+    bm = engine.bin_mean(batch).to_host()
+    assert np.all(bm["status"] == 0)
+    rng = np.random.default_rng(3)
+    small = np.flatnonzero(sizes <= 48)
+    pick = np.concatenate([np.flatnonzero(sizes > 48), rng.choice(small, 2000, replace=False)])
+    sub = SpectraCSR.select_from_device(t, pick)
+    assert_bin_mean_equal(_subset_host(t, bm, pick), c_oracle.bin_mean(sub))

@@ -396,3 +396,58 @@ def test_zero_peak_tail_all_entry_points(gpu, which):
     wcos, wavg, wst = np_oracle.binned_cosine(csr, r["out_off"], r["out_mz"], r["out_int"])
     np.testing.assert_array_equal(st[:csr.n_clusters], wst)
     torch.cuda.synchronize()
+
+
+def test_medoid_many_runtime_deferrals(gpu):
+    """small clusters that the register kernel defers only at run
+    time (m/z above 3,276.8 = outside its 32,768-bin table) land in the large-path
+    arena; 300 of them must all resolve (the engine re-budgets the workspace on
+    SPX_REP_ARENA and re-runs), with representatives and totals equal to the oracle."""
+    rng = np.random.default_rng(7)
+    clusters = []
+    for _c in range(300):
+        n = int(rng.integers(2, 24))
+        base = np.sort(rng.uniform(100.0, 4500.0, 150))
+        spectra = []
+        for _s in range(n):
+            keep = rng.random(150) > 0.1
+            mz = np.sort(np.round(base[keep] + rng.normal(0.0, 0.003, int(keep.sum())), 5))
+            spectra.append({"m/z array": mz, "intensity array": np.ones(len(mz))})
+        clusters.append(spectra)
+    csr = SpectraCSR.from_clusters(clusters)
+    rep, tot = engine.medoid(engine.DeviceBatch.from_host(csr), with_totals=True).to_host()
+    want_rep, want_tot = c_oracle.medoid(csr, with_totals=True)
+    assert np.all(rep >= 0)
+    np.testing.assert_array_equal(rep, want_rep)
+    np.testing.assert_array_equal(tot, want_tot)
+
+
+def test_bin_mean_split_path(gpu):
+    """Clusters past the register and LDS kernels (> 128 spectra, > 1,536 distinct
+    bins, 600-peak spectra) through the bin-range split path: one 3,000-spectrum
+    cluster, long-spectrum clusters, a giant unsorted one (flagged by the fold ->
+    the global kernel), a giant mixed-charge one and NaN m/z in a long one, mixed
+    with ordinary clusters; bit-exact against the C oracle, values included."""
+    big = make_clusters_np(1, seed=41, sizes=np.array([3000]))
+    longsp = make_clusters_np(12, seed=42, n_template=600, max_size=30)
+    plain = make_clusters_np(30, seed=43)
+    uns = _shuffled(make_clusters_np(1, seed=44, sizes=np.array([400])), seed=5)
+    mixed = make_clusters_np(1, seed=45, sizes=np.array([300]))
+    mixed.charge[7] = mixed.charge[0] + 1
+    nan = make_clusters_np(1, seed=46, n_template=500, sizes=np.array([20]))
+    nan.mz[nan.spec_off[3] + 5] = np.nan
+
+    def cat(parts):
+        cl, sp, mz, it, pr, ch, rt = [0], [0], [], [], [], [], []
+        for p in parts:
+            cl += list(cl[-1] + p.cluster_off[1:])
+            sp += list(sp[-1] + p.spec_off[1:])
+            mz.append(p.mz); it.append(p.inten); pr.append(p.prec_mz); ch.append(p.charge); rt.append(p.rt)
+        return SpectraCSR(np.array(cl), np.array(sp), np.concatenate(mz), np.concatenate(it), np.concatenate(pr),
+                          np.concatenate(ch), np.concatenate(rt))
+
+    csr = cat([plain, big, longsp, uns, mixed, nan, plain])
+    got = _bin_mean(csr)
+    want = c_oracle.bin_mean(csr)
+    assert_bin_mean_equal(got, want)
+    assert np.any(want["status"] == engine.STATUS_MIXED_CHARGE)
