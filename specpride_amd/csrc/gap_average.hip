@@ -44,12 +44,17 @@ struct GapParams {
 constexpr int GA_BLOCK = 512;  // 2 workgroups per CU (LDS): 16 waves
 constexpr int GA_NW = GA_BLOCK / kWave;
 #ifndef SPX_GA_UM
-#define SPX_GA_UM 16
+#define SPX_GA_UM 20
+#endif
+#ifndef SPX_GA_IT
+// register clusters' intensities: 0 streamed by passes 1 and 5; 1 loaded with the
+// m/z (pass 1) and re-loaded right after pass 3 (pass 5); 2 loaded once, kept
+#define SPX_GA_IT 0
 #endif
 #ifndef SPX_GA_TAGS
 #define SPX_GA_TAGS 1  // pass 3's per-peak slots kept in registers (u16 pairs) for pass 5
 #endif
-constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (8,192 per cluster)
+constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10,240 per cluster: n <= 51 at ~200 peaks)
 constexpr int GA_WMAX = 3584;  // 229,376 buckets (2,293 Da at 0.01)
 constexpr int GA_DCAP = 1536;  // occupied buckets per cluster
 
@@ -74,6 +79,7 @@ struct GapSmem {
   int tmp[GA_BLOCK / kWave + 1];
   int votes[2 * GA_NW];
   double red[GA_BLOCK / kWave * 3];
+  int prank[2 * GA_NW * kWave];  // per-wave partial precursor ranks (mass, RT)
 };
 
 __device__ __forceinline__ double nan_d() { return __longlong_as_double(0x7ff8000000000000ll); }
@@ -102,7 +108,34 @@ __device__ __forceinline__ PrecLanes prec_lanes(const CsrView& v, int64_t s0, in
   return PrecLanes{valid ? v.charge[s0 + lane] : 0, valid ? v.prec_mz[s0 + lane] : 0.0, valid ? v.rt[s0 + lane] : 0.0};
 }
 
-__device__ PrecSummary precursor_summary_wave(const PrecLanes& pl, int n, const GapParams& P) {
+// Stable ranks of lane i's neutral mass and RT among the cluster's n <= 64
+// spectra, counted over j = j0, j0 + dj, ... only: the LDS kernel splits the O(n^2)
+// comparisons over its 8 waves (j0 = wave, dj = 8) and sums the partial ranks.
+struct PrecRanks {
+  int m, r;
+};
+__device__ __forceinline__ PrecRanks prec_ranks(const PrecLanes& pl, int n, const GapParams& P, int j0, int dj) {
+  const int lane = lane_id();
+  const double z = (double)pl.z;
+  const double mi = pl.pm * z - z * P.proton;  // (m*c - c*H), no contraction
+  const double ri = pl.rt;
+  PrecRanks k{0, 0};
+  for (int j = j0; j < n; j += dj) {
+    const double mj = readlane_f64(mi, j);
+    k.m += lt_nan_last(mj, mi) || (!lt_nan_last(mi, mj) && j < lane);
+  }
+  if (P.rt_mode == 0) {
+    for (int j = j0; j < n; j += dj) {
+      const double rj = readlane_f64(ri, j);
+      k.r += lt_nan_last(rj, ri) || (!lt_nan_last(ri, rj) && j < lane);
+    }
+  }
+  return k;
+}
+
+// ranks: the summed partial ranks, or nullptr to count them here
+__device__ PrecSummary precursor_summary_wave(const PrecLanes& pl, int n, const GapParams& P,
+                                              const PrecRanks* ranks = nullptr) {
   PrecSummary R;
   const int lane = lane_id();
   const double H = P.proton;
@@ -112,22 +145,15 @@ __device__ PrecSummary precursor_summary_wave(const PrecLanes& pl, int n, const 
   const double pm = pl.pm;
   const double mi = pm * z - z * H;  // (m*c - c*H), no contraction
   const double ri = pl.rt;
+  const PrecRanks K = ranks ? *ranks : prec_ranks(pl, n, P, 0, 1);
   // lower-median index of the neutral masses: rank == (n-1)//2
   const int want = (n - 1) / 2;
-  int rank = 0;
-  for (int j = 0; j < n; ++j) {
-    const double mj = readlane_f64(mi, j);
-    rank += lt_nan_last(mj, mi) || (!lt_nan_last(mi, mj) && j < lane);
-  }
+  const int rank = K.m;
   const unsigned long long hit = __ballot(valid && rank == want);
   const int lm = hit ? __ffsll((long long)hit) - 1 : 0;
   double rt_lo = 0.0, rt_hi = 0.0;
   if (P.rt_mode == 0) {  // np.median
-    int rr = 0;
-    for (int j = 0; j < n; ++j) {
-      const double rj = readlane_f64(ri, j);
-      rr += lt_nan_last(rj, ri) || (!lt_nan_last(ri, rj) && j < lane);
-    }
+    const int rr = K.r;
     const unsigned long long h1 = __ballot(valid && rr == (n - 1) / 2), h2 = __ballot(valid && rr == n / 2);
     rt_lo = readlane_f64(ri, __ffsll((long long)h1) - 1);
     rt_hi = readlane_f64(ri, __ffsll((long long)h2) - 1);
@@ -279,7 +305,7 @@ __device__ __forceinline__ void gap_peaks(const CsrView& v, int64_t p0, int64_t 
 template <class PrefixT>
 __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState<PrefixT>& S, int64_t c,
                             const PeaksOut& out, int* tmp, double* red, int* votes, const PrecLanes* pl = nullptr,
-                            PrecSummary* early = nullptr) {
+                            int* prank = nullptr) {
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
   // LDS state (the LDS kernel): barriers order LDS only, so register loads in
   // flight survive them; global-scratch state (the fallback kernel): full barriers
@@ -296,14 +322,24 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   if (n == 0) return kNoGap;
 
   // The cluster's m/z values are read from HBM ONCE into registers when they
-  // fit (<= GA_UM per thread = 8,192 peaks: ~80% of the U{2..50} clusters of
+  // fit (<= GA_UM per thread = 10,240 peaks: nearly every U{2..50} cluster of
   // the configs); passes 2-3 run from registers, and pass 3's slot per peak is
   // kept (u16 pairs) for pass 5.  Intensities are needed only by
   // passes 1 and 5 and are streamed there (8 loads in flight), so the register
   // budget holds twice as many peaks as m/z + intensity pairs would.  Larger
   // clusters re-read both per pass.
   const bool inreg = N <= (int64_t)GA_UM * GA_BLOCK;  // uniform
+  constexpr int kIt = SPX_GA_IT;
   double rm[GA_UM];
+  double ri[kIt ? GA_UM : 1];
+  auto load_ri = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < (kIt ? GA_UM : 0); ++u) {
+      const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
+      const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
+      ri[u] = N > 0 ? v.inten[kk] : 0.0;
+    }
+  };
   uint32_t tags[(GA_UM + 1) / 2];  // pass-3 slot of each register peak (u16 pairs), reused by pass 5
 #pragma unroll
   for (int q = 0; q < (GA_UM + 1) / 2; ++q) tags[q] = 0u;
@@ -314,8 +350,13 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
       rm[u] = N > 0 ? v.mz[kk] : 0.0;
     }
+    load_ri();
   }
-  if (early && pl && wid == 0 && n <= kWave) *early = precursor_summary_wave(*pl, (int)n, P);
+  if (prank && pl && n <= kWave) {  // uniform: every wave's share of the precursor ranks
+    const PrecRanks k = prec_ranks(*pl, (int)n, P, wid, GA_NW);
+    prank[wid * kWave + lane] = k.m;
+    prank[(GA_NW + wid) * kWave + lane] = k.r;
+  }
   SPX_STAMP(1);
   // f(m, it, tag) over every peak; kInten false passes it = 0 and loads none
   auto peaks_g = [&](auto inten_c, auto tagout_c, auto f) __attribute__((always_inline)) {
@@ -326,7 +367,10 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 #pragma unroll
       for (int u0 = 0; u0 < GA_UM; u0 += 8) {
         double itb[8];
-        if constexpr (kInten) {
+        if constexpr (kInten && kIt) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) itb[q] = (u0 + q < GA_UM) ? ri[u0 + q] : 0.0;
+        } else if constexpr (kInten) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const int64_t k = p0 + (int64_t)(u0 + q) * GA_BLOCK + tid;
@@ -445,6 +489,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)key);
     atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)key);
   });
+  if (kIt == 1 && inreg) load_ri();  // lands during the gap scan (pass 4)
   bar();
 
   SPX_STAMP(4);
@@ -539,13 +584,23 @@ template <class PrefixT>
 __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P, int64_t c, int32_t st,
                                            const PeaksOut& out, double* prec_out, int32_t* charge_out,
                                            double* rt_out, int32_t* status, const PrecLanes* pl = nullptr,
-                                           const PrecSummary* early = nullptr) {
+                                           const int* prank = nullptr) {
   const int64_t s0 = v.cluster_off[c], n = v.cluster_off[c + 1] - s0;
   if (st == kDeferred) return;
   if (wave_id() == 0) {
     PrecSummary R{nan_d(), nan_d(), 0, kOk};
-    if (early && n > 0 && n <= kWave) R = *early;
-    else if (n > 0) R = (pl && n <= kWave) ? precursor_summary_wave(*pl, (int)n, P) : precursor_summary(v, s0, n, P);
+    if (prank && pl && n > 0 && n <= kWave) {
+      PrecRanks K{0, 0};
+      const int lane = lane_id();
+#pragma unroll
+      for (int w = 0; w < GA_NW; ++w) {
+        K.m += prank[w * kWave + lane];
+        K.r += prank[(GA_NW + w) * kWave + lane];
+      }
+      R = precursor_summary_wave(*pl, (int)n, P, &K);
+    } else if (n > 0) {
+      R = (pl && n <= kWave) ? precursor_summary_wave(*pl, (int)n, P) : precursor_summary(v, s0, n, P);
+    }
     if (lane_id() == 0) {
       // the reference computes the precursor first (:161-163): its error wins
       const int32_t fin = R.status != kOk ? R.status : st;
@@ -568,9 +623,8 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   GapState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.gcnt, L.kmin, L.kmax, GA_WMAX, GA_DCAP};
   const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
   PrecLanes pl{0, 0.0, 0.0};
-  if (wave_id() == 0 && pn <= kWave) pl = prec_lanes(v, ps0, pn);
-  PrecSummary early{0.0, 0.0, 0, kOk};
-  const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, &early);
+  if (pn <= kWave) pl = prec_lanes(v, ps0, pn);
+  const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
   if (st == kDeferred) {
     if (threadIdx.x == 0) {
       status[c] = kDeferred;
@@ -578,7 +632,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
     }
     return;
   }
-  gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, nullptr, &early);
+  gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank);
   SPX_STAMP(7);
 }
 
