@@ -46,11 +46,6 @@ constexpr int GA_NW = GA_BLOCK / kWave;
 #ifndef SPX_GA_UM
 #define SPX_GA_UM 20
 #endif
-#ifndef SPX_GA_IT
-// register clusters' intensities: 0 streamed by passes 1 and 5; 1 loaded with the
-// m/z (pass 1) and re-loaded right after pass 3 (pass 5); 2 loaded once, kept
-#define SPX_GA_IT 0
-#endif
 #ifndef SPX_GA_TAGS
 #define SPX_GA_TAGS 1  // pass 3's per-peak slots kept in registers (u16 pairs) for pass 5
 #endif
@@ -329,17 +324,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   // budget holds twice as many peaks as m/z + intensity pairs would.  Larger
   // clusters re-read both per pass.
   const bool inreg = N <= (int64_t)GA_UM * GA_BLOCK;  // uniform
-  constexpr int kIt = SPX_GA_IT;
   double rm[GA_UM];
-  double ri[kIt ? GA_UM : 1];
-  auto load_ri = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < (kIt ? GA_UM : 0); ++u) {
-      const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
-      const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
-      ri[u] = N > 0 ? v.inten[kk] : 0.0;
-    }
-  };
   uint32_t tags[(GA_UM + 1) / 2];  // pass-3 slot of each register peak (u16 pairs), reused by pass 5
 #pragma unroll
   for (int q = 0; q < (GA_UM + 1) / 2; ++q) tags[q] = 0u;
@@ -350,7 +335,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
       rm[u] = N > 0 ? v.mz[kk] : 0.0;
     }
-    load_ri();
   }
   if (prank && pl && n <= kWave) {  // uniform: every wave's share of the precursor ranks
     const PrecRanks k = prec_ranks(*pl, (int)n, P, wid, GA_NW);
@@ -367,10 +351,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 #pragma unroll
       for (int u0 = 0; u0 < GA_UM; u0 += 8) {
         double itb[8];
-        if constexpr (kInten && kIt) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) itb[q] = (u0 + q < GA_UM) ? ri[u0 + q] : 0.0;
-        } else if constexpr (kInten) {
+        if constexpr (kInten) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const int64_t k = p0 + (int64_t)(u0 + q) * GA_BLOCK + tid;
@@ -489,7 +470,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)key);
     atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)key);
   });
-  if (kIt == 1 && inreg) load_ri();  // lands during the gap scan (pass 4)
   bar();
 
   SPX_STAMP(4);
