@@ -1,0 +1,90 @@
+/* spx_mgf.h — the host MGF ingest/emit C-ABI (specpride_amd/lib/libspx_mgf.so,
+ * built from specpride_amd/csrc/mgf_io.cpp with g++; no GPU, no torch types).
+ *
+ * the readers and writers on either side of the hot path.
+ * Each entry point replaces (or feeds) one piece of the reference:
+ *
+ *   spx_mgf_parse              src/binning.py:122-167      read_mgf line loop
+ *   spx_mgf_parse_general      the readers of the other two CLIs: pyteomics
+ *                              mgf.IndexedMGF / mgf.read (average_spectrum_clustering.py:156,
+ *                              :200) and OpenMS MascotGenericFile().load
+ *                              (most_similar_representative.py:41-43); one well-formed
+ *                              subset, checked against the Python reader the shims use
+ *   spx_mgf_index              no reference counterpart: record byte ranges, titles and
+ *                              peak-line counts (no number parsed), so ranks of a sharded
+ *                              CLI can group the records the reference's way
+ *                              (average_spectrum_clustering.py:151-160,
+ *                              most_similar_representative.py:48-52) before parsing
+ *   spx_mgf_parse_ranges       the same parsers over only the listed records
+ *   spx_mgf_format_binning /   src/binning.py:234-245 writer (f-string of numpy floats)
+ *   spx_mgf_write_binning_batch
+ *   spx_py_repr                Python repr() of a float64
+ *
+ * Parse results are opaque handles: query sizes, copy the arrays into caller-owned
+ * buffers, then free the handle.  A parse whose input is outside the native subset
+ * reports an error string starting with "fallback:"; the caller then re-reads the file
+ * with the reference's own Python reader, so the outcome is the reference's either way.
+ */
+#ifndef SPX_MGF_H
+#define SPX_MGF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- parse results (spx_mgf_parse, spx_mgf_parse_general, spx_mgf_parse_ranges) ---- */
+
+/* binning.py:122-167 semantics.  threads <= 0: min(16, hardware threads). */
+void* spx_mgf_parse(const char* path, int threads);
+/* The pyteomics-shaped reader (PEPMASS second token, CHARGE, RTINSECONDS, TITLE). */
+void* spx_mgf_parse_general(const char* path, int threads);
+/* Only records [begin[i], end[i]) (byte ranges from spx_mgf_index), in the given order;
+ * general: 0 binning.py grammar, 1 the pyteomics-shaped grammar. */
+void* spx_mgf_parse_ranges(const char* path, const int64_t* begin, const int64_t* end, int64_t n, int general,
+                           int threads);
+
+/* NULL on success, else the message ("fallback: ..." = outside the native subset). */
+const char* spx_mgf_error(void* h);
+int64_t spx_mgf_n_spectra(void* h);
+int64_t spx_mgf_n_peaks(void* h);
+/* spec_off[S+1], mz[P], it[P], prec[S], charge[S], flags[S] (bit0 PEPMASS, bit1 CHARGE,
+ * general reader also bit2 RTINSECONDS, bit3 TITLE). */
+void spx_mgf_copy(void* h, int64_t* spec_off, double* mz, double* it, double* prec, int64_t* charge, int32_t* flags);
+/* rt[S] (general reader; NaN where absent). */
+void spx_mgf_copy_rt(void* h, double* rt);
+/* '\n'-joined titles, one per spectrum. */
+const char* spx_mgf_titles(void* h);
+void spx_mgf_free(void* h);
+
+/* ---- record index ---- */
+
+void* spx_mgf_index(const char* path, int general);
+const char* spx_mgf_index_error(void* h);
+int64_t spx_mgf_index_n(void* h);
+/* begin[n], end[n]: byte range of each record; npk[n]: its peak lines. */
+void spx_mgf_index_copy(void* h, int64_t* begin, int64_t* end, int64_t* npk);
+const char* spx_mgf_index_titles(void* h);
+void spx_mgf_index_free(void* h);
+
+/* ---- writers ---- */
+
+/* One consensus spectrum as binning.py:234-245 text into buf (cap bytes); returns the
+ * length, or -1 when cap < 64 + strlen(cid) + strlen(charge_str) + 52 n.
+ * skip_nan: omit NaN peaks. */
+int64_t spx_mgf_format_binning(char* buf, int64_t cap, const char* cid, const char* charge_str, double prec,
+                               const double* mz, const double* it, int64_t n, int skip_nan);
+/* Python repr(x) into out (>= 32 bytes, not NUL-terminated); returns the length. */
+int spx_py_repr(double x, char* out);
+/* C consensus spectra (cluster c = peaks [off[c], off[c+1])), ids '\n'-joined, written
+ * in order.  Returns 0, or -1 on an I/O error. */
+int spx_mgf_write_binning_batch(const char* path, int64_t C, const char* ids, const int64_t* charge,
+                                const double* prec, const int64_t* off, const double* mz, const double* it,
+                                int threads);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPX_MGF_H */

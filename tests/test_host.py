@@ -8,6 +8,7 @@ import ctypes
 import io
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -38,6 +39,23 @@ def test_hip_library_exports_every_declared_symbol():
     assert not missing, missing
     L.spx_abi_version.restype = ctypes.c_int
     assert L.spx_abi_version() == _lib.SPX_ABI_VERSION == 2
+
+
+MGF_HEADER = os.path.join(REPO, "include", "spx_mgf.h")
+
+
+def test_mgf_library_exports_every_declared_symbol():
+    text = re.sub(r"/\*.*?\*/", "", open(MGF_HEADER).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(spx_[a-z0-9_]+)\s*\(", text)))
+    assert len(declared) == 19, declared
+    L = ctypes.CDLL(_lib.build_mgf())
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    # and nothing exported that the header leaves out
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.build_mgf()], capture_output=True, text=True)
+    if nm.returncode == 0:
+        exported = sorted(set(re.findall(r"\b[TW] (spx_[a-z0-9_]+)$", nm.stdout, flags=re.M)))
+        assert exported == declared
 
 
 def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
