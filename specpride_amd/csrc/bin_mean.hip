@@ -505,6 +505,34 @@ __device__ __forceinline__ void unrolled_while(int n, F&& f, std::integer_sequen
   (void)((more(Js) ? (f(std::integral_constant<int, Js>{}), true) : false) && ...);
 }
 
+// The same over pairs of steps: f(2k) and f(2k+1) share one guard (2k < n), so
+// the two steps are one basic block and their dependency chains interleave.
+// Only for steps that are harmless past n (their lanes contribute nothing).
+template <class F, int... Ks>
+__device__ __forceinline__ void unrolled_pairs(int n, F&& f, std::integer_sequence<int, Ks...>) {
+  int nn = __builtin_amdgcn_readfirstlane(n);
+  auto more = [&](int j) __attribute__((always_inline)) {
+    asm volatile("" : "+s"(nn));
+    return j < nn;
+  };
+  auto pair = [&](auto kc) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    f(std::integral_constant<int, 2 * k>{});
+    f(std::integral_constant<int, 2 * k + 1>{});
+  };
+  (void)((more(2 * Ks) ? (pair(std::integral_constant<int, Ks>{}), true) : false) && ...);
+}
+#ifndef SPX_BR_PAIRS
+#define SPX_BR_PAIRS 0  // bit 0: phase A in pairs, bit 1: phase B, bit 2: phase C
+#endif
+template <int kBit, class F>
+__device__ __forceinline__ void reg_steps(int n, F&& f) {
+  if constexpr ((SPX_BR_PAIRS >> kBit) & 1)
+    unrolled_pairs(n, f, std::make_integer_sequence<int, BR_NMAX / 2>{});
+  else
+    unrolled_while(n, f, std::make_integer_sequence<int, BR_NMAX>{});
+}
+
 __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const BinMeanParams& P, BinRegSmem& L,
                                                      int64_t c, const PeaksOut& out, double* prec_out,
                                                      int32_t* charge_out) {
@@ -570,7 +598,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
 #pragma unroll
     for (int j = 0; j < BR_NMAX; ++j) code[j] = -1;
-    unrolled_while(n, [&](auto jc) __attribute__((always_inline)) {
+    reg_steps<0>(n, [&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       const double m = ra[j % BR_PFA];
       const int len = rl[j % BR_PFA];
@@ -588,7 +616,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       // LDS atomics serialise; distinct words do not)
       atomicOr(&bm32[valid ? key >> 5 : lane], valid ? 1u << (key & 31) : 0u);
       code[j] = valid ? key : -1;
-    }, std::make_integer_sequence<int, BR_NMAX>{});
+    });
   }
   // phase C's first (m/z, intensity) loads go out now and land during phase B
   // (whose barriers are LDS-only, so they stay in flight)
@@ -608,7 +636,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   for (int d = tid; d < D; d += BM_BLOCK) L.cnt[d] = 0u;
   if (tid < kWave) L.cnt[BM_DCAP + tid] = 0u;
   lds_barrier();
-  unrolled_while(n, [&](auto jc) __attribute__((always_inline)) {
+  reg_steps<1>(n, [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     const bool valid = code[j] >= 0;
     const uint32_t b = (uint32_t)(valid ? code[j] : 0);
@@ -616,14 +644,14 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     const int slot = (int)L.u.b.pre[w] + __popc(L.u.b.bits[w] & ((1u << (b & 31)) - 1u));
     code[j] = valid ? slot : BM_DCAP + lane;  // a dummy slot of its own, never read
     atomicAdd(&L.cnt[code[j]], valid ? 1u : 0u);
-  }, std::make_integer_sequence<int, BR_NMAX>{});
+  });
   lds_barrier();  // the bitmap is dead: the accumulators take its place
   for (int d = tid; d < D; d += BM_BLOCK) L.u.acc[d] = make_float2(0.0f, 0.0f);
   lds_barrier();
   SPX_STAMP(3);
 
   // ---- C: the ordered fold (spectrum order per slot = the reference's order)
-  unrolled_while(n, [&](auto jc) __attribute__((always_inline)) {
+  reg_steps<2>(n, [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     const double m = rm[j % BR_PFC], it = ri[j % BR_PFC];
     const uint32_t bo = boff(j + BR_PFC);
@@ -635,7 +663,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     a.y = (float)((double)a.y + m);
     L.u.acc[slot] = a;
     lds_barrier();
-  }, std::make_integer_sequence<int, BR_NMAX>{});
+  });
   SPX_STAMP(4);
 
   // ---- D: quorum filter and ordered output (binning.py:181-183, 209-222)

@@ -46,9 +46,6 @@ constexpr int GA_NW = GA_BLOCK / kWave;
 #ifndef SPX_GA_UM
 #define SPX_GA_UM 20
 #endif
-#ifndef SPX_GA_TAGS
-#define SPX_GA_TAGS 1  // pass 3's per-peak slots kept in registers (u16 pairs) for pass 5
-#endif
 constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10,240 per cluster: n <= 51 at ~200 peaks)
 constexpr int GA_WMAX = 3584;  // 229,376 buckets (2,293 Da at 0.01)
 constexpr int GA_DCAP = 1536;  // occupied buckets per cluster
@@ -318,16 +315,16 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 
   // The cluster's m/z values are read from HBM ONCE into registers when they
   // fit (<= GA_UM per thread = 10,240 peaks: nearly every U{2..50} cluster of
-  // the configs); passes 2-3 run from registers, and pass 3's slot per peak is
-  // kept (u16 pairs) for pass 5.  Intensities are needed only by
+  // the configs); passes 2-3 run from registers, pass 2's bucket per peak is
+  // kept for pass 3 and pass 3's slot for pass 5 (a u32 each).  Intensities are needed only by
   // passes 1 and 5 and are streamed there (8 loads in flight), so the register
   // budget holds twice as many peaks as m/z + intensity pairs would.  Larger
   // clusters re-read both per pass.
   const bool inreg = N <= (int64_t)GA_UM * GA_BLOCK;  // uniform
   double rm[GA_UM];
-  uint32_t tags[(GA_UM + 1) / 2];  // pass-3 slot of each register peak (u16 pairs), reused by pass 5
+  uint32_t tags[GA_UM];  // per register peak: pass 2's bucket, then pass 3's slot (for pass 5)
 #pragma unroll
-  for (int q = 0; q < (GA_UM + 1) / 2; ++q) tags[q] = 0u;
+  for (int q = 0; q < GA_UM; ++q) tags[q] = 0u;
   if (inreg) {
 #pragma unroll
     for (int u = 0; u < GA_UM; ++u) {
@@ -363,12 +360,9 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
           const int u = u0 + q;
           if (u < GA_UM) {
             const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
-            int32_t tag = (int32_t)((tags[u >> 1] >> (16 * (u & 1))) & 0xFFFFu);
+            int32_t tag = (int32_t)tags[u];
             if (k < p1) f(rm[u], kInten ? itb[q] : 0.0, tag);
-            if constexpr (kTagOut) {
-              if (u & 1) tags[u >> 1] |= (uint32_t)tag << 16;
-              else tags[u >> 1] = (uint32_t)tag & 0xFFFFu;
-            }
+            if constexpr (kTagOut) tags[u] = (uint32_t)tag;
           }
         }
       }
@@ -380,9 +374,8 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     }
   };
   auto peaks = [&](auto f) __attribute__((always_inline)) { peaks_g(std::true_type{}, std::false_type{}, f); };
-  auto peaks_m = [&](auto f) __attribute__((always_inline)) { peaks_g(std::false_type{}, std::false_type{}, f); };
   auto peaks_m_tag = [&](auto f) __attribute__((always_inline)) { peaks_g(std::false_type{}, std::true_type{}, f); };
-  const bool tagged = SPX_GA_TAGS && inreg;  // pass 5 takes pass 3's slots from registers (uniform)
+  const bool tagged = inreg;  // passes 3 and 5 take the bucket / slot from registers (uniform)
 
   // 1: extrema and finiteness
   double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
@@ -443,11 +436,13 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   // 2: occupied buckets
   for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
   bar();
-  peaks_m([&](double m, double, int32_t& tag) {
+  auto pass2 = [&](double m, double, int32_t& tag) __attribute__((always_inline)) {
     const int64_t b = floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
+    tag = (int32_t)b;
     SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
     atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
-  });
+  };
+  peaks_m_tag(pass2);
   bar();
   const int D = bitmap_prefix<GA_BLOCK, PrefixT, kL>(S.bitmap, S.wprefix, (int)nw, tmp);
   if (D > S.dcap) return kDeferred;
@@ -462,7 +457,8 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 
   // 3: per-slot count and m/z extent
   peaks_m_tag([&](double m, double, int32_t& tag) {
-    const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
+    const int64_t b = tagged ? (int64_t)tag : floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
+    const int slot = bitmap_rank(S.bitmap, S.wprefix, b);
     tag = slot;
     const uint64_t key = f64_order_key(m);
     SPX_GUARD(slot >= 0 && slot < D, "gap slot c=%ld slot=%d D=%d\n", (long)c, slot, D)
