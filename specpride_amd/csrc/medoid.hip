@@ -1090,27 +1090,66 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_argmin_kernel(const MedoidMet
 
 // ---------------------------------------------------------- pair distances
 // distance(spec1, spec2) of most_similar_representative.py:13-19 for arbitrary
-// (global) spectrum pairs: one wave per pair.  |B_a ∩ B_b| counts the distinct
-// bins of a (first occurrence in a) that occur in b.  O(p_a * (p_a + p_b)) per
-// pair: this is the per-call API, not the batched medoid path.
-__global__ __launch_bounds__(256) void xcorr_pairs_kernel(CsrView v, MedoidParams P, const int64_t* __restrict__ pairs,
-                                                          int64_t n_pairs, double* __restrict__ out) {
-  const int64_t p = (int64_t)blockIdx.x * 4 + wave_id();
-  if (p >= n_pairs) return;
-  const int64_t sa = pairs[2 * p], sb = pairs[2 * p + 1];
-  const int64_t a0 = v.spec_off[sa], a1 = v.spec_off[sa + 1], b0 = v.spec_off[sb], b1 = v.spec_off[sb + 1];
-  uint32_t cnt = 0;
-  for (int64_t ka = a0 + lane_id(); ka < a1; ka += kWave) {
-    const int64_t bk = md_bin(v.mz[ka], P);
-    bool first = true;
-    for (int64_t kk = a0; kk < ka && first; ++kk) first = md_bin(v.mz[kk], P) != bk;
-    if (!first) continue;
-    bool found = false;
-    for (int64_t kb = b0; kb < b1 && !found; ++kb) found = md_bin(v.mz[kb], P) == bk;
-    cnt += found;
+// (global) spectrum pairs: one workgroup per pair.  |B_a ∩ B_b| = popcount of the
+// AND of the two spectra's bin bitmaps in LDS (bins [0, XC_BINS): m/z < 6,553.6 at
+// tol 0.1); a pair with a bin outside that range falls back to one wave's
+// O(p_a * (p_a + p_b)) scan (first occurrence in a, membership in b).
+constexpr int XC_BLOCK = 256;
+constexpr int XC_BINS = 1 << 16;
+constexpr int XC_W = XC_BINS / 32;
+
+__global__ __launch_bounds__(XC_BLOCK) void xcorr_pairs_kernel(CsrView v, MedoidParams P,
+                                                               const int64_t* __restrict__ pairs, int64_t n_pairs,
+                                                               double* __restrict__ out) {
+  __shared__ uint32_t bma[XC_W], bmb[XC_W];
+  __shared__ int votes[2 * (XC_BLOCK / kWave)];
+  __shared__ uint32_t part[XC_BLOCK / kWave];
+  const int tid = threadIdx.x;
+  for (int64_t p = blockIdx.x; p < n_pairs; p += gridDim.x) {
+    const int64_t sa = pairs[2 * p], sb = pairs[2 * p + 1];
+    const int64_t a0 = v.spec_off[sa], a1 = v.spec_off[sa + 1], b0 = v.spec_off[sb], b1 = v.spec_off[sb + 1];
+    for (int w = tid; w < XC_W; w += XC_BLOCK) { bma[w] = 0u; bmb[w] = 0u; }
+    __syncthreads();
+    int outside = 0;
+    for (int64_t k = a0 + tid; k < a1; k += XC_BLOCK) {
+      const int64_t bk = md_bin(v.mz[k], P);
+      if (bk < 0 || bk >= XC_BINS) outside = 1;
+      else atomicOr(&bma[bk >> 5], 1u << (bk & 31));
+    }
+    for (int64_t k = b0 + tid; k < b1; k += XC_BLOCK) {
+      const int64_t bk = md_bin(v.mz[k], P);
+      if (bk < 0 || bk >= XC_BINS) outside = 1;
+      else atomicOr(&bmb[bk >> 5], 1u << (bk & 31));
+    }
+    if (block_any<XC_BLOCK, false>(outside, votes, 0)) {
+      if (wave_id() == 0) {  // the scan, one wave
+        uint32_t cnt = 0;
+        for (int64_t ka = a0 + lane_id(); ka < a1; ka += kWave) {
+          const int64_t bk = md_bin(v.mz[ka], P);
+          bool first = true;
+          for (int64_t kk = a0; kk < ka && first; ++kk) first = md_bin(v.mz[kk], P) != bk;
+          if (!first) continue;
+          bool found = false;
+          for (int64_t kb = b0; kb < b1 && !found; ++kb) found = md_bin(v.mz[kb], P) == bk;
+          cnt += found;
+        }
+        cnt = wave_sum(cnt);
+        if (lane_id() == 0) out[p] = md_dist(cnt, a1 - a0, b1 - b0);
+      }
+    } else {
+      uint32_t cnt = 0;
+      for (int w = tid; w < XC_W; w += XC_BLOCK) cnt += (uint32_t)__popc(bma[w] & bmb[w]);
+      cnt = wave_sum(cnt);
+      if (lane_id() == 0) part[wave_id()] = cnt;
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t c = 0;
+        for (int w = 0; w < XC_BLOCK / kWave; ++w) c += part[w];
+        out[p] = md_dist(c, a1 - a0, b1 - b0);
+      }
+    }
+    __syncthreads();
   }
-  cnt = wave_sum(cnt);
-  if (lane_id() == 0) out[p] = md_dist(cnt, a1 - a0, b1 - b0);
 }
 
 }  // namespace spx

@@ -377,7 +377,7 @@ extern "C" int spx_xcorr_distance(const spx_csr* csr, const spx_medoid_params* p
   if (!(params->tolerance > 0)) return fail(SPX_EINVAL, "spx_xcorr_distance: tolerance must be > 0");
   if (n_pairs <= 0) return SPX_SUCCESS;
   spx::MedoidParams P{params->tolerance, 1.0 / params->tolerance};
-  hipLaunchKernelGGL(spx::xcorr_pairs_kernel, dim3((unsigned)((n_pairs + 3) / 4)), dim3(256), 0,
+  hipLaunchKernelGGL(spx::xcorr_pairs_kernel, dim3((unsigned)std::min<int64_t>(n_pairs, 65536)), dim3(spx::XC_BLOCK), 0,
                      reinterpret_cast<hipStream_t>(stream), view(csr), P, pairs, n_pairs, out);
   return check_launch("xcorr_pairs_kernel");
 }

@@ -40,6 +40,39 @@ def _stream_handle(stream=None) -> Optional[int]:
     return s.cuda_stream or None
 
 
+# Small batches (the per-cluster shim calls: one cluster, one pair) cross PCIe
+# as ONE packed copy each way through a reused pinned buffer, instead of one
+# pageable copy per array: the per-call cost is then launches + two copies.
+PACKED_MAX_BYTES = 64 << 20
+
+
+class _Pinned:
+    """A grow-only pinned host staging buffer (one per direction).  Every copy
+    through it is waited for before the call returns, so it is free again."""
+
+    def __init__(self):
+        self.buf = None
+
+    def take(self, nbytes: int):
+        import torch
+
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(int(nbytes), 1 << 16) * 2, dtype=torch.uint8, pin_memory=True)
+        return self.buf
+
+
+_H2D, _D2H = _Pinned(), _Pinned()
+
+
+def _layout(items):
+    """Byte offsets (256-aligned) of (name, numpy array) items; total bytes."""
+    off, o = {}, 0
+    for name, a in items:
+        off[name] = o
+        o += (a.nbytes + 255) & ~255
+    return off, o
+
+
 class DeviceBatch:
     """A SpectraCSR mirrored into HBM, with the host metadata the ABI needs."""
 
@@ -68,8 +101,15 @@ class DeviceBatch:
         # SPX_NON_FINITE, it must not blow up the workspace sizing of the others
         fin = csr.mz[np.isfinite(csr.mz)] if csr.n_peaks else csr.mz
         span = float(fin.max() - fin.min()) if len(fin) else 0.0
-        return cls(csr.to_device(device), csr.cluster_off, csr.spec_off, span,
-                   cluster_ids=csr.cluster_ids, titles=csr.titles)
+        items = [("cluster_off", csr.cluster_off), ("spec_off", csr.spec_off), ("mz", csr.mz),
+                 ("inten", csr.inten), ("prec_mz", csr.prec_mz), ("charge", csr.charge), ("rt", csr.rt)]
+        off, total = _layout(items)
+        if total > PACKED_MAX_BYTES:
+            tensors = csr.to_device(device)
+        else:
+            tensors = _packed_to_device(items, off, total, device)
+            tensors.update(n_clusters=csr.n_clusters, n_spectra=csr.n_spectra, n_peaks=csr.n_peaks)
+        return cls(tensors, csr.cluster_off, csr.spec_off, span, cluster_ids=csr.cluster_ids, titles=csr.titles)
 
     @classmethod
     def from_device(cls, tensors: dict) -> "DeviceBatch":
@@ -98,6 +138,49 @@ class DeviceBatch:
     @property
     def device(self):
         return self.t["mz"].device
+
+
+def _packed_to_device(items, off, total, device):
+    """One pinned staging copy + one H2D for all of ``items``; device views."""
+    import torch
+
+    host = _H2D.take(total)
+    hv = host.numpy()
+    for name, a in items:
+        hv[off[name]:off[name] + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    dev = torch.empty(max(total, 256), dtype=torch.uint8, device=device)
+    dev[:total].copy_(host[:total], non_blocking=True)
+    # ordered before later work on this stream, and waited for here like the
+    # pageable copies it replaces (so any stream may consume the batch)
+    torch.cuda.current_stream(dev.device).synchronize()
+    out = {}
+    for name, a in items:
+        dt = {np.dtype(np.int64): torch.int64, np.dtype(np.float64): torch.float64,
+              np.dtype(np.int32): torch.int32}[a.dtype]
+        out[name] = dev[off[name]:off[name] + a.nbytes].view(dt)
+    return out
+
+
+def _packed_to_host(tensors):
+    """One device concatenation + one D2H of the (name, tensor) list (8-byte
+    dtypes first, so every piece stays aligned); numpy copies."""
+    import torch
+
+    tensors = sorted(tensors, key=lambda nt: -nt[1].element_size())
+    flat = [t.reshape(-1).view(torch.uint8) for _, t in tensors]
+    dev = torch.cat(flat) if flat else torch.zeros(0, dtype=torch.uint8)
+    n = dev.numel()
+    host = _D2H.take(n)
+    host[:n].copy_(dev, non_blocking=True)
+    torch.cuda.current_stream(dev.device).synchronize()
+    hv = host.numpy()
+    res, o = {}, 0
+    for name, t in tensors:
+        nb = t.numel() * t.element_size()
+        np_dt = {torch.int64: np.int64, torch.float64: np.float64, torch.int32: np.int32}[t.dtype]
+        res[name] = hv[o:o + nb].view(np_dt).copy()
+        o += nb
+    return res
 
 
 @dataclass
@@ -136,11 +219,38 @@ class PeaksResult:
         return out_off, dmz[:n], dint[:n]
 
     def to_host(self) -> dict:
+        C, P = self.batch.n_clusters, self.batch.n_peaks
+        if 16 * P + 32 * C <= PACKED_MAX_BYTES:
+            return self._to_host_small()
         out_off, mz, inten = self.compact()
         d = dict(out_off=out_off.cpu().numpy(), out_mz=mz.cpu().numpy(), out_int=inten.cpu().numpy(),
                  status=self.status.cpu().numpy(), prec=self.prec.cpu().numpy(), charge=self.charge.cpu().numpy())
         if self.rt is not None:
             d["rt"] = self.rt.cpu().numpy()
+        return d
+
+    def _to_host_small(self) -> dict:
+        """Small batches: the capacity-layout arrays and the scalars in one D2H
+        (after the producing stream), compacted on the host."""
+        import torch
+
+        C, P = self.batch.n_clusters, self.batch.n_peaks
+        if self.stream is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        items = [("count", self.count[:C]), ("status", self.status[:C]), ("prec", self.prec[:C]),
+                 ("charge", self.charge[:C]), ("mz", self.mz[:P]), ("inten", self.inten[:P])]
+        if self.rt is not None:
+            items.append(("rt", self.rt[:C]))
+        h = _packed_to_host(items)
+        count = h["count"]
+        out_off = np.zeros(C + 1, np.int64)
+        np.cumsum(count, out=out_off[1:])
+        base = self.batch.host_spec_off[self.batch.host_cluster_off[:C]]
+        idx = np.repeat(base - out_off[:-1], count) + np.arange(out_off[-1], dtype=np.int64)
+        d = dict(out_off=out_off, out_mz=h["mz"][idx], out_int=h["inten"][idx], status=h["status"],
+                 prec=h["prec"], charge=h["charge"])
+        if self.rt is not None:
+            d["rt"] = h["rt"]
         return d
 
 
@@ -276,7 +386,10 @@ def xcorr_distance(batch: DeviceBatch, pairs, tolerance=0.1, stream=None):
     spectrum index) pairs; returns a device f64 tensor."""
     import torch
 
-    pairs_t = torch.as_tensor(np.asarray(pairs, np.int64).reshape(-1, 2), device=batch.device).contiguous()
+    if isinstance(pairs, torch.Tensor):
+        pairs_t = pairs.to(device=batch.device, dtype=torch.int64).reshape(-1, 2).contiguous()
+    else:
+        pairs_t = torch.as_tensor(np.asarray(pairs, np.int64).reshape(-1, 2), device=batch.device).contiguous()
     out = torch.empty(max(len(pairs_t), 1), dtype=torch.float64, device=batch.device)
     prm = _lib.SpxMedoidParams(float(tolerance), 0)
     _lib.check(_lib.lib().spx_xcorr_distance(ctypes.byref(batch.csr), ctypes.byref(prm), _ptr(pairs_t),

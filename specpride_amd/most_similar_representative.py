@@ -52,8 +52,22 @@ def distance(spec1, spec2, method="xcorr"):
     m1, m2 = _mz_of(spec1), _mz_of(spec2)
     csr = SpectraCSR.from_clusters([[{"m/z array": m1, "intensity array": np.zeros_like(m1)},
                                      {"m/z array": m2, "intensity array": np.zeros_like(m2)}]])
-    d = engine.xcorr_distance(engine.DeviceBatch.from_host(csr), [(0, 1)], TOLERANCE)
+    batch = engine.DeviceBatch.from_host(csr)
+    d = engine.xcorr_distance(batch, _pair01(batch.device), TOLERANCE)
     return float(d.cpu().numpy()[0])
+
+
+_PAIR01 = {}
+
+
+def _pair01(device):
+    """The device pair (0, 1), made once per device (no H2D per distance call)."""
+    import torch
+
+    t = _PAIR01.get(str(device))
+    if t is None:
+        t = _PAIR01[str(device)] = torch.tensor([[0, 1]], dtype=torch.int64, device=device)
+    return t
 
 
 def _first_runs(names):

@@ -75,6 +75,29 @@ def test_distance_matches_oracle(gpu):
     assert msr.distance([1.0], [2.0], method="other") == 0
 
 
+def test_xcorr_distance_batched_pairs_vs_oracle(gpu):
+    """spx_xcorr_distance over many pairs: the LDS-bitmap path and, for spectra
+    with a bin outside [0, 65,536) (m/z >= 6,553.6 or negative), the scan path."""
+    from specpride_amd import engine
+    from specpride_amd.csr import SpectraCSR
+
+    rng = np.random.default_rng(11)
+    spectra = []
+    for k in range(60):
+        n = int(rng.integers(0, 300))
+        hi = 9000.0 if k % 7 == 3 else 2000.0
+        lo = -5.0 if k % 11 == 5 else 100.0
+        m = np.round(np.sort(rng.uniform(lo, hi, n)), 4)
+        if n > 4 and k % 5 == 0:
+            m[1] = m[0]  # a repeated bin inside one spectrum
+        spectra.append(m)
+    csr = SpectraCSR.from_clusters([[{"m/z array": m, "intensity array": np.ones_like(m)} for m in spectra]])
+    pairs = [(i, j) for i in range(60) for j in range(i, 60) if (i * 7 + j) % 3 == 0]
+    got = engine.xcorr_distance(engine.DeviceBatch.from_host(csr), pairs, 0.1).cpu().numpy()
+    want = np.array([1.0 - np_oracle.xcorr(spectra[i], spectra[j], 0.1) for i, j in pairs])
+    np.testing.assert_array_equal(got, want)
+
+
 def test_average_spectrum_per_cluster_vs_golden(gpu):
     z, csr = load_golden("gap_average_edge.npz")
     kw = gap_params(z)
