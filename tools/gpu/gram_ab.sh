@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for v in ${VARIANTS:-gramlds nb2 nb4}; do
+for v in ${VARIANTS:?set VARIANTS to the ab_<name>.so builds to compare}; do
   SPX_LIB="$R/specpride_amd/lib/ab_$v.so" timeout -k 10 300 python tools/bench_medoid_large.py --reps 5 --check > gpurun_out/gram_$v.log 2>&1 || { echo "variant $v failed"; tail -5 gpurun_out/gram_$v.log; exit 1; }
   echo "$v $(tail -1 gpurun_out/gram_$v.log)"
 done
