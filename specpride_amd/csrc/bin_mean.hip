@@ -61,7 +61,7 @@ struct BinMeanState {
 #define SPX_BM_MINW 4  // __launch_bounds__ minimum waves per SIMD for bin_mean_lds_kernel (the leftovers)
 #endif
 #ifndef SPX_BR_MINW
-#define SPX_BR_MINW 5  // the same for bin_mean_reg_kernel (48 register codes)
+#define SPX_BR_MINW 5  // the same for bin_mean_reg_kernel (50 register codes)
 #endif
 #ifndef SPX_BM_PF
 #define SPX_BM_PF 10  // spectra in flight per thread in the fast path's register ring
@@ -463,7 +463,7 @@ __device__ __forceinline__ int32_t bin_mean_body(const CsrView& v, const BinMean
 // A key inversion or NaN inside a spectrum sends the cluster to the generic
 // kernel.  Returns kNotHere when the cluster does not fit this path.
 #ifndef SPX_BR_NMAX
-#define SPX_BR_NMAX 48
+#define SPX_BR_NMAX 50
 #endif
 constexpr int BR_NMAX = SPX_BR_NMAX;  // spectra per cluster: one code VGPR each
 constexpr int BR_PFA = 8;             // phase-A m/z loads in flight per lane
@@ -505,32 +505,10 @@ __device__ __forceinline__ void unrolled_while(int n, F&& f, std::integer_sequen
   (void)((more(Js) ? (f(std::integral_constant<int, Js>{}), true) : false) && ...);
 }
 
-// The same over pairs of steps: f(2k) and f(2k+1) share one guard (2k < n), so
-// the two steps are one basic block and their dependency chains interleave.
-// Only for steps that are harmless past n (their lanes contribute nothing).
-template <class F, int... Ks>
-__device__ __forceinline__ void unrolled_pairs(int n, F&& f, std::integer_sequence<int, Ks...>) {
-  int nn = __builtin_amdgcn_readfirstlane(n);
-  auto more = [&](int j) __attribute__((always_inline)) {
-    asm volatile("" : "+s"(nn));
-    return j < nn;
-  };
-  auto pair = [&](auto kc) __attribute__((always_inline)) {
-    constexpr int k = decltype(kc)::value;
-    f(std::integral_constant<int, 2 * k>{});
-    f(std::integral_constant<int, 2 * k + 1>{});
-  };
-  (void)((more(2 * Ks) ? (pair(std::integral_constant<int, Ks>{}), true) : false) && ...);
-}
-#ifndef SPX_BR_PAIRS
-#define SPX_BR_PAIRS 0  // bit 0: phase A in pairs, bit 1: phase B, bit 2: phase C
-#endif
-template <int kBit, class F>
+// the register path's step loops: n <= BR_NMAX steps, uniform early exit
+template <class F>
 __device__ __forceinline__ void reg_steps(int n, F&& f) {
-  if constexpr ((SPX_BR_PAIRS >> kBit) & 1)
-    unrolled_pairs(n, f, std::make_integer_sequence<int, BR_NMAX / 2>{});
-  else
-    unrolled_while(n, f, std::make_integer_sequence<int, BR_NMAX>{});
+  unrolled_while(n, f, std::make_integer_sequence<int, BR_NMAX>{});
 }
 
 __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const BinMeanParams& P, BinRegSmem& L,
@@ -598,7 +576,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
 #pragma unroll
     for (int j = 0; j < BR_NMAX; ++j) code[j] = -1;
-    reg_steps<0>(n, [&](auto jc) __attribute__((always_inline)) {
+    reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       const double m = ra[j % BR_PFA];
       const int len = rl[j % BR_PFA];
@@ -636,7 +614,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   for (int d = tid; d < D; d += BM_BLOCK) L.cnt[d] = 0u;
   if (tid < kWave) L.cnt[BM_DCAP + tid] = 0u;
   lds_barrier();
-  reg_steps<1>(n, [&](auto jc) __attribute__((always_inline)) {
+  reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     const bool valid = code[j] >= 0;
     const uint32_t b = (uint32_t)(valid ? code[j] : 0);
@@ -651,7 +629,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   SPX_STAMP(3);
 
   // ---- C: the ordered fold (spectrum order per slot = the reference's order)
-  reg_steps<2>(n, [&](auto jc) __attribute__((always_inline)) {
+  reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     const double m = rm[j % BR_PFC], it = ri[j % BR_PFC];
     const uint32_t bo = boff(j + BR_PFC);
