@@ -466,14 +466,20 @@ __device__ __forceinline__ int32_t bin_mean_body(const CsrView& v, const BinMean
 #define SPX_BR_NMAX 50
 #endif
 constexpr int BR_NMAX = SPX_BR_NMAX;  // spectra per cluster: one code VGPR each
-constexpr int BR_PFA = 8;             // phase-A m/z loads in flight per lane
-constexpr int BR_PFC = 4;             // phase-C (m/z, intensity) loads in flight per lane
+#ifndef SPX_BR_PFA
+#define SPX_BR_PFA 8
+#endif
+#ifndef SPX_BR_PFC
+#define SPX_BR_PFC 4
+#endif
+constexpr int BR_PFA = SPX_BR_PFA;    // phase-A m/z loads in flight per lane
+constexpr int BR_PFC = SPX_BR_PFC;    // phase-C (m/z, intensity) loads in flight per lane
 constexpr int BR_W32 = 2 * BM_WMAX;   // 32-bit occupancy words
 
 // LDS of the register path.  The occupancy bitmap (32-bit words + per-word rank
 // prefix) is dead once every code is a slot, so the accumulators overlay it.
 struct BinRegSmem {
-  union {
+  union alignas(16) {
     struct {
       uint32_t bits[BR_W32];
       uint16_t pre[BR_W32];
@@ -487,6 +493,38 @@ struct BinRegSmem {
   int tmp[BM_BLOCK / kWave + 1];
 };
 constexpr int32_t kNotHere = -1;
+
+// Exclusive popcount prefix over ALL BR_W32 occupancy words (BR_W32 / 256 = 12
+// contiguous words per thread): three ds_read_b128 per thread -- the 48-B lane
+// stride puts each 16-lane group on 16 distinct 16-B bank slots, conflict-free --
+// and the u16 prefixes written as three quads.  Words past the batch's bin range
+// are zero (the set-up clears all BR_W32).  Returns the number of occupied bins.
+constexpr int BR_WPT = BR_W32 / BM_BLOCK;
+static_assert(BR_WPT == 12, "reg_prefix reads three b128 quads per thread");
+__device__ __forceinline__ int reg_prefix(BinRegSmem& L) {
+  const uint4* src = reinterpret_cast<const uint4*>(L.u.b.bits) + threadIdx.x * (BR_WPT / 4);
+  uint32_t w[BR_WPT];
+#pragma unroll
+  for (int k = 0; k < BR_WPT / 4; ++k) {
+    const uint4 q = src[k];
+    w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
+  }
+  int local = 0;
+#pragma unroll
+  for (int k = 0; k < BR_WPT; ++k) local += __popc(w[k]);
+  int total;
+  int base = block_exclusive_scan<BM_BLOCK, int, true, false>(local, L.tmp, total);
+  uint2* dst = reinterpret_cast<uint2*>(L.u.b.pre) + threadIdx.x * (BR_WPT / 4);
+#pragma unroll
+  for (int k = 0; k < BR_WPT / 4; ++k) {
+    uint32_t p[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { p[i] = (uint32_t)base; base += __popc(w[4 * k + i]); }
+    dst[k] = make_uint2(p[0] | (p[1] << 16), p[2] | (p[3] << 16));
+  }
+  lds_barrier();
+  return total;
+}
 
 // f(integral_constant<int, J>) for J = 0, 1, ... while J < n (n <= sizeof...(Js)):
 // a compile-time-unrolled loop with a uniform early exit.  Register arrays are
@@ -533,8 +571,11 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     return kMixedCharge;
   }
   if (wid == 0 && mine) L.prec[lane] = pl;
-  const int nw32 = 2 * P.n_words;
-  for (int w = tid; w < nw32; w += BM_BLOCK) L.u.b.bits[w] = 0u;
+  {
+    uint4* z = reinterpret_cast<uint4*>(L.u.b.bits) + tid * (BR_WPT / 4);
+#pragma unroll
+    for (int k = 0; k < BR_WPT / 4; ++k) z[k] = make_uint4(0u, 0u, 0u, 0u);
+  }
   lds_barrier();
   SPX_STAMP(1);
 
@@ -552,7 +593,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     const int jj = j < n ? j : n - 1;
     const int a = __builtin_amdgcn_readlane(rlo, jj), e = __builtin_amdgcn_readlane(rhi, jj);
     const int k = a + fpos;
-    return (j < n && k < e) ? (uint32_t)k * 8u : 0u;
+    return k < e ? (uint32_t)k * 8u : 0u;
   };
   auto ld = [&](const char* base, uint32_t bo) -> double { return *reinterpret_cast<const double*>(base + bo); };
 
@@ -565,12 +606,14 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     // once, when the load is issued)
     double ra[BR_PFA];
     int rl[BR_PFA];
+    // a step past the cluster's last spectrum (never executed) re-reads the last
+    // spectrum: no per-step "j < n" lane mask to keep
     auto fetch = [&](int j, double& m, int& len) __attribute__((always_inline)) {
       const int jj = j < n ? j : n - 1;
       const int a = __builtin_amdgcn_readlane(rlo, jj), e = __builtin_amdgcn_readlane(rhi, jj);
       const int k = a + fpos;
-      len = j < n ? e - a : 0;
-      m = ld(mzb, (j < n && k < e) ? (uint32_t)k * 8u : 0u);
+      len = e - a;
+      m = ld(mzb, k < e ? (uint32_t)k * 8u : 0u);
     };
 #pragma unroll
     for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
@@ -583,7 +626,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       fetch(j + BR_PFA, ra[j % BR_PFA], rl[j % BR_PFA]);
       const bool act = fpos < len;
       const bool inr = act & (m >= P.minimum) & (m < P.maximum);
-      const int32_t kb = bin_small(inr ? m : P.minimum, P);
+      const int32_t kb = bin_small(m, P);  // used only where inr
       // inactive lanes (past the spectrum's end) carry INT_MAX: the last active
       // peak's neighbour then always differs from it, and never sorts below it
       const int32_t key = inr ? kb : ((act & (m < P.minimum)) ? -1 : 0x7fffffff);
@@ -594,6 +637,9 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       // LDS atomics serialise; distinct words do not)
       atomicOr(&bm32[valid ? key >> 5 : lane], valid ? 1u << (key & 31) : 0u);
       code[j] = valid ? key : -1;
+      // opaque to the compiler: phase B re-tests code >= 0 by a compare instead of
+      // keeping each step's 64-bit valid mask live (50 SGPR pairs: spills)
+      asm volatile("" : "+v"(code[j]));
     });
   }
   // phase C's first (m/z, intensity) loads go out now and land during phase B
@@ -609,7 +655,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   SPX_STAMP(2);
 
   // ---- B: slots in bin order, codes -> slots, contribution counts
-  const int D = bitmap_prefix32<BM_BLOCK>(L.u.b.bits, L.u.b.pre, nw32, L.tmp);
+  const int D = reg_prefix(L);
   if (D > BM_DCAP) return kDeferred;
   for (int d = tid; d < D; d += BM_BLOCK) L.cnt[d] = 0u;
   if (tid < kWave) L.cnt[BM_DCAP + tid] = 0u;
