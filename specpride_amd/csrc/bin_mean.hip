@@ -140,10 +140,10 @@ __device__ __forceinline__ void sorted_lane(const BinMeanState<PrefixT, CountT>&
 // earlier stripes + kept in earlier waves of its stripe + earlier lanes of its wave
 // (ballot).  Per-(stripe, wave) counts go to `wcnt` (the dead bitmap): one barrier.
 // Returns the number of peaks written.
-template <class CountT, class AccI, class AccM>
-__device__ __forceinline__ int emit_striped(const CountT* cnt, const AccI& acc_i, const AccM& acc_m, int* wcnt,
-                                            int D, uint32_t quorum, double* __restrict__ omz,
-                                            double* __restrict__ oint) {
+template <class Cnt, class AccI, class AccM>
+__device__ __forceinline__ int emit_striped_f(const Cnt& cnt, const AccI& acc_i, const AccM& acc_m, int* wcnt,
+                                              int D, uint32_t quorum, double* __restrict__ omz,
+                                              double* __restrict__ oint) {
   constexpr int NW = BM_BLOCK / kWave;
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
   const int per = (D + BM_BLOCK - 1) / BM_BLOCK;  // <= BM_DCAP / BM_BLOCK
@@ -151,7 +151,7 @@ __device__ __forceinline__ int emit_striped(const CountT* cnt, const AccI& acc_i
   uint32_t keep = 0u;  // bit j: slot j*256 + tid is emitted
   for (int j = 0; j < per; ++j) {
     const int d = j * BM_BLOCK + tid;
-    const bool k = d < D && (uint32_t)cnt[d] >= quorum && !isnan(acc_i(d));  // cnt >= 1: mean NaN iff sum NaN
+    const bool k = d < D && (uint32_t)cnt(d) >= quorum && !isnan(acc_i(d));  // cnt >= 1: mean NaN iff sum NaN
     const unsigned long long b = __ballot(k);
     if (lane == 0) wcnt[j * NW + wid] = __popcll(b);
     keep |= (uint32_t)k << j;
@@ -171,7 +171,7 @@ __device__ __forceinline__ int emit_striped(const CountT* cnt, const AccI& acc_i
     if (k) {
       const int d = j * BM_BLOCK + tid;
       const int o = base + before + __popcll(b & below);
-      const double cn = (double)cnt[d];
+      const double cn = (double)cnt(d);
       const float si = acc_i(d), sm = acc_m(d);
       oint[o] = (double)si / cn;
       omz[o] = sm == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)sm / cn;
@@ -179,6 +179,12 @@ __device__ __forceinline__ int emit_striped(const CountT* cnt, const AccI& acc_i
     base += tot;
   }
   return base;
+}
+template <class CountT, class AccI, class AccM>
+__device__ __forceinline__ int emit_striped(const CountT* cnt, const AccI& acc_i, const AccM& acc_m, int* wcnt,
+                                            int D, uint32_t quorum, double* __restrict__ omz,
+                                            double* __restrict__ oint) {
+  return emit_striped_f([&](int d) { return (uint32_t)cnt[d]; }, acc_i, acc_m, wcnt, D, quorum, omz, oint);
 }
 
 template <bool kSmall, class PrefixT, class CountT>
@@ -454,11 +460,13 @@ __device__ __forceinline__ int32_t bin_mean_body(const CsrView& v, const BinMean
 //      bin, DPP neighbour key -> last-in-bin (numpy fancy-index "+=" keeps the
 //      last, binning.py:197-199), occupancy bitmap (32-bit LDS atomics), and
 //      code[j] = bin of the contribution (-1: none)
-//   B  popcount prefix -> slot per bin in ascending order; codes -> slots, the
-//      per-slot contribution count by LDS atomics (integer: order-free)
-//   C  spectra in order: I = f32(f64(I) + inten), M = f32(f64(M) + mz) of each
-//      contribution's slot -- the reference's float32 accumulation order
-//      (binning.py:198-199); one LDS-only barrier per spectrum
+//   B  popcount prefix -> slot per bin in ascending order; codes -> slots
+//   C  spectra in order: I = f32(f64(I) + inten), M = f32(f64(M) + mz) and the
+//      count of each contribution's slot (one 16-B LDS record) -- the reference's
+//      float32 accumulation order (binning.py:198-199); one LDS-only barrier per
+//      spectrum
+// The step masks never live in SGPRs across phases (the codes are opaque to the
+// compiler after A): 50 kept masks spilled SGPRs into VGPR lanes and cost ~10%.
 //   D  quorum + ordered output (emit_striped), precursor mean
 // A key inversion or NaN inside a spectrum sends the cluster to the generic
 // kernel.  Returns kNotHere when the cluster does not fit this path.
@@ -475,6 +483,11 @@ constexpr int BR_NMAX = SPX_BR_NMAX;  // spectra per cluster: one code VGPR each
 constexpr int BR_PFA = SPX_BR_PFA;    // phase-A m/z loads in flight per lane
 constexpr int BR_PFC = SPX_BR_PFC;    // phase-C (m/z, intensity) loads in flight per lane
 constexpr int BR_W32 = 2 * BM_WMAX;   // 32-bit occupancy words
+// phases C-D accumulator of one slot: (intensity, m/z) sums and the contribution count
+struct alignas(16) BinAcc {
+  float i, m;
+  uint32_t n, pad;
+};
 
 // LDS of the register path.  The occupancy bitmap (32-bit words + per-word rank
 // prefix) is dead once every code is a slot, so the accumulators overlay it.
@@ -484,9 +497,8 @@ struct BinRegSmem {
       uint32_t bits[BR_W32];
       uint16_t pre[BR_W32];
     } b;                         // phases A-B
-    float2 acc[BM_DCAP + kWave];  // phases C-D: (intensity, m/z) sums; [BM_DCAP + lane]: dummies
+    BinAcc acc[BM_DCAP + kWave];  // phases C-D; [BM_DCAP + lane]: dummies
   } u;
-  uint32_t cnt[BM_DCAP + kWave];  // contributions per slot; [BM_DCAP + lane]: dummies
   double prec[BR_NMAX];
   int wcnt[(BM_DCAP / BM_BLOCK) * (BM_BLOCK / kWave)];  // emit: kept slots per (stripe, wave)
   int votes[2 * (BM_BLOCK / kWave)];
@@ -581,21 +593,18 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 
   const int fpos = wid * (kWave - 1) + lane;  // this lane's peak in every spectrum
   const bool owner = lane < kWave - 1;
-  const char* __restrict__ mzb = reinterpret_cast<const char*>(v.mz + p0);
-  const char* __restrict__ itb = reinterpret_cast<const char*>(v.inten + p0);
-  // cluster-relative byte offset of this lane's peak of spectrum j (0 past its
-  // end: the cluster's first peak, in bounds since the cluster has peaks)
-  // Spectra past the cluster's last (j >= n, a ring's tail prefetch) map every
-  // lane to byte 0: one cache line per wave, so the ring's loads are unconditional
-  // (a conditional load makes its ring register a merge of two values, which
-  // compiles to a wait for the load right after issuing it).
-  auto boff = [&](int j) -> uint32_t {
+  // Buffer descriptors over the cluster's peaks.  A lane past its spectrum's end
+  // reads the next spectrum's peak, or 0 past the cluster's end (out of the
+  // descriptor's range: no fault), so the offsets need no select; spectra past
+  // the cluster's last (j >= n, a ring's tail prefetch) re-read the last one.
+  // The ring's loads are unconditional (a conditional load makes its ring
+  // register a merge of two values, which compiles to a wait right after issue).
+  const __amdgpu_buffer_rsrc_t rmz = bf_rsrc(v.mz + p0, (int)(p1 - p0));
+  const __amdgpu_buffer_rsrc_t rit = bf_rsrc(v.inten + p0, (int)(p1 - p0));
+  auto boffb = [&](int j) -> int {  // byte offset of this lane's peak of spectrum j
     const int jj = j < n ? j : n - 1;
-    const int a = __builtin_amdgcn_readlane(rlo, jj), e = __builtin_amdgcn_readlane(rhi, jj);
-    const int k = a + fpos;
-    return k < e ? (uint32_t)k * 8u : 0u;
+    return (__builtin_amdgcn_readlane(rlo, jj) + fpos) * 8;
   };
-  auto ld = [&](const char* base, uint32_t bo) -> double { return *reinterpret_cast<const double*>(base + bo); };
 
   // ---- A: bins, last-in-bin, occupancy, codes (branch-free per lane)
   int32_t code[BR_NMAX];
@@ -606,14 +615,12 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     // once, when the load is issued)
     double ra[BR_PFA];
     int rl[BR_PFA];
-    // a step past the cluster's last spectrum (never executed) re-reads the last
-    // spectrum: no per-step "j < n" lane mask to keep
     auto fetch = [&](int j, double& m, int& len) __attribute__((always_inline)) {
       const int jj = j < n ? j : n - 1;
       const int a = __builtin_amdgcn_readlane(rlo, jj), e = __builtin_amdgcn_readlane(rhi, jj);
       const int k = a + fpos;
       len = e - a;
-      m = ld(mzb, k < e ? (uint32_t)k * 8u : 0u);
+      m = bf_load(rmz, k * 8, 0);
     };
 #pragma unroll
     for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
@@ -647,19 +654,17 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   double rm[BR_PFC], ri[BR_PFC];
 #pragma unroll
   for (int j = 0; j < BR_PFC; ++j) {
-    const uint32_t bo = boff(j);
-    rm[j] = ld(mzb, bo);
-    ri[j] = ld(itb, bo);
+    const int bo = boffb(j);
+    rm[j] = bf_load(rmz, bo, 0);
+    ri[j] = bf_load(rit, bo, 0);
   }
   if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
   SPX_STAMP(2);
 
-  // ---- B: slots in bin order, codes -> slots, contribution counts
+  // ---- B: slots in bin order, codes -> slots (the contribution count rides
+  // phase C's read-modify-write)
   const int D = reg_prefix(L);
   if (D > BM_DCAP) return kDeferred;
-  for (int d = tid; d < D; d += BM_BLOCK) L.cnt[d] = 0u;
-  if (tid < kWave) L.cnt[BM_DCAP + tid] = 0u;
-  lds_barrier();
   reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     const bool valid = code[j] >= 0;
@@ -667,10 +672,9 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     const uint32_t w = b >> 5;
     const int slot = (int)L.u.b.pre[w] + __popc(L.u.b.bits[w] & ((1u << (b & 31)) - 1u));
     code[j] = valid ? slot : BM_DCAP + lane;  // a dummy slot of its own, never read
-    atomicAdd(&L.cnt[code[j]], valid ? 1u : 0u);
   });
   lds_barrier();  // the bitmap is dead: the accumulators take its place
-  for (int d = tid; d < D; d += BM_BLOCK) L.u.acc[d] = make_float2(0.0f, 0.0f);
+  for (int d = tid; d < D; d += BM_BLOCK) L.u.acc[d] = BinAcc{0.0f, 0.0f, 0u, 0u};
   lds_barrier();
   SPX_STAMP(3);
 
@@ -678,13 +682,14 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     const double m = rm[j % BR_PFC], it = ri[j % BR_PFC];
-    const uint32_t bo = boff(j + BR_PFC);
-    rm[j % BR_PFC] = ld(mzb, bo);
-    ri[j % BR_PFC] = ld(itb, bo);
+    const int bo = boffb(j + BR_PFC);
+    rm[j % BR_PFC] = bf_load(rmz, bo, 0);
+    ri[j % BR_PFC] = bf_load(rit, bo, 0);
     const int slot = code[j];
-    float2 a = L.u.acc[slot];
-    a.x = (float)((double)a.x + it);
-    a.y = (float)((double)a.y + m);
+    BinAcc a = L.u.acc[slot];
+    a.i = (float)((double)a.i + it);
+    a.m = (float)((double)a.m + m);
+    a.n += 1u;
     L.u.acc[slot] = a;
     lds_barrier();
   });
@@ -692,8 +697,9 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 
   // ---- D: quorum filter and ordered output (binning.py:181-183, 209-222)
   const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
-  const int total = emit_striped(L.cnt, [&](int d) { return L.u.acc[d].x; }, [&](int d) { return L.u.acc[d].y; },
-                                 L.wcnt, D, quorum, out.mz + p0, out.inten + p0);
+  const int total = emit_striped_f([&](int d) { return L.u.acc[d].n; }, [&](int d) { return L.u.acc[d].i; },
+                                   [&](int d) { return L.u.acc[d].m; }, L.wcnt, D, quorum, out.mz + p0,
+                                   out.inten + p0);
   if (tid == 0) {
     out.count[c] = total;
     charge_out[c] = z0;
