@@ -49,6 +49,32 @@ constexpr int GA_NW = GA_BLOCK / kWave;
 constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10,240 per cluster: n <= 51 at ~200 peaks)
 constexpr int GA_WMAX = 3584;  // 229,376 buckets (2,293 Da at 0.01)
 constexpr int GA_DCAP = 1536;  // occupied buckets per cluster
+static_assert(GA_WMAX % GA_BLOCK == 0, "the LDS bitmap is whole words per thread");
+
+// Exclusive popcount prefix over ALL of an LDS bitmap of BLOCK * WPT u64 words
+// (words past the cluster's range are zero): each thread's WPT contiguous words
+// are read unconditionally (the reads pipeline: one wait, not one per word) --
+// the 8*WPT-B lane stride is bank-conflict-free for odd WPT -- then one block
+// scan and the u16 prefixes.  Returns the number of set bits.
+template <int BLOCK, int WPT>
+__device__ __forceinline__ int bitmap_prefix_fixed(const unsigned long long* bm, uint16_t* pref, int* tmp) {
+  const int w0 = threadIdx.x * WPT;
+  unsigned long long w[WPT];
+#pragma unroll
+  for (int k = 0; k < WPT; ++k) w[k] = bm[w0 + k];
+  int local = 0;
+#pragma unroll
+  for (int k = 0; k < WPT; ++k) local += __popcll(w[k]);
+  int total;
+  int base = block_exclusive_scan<BLOCK, int, true>(local, tmp, total);
+#pragma unroll
+  for (int k = 0; k < WPT; ++k) {
+    pref[w0 + k] = (uint16_t)base;
+    base += __popcll(w[k]);
+  }
+  lds_barrier();
+  return total;
+}
 
 template <class PrefixT>
 struct GapState {
@@ -434,7 +460,12 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   if (nw > S.wcap) return kDeferred;
 
   // 2: occupied buckets
-  for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
+  if constexpr (kL) {  // the whole LDS bitmap (the fixed-size prefix reads all of it)
+#pragma unroll
+    for (int k = 0; k < GA_WMAX / GA_BLOCK; ++k) S.bitmap[k * GA_BLOCK + tid] = 0ull;
+  } else {
+    for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
+  }
   bar();
   auto pass2 = [&](double m, double, int32_t& tag) __attribute__((always_inline)) {
     const int64_t b = floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
@@ -444,7 +475,9 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   };
   peaks_m_tag(pass2);
   bar();
-  const int D = bitmap_prefix<GA_BLOCK, PrefixT, kL>(S.bitmap, S.wprefix, (int)nw, tmp);
+  int D;
+  if constexpr (kL) D = bitmap_prefix_fixed<GA_BLOCK, GA_WMAX / GA_BLOCK>(S.bitmap, S.wprefix, tmp);
+  else D = bitmap_prefix<GA_BLOCK, PrefixT, kL>(S.bitmap, S.wprefix, (int)nw, tmp);
   if (D > S.dcap) return kDeferred;
   SPX_STAMP(3);
   for (int d = tid; d < D; d += GA_BLOCK) {
