@@ -293,16 +293,21 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   // P2: compact columns (exclusive popcount prefix into the records)
   int K;
   {
-    const int per = (nw + MD_BLOCK - 1) / MD_BLOCK, w0 = tid * per;
+    // all MR_WMAX records (P0 cleared them; bins stop below nw * 64), RPT
+    // contiguous per thread, read unconditionally: the reads pipeline
+    constexpr int RPT = MR_WMAX / MD_BLOCK;
+    const int w0 = tid * RPT;
+    unsigned long long b[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) b[k] = L.u.a.rec[w0 + k].bits;
     int local = 0;
-    for (int k = 0; k < per; ++k)
-      if (w0 + k < nw) local += __popcll(L.u.a.rec[w0 + k].bits);
-    int base = block_exclusive_scan<MD_BLOCK>(local, L.tmp, K);
-    for (int k = 0; k < per; ++k) {
-      if (w0 + k < nw) {
-        L.u.a.rec[w0 + k].pre = (uint32_t)base;
-        base += __popcll(L.u.a.rec[w0 + k].bits);
-      }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) local += __popcll(b[k]);
+    int base = block_exclusive_scan<MD_BLOCK, int, true>(local, L.tmp, K);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      L.u.a.rec[w0 + k].pre = (uint32_t)base;
+      base += __popcll(b[k]);
     }
   }
   // row stride KW is odd: lanes reading rows j, j+1, ... at one word hit
