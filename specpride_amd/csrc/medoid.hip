@@ -203,7 +203,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   for (int w = tid; w < nsw; w += MD_BLOCK) L.u.a.sbits[w] = 0ull;
   if (tid <= n) L.soff[tid] = (int32_t)(v.spec_off[s0 + tid] - p0);
   for (int w = tid; w < MR_WMAX; w += MD_BLOCK) L.u.a.rec[w].bits = 0ull;
-  if (tid == 0) L.red[0] = 0;
   __syncthreads();
   if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
     const bool empty_spec = tid < n && L.soff[tid + 1] == L.soff[tid];
@@ -234,7 +233,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   // value, and the compiler waits with counted vmcnt.
   uint32_t bins[MR_UMAX / 2];
   int outside = 0;
-  uint32_t bmax = 0u;
   constexpr uint32_t kBins = (uint32_t)MR_WMAX * 64u;
   constexpr int NB = MR_UMAX / 8;
   auto pass1 = [&](auto nbt_c) __attribute__((always_inline)) {
@@ -262,7 +260,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
               outside = 1;
             } else {
               b = (uint32_t)bb;
-              bmax = b > bmax ? b : bmax;
               // 32-bit half of the occupancy word (same-address LDS atomics serialise)
               atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rec[b >> 6].bits) + ((b >> 5) & 1), 1u << (b & 31));
             }
@@ -283,17 +280,15 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     default: pass1(std::integral_constant<int, NB>{}); break;
   }
   static_assert(NB == 6, "size classes above cover MR_UMAX = 48");
-  if (bmax) atomicMax(reinterpret_cast<int*>(&L.red[0]), (int)bmax);
   if (__syncthreads_or(outside)) {  // m/z out of the LDS bitmap's range: general path
     if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
     return;
   }
-  const int nw = np > 0 ? (int)(L.red[0] >> 6) + 1 : 0;
   SPX_STAMP(2);
   // P2: compact columns (exclusive popcount prefix into the records)
   int K;
   {
-    // all MR_WMAX records (P0 cleared them; bins stop below nw * 64), RPT
+    // all MR_WMAX records (P0 cleared them), RPT
     // contiguous per thread, read unconditionally: the reads pipeline
     constexpr int RPT = MR_WMAX / MD_BLOCK;
     const int w0 = tid * RPT;
