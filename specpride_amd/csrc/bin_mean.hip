@@ -482,6 +482,13 @@ constexpr int BR_NMAX = SPX_BR_NMAX;  // spectra per cluster: one code VGPR each
 #endif
 constexpr int BR_PFA = SPX_BR_PFA;    // phase-A m/z loads in flight per lane
 constexpr int BR_PFC = SPX_BR_PFC;    // phase-C (m/z, intensity) loads in flight per lane
+#ifndef SPX_BR_KM
+#define SPX_BR_KM 6
+#endif
+// Spectra whose m/z phase A keeps in registers for phase C (no re-read for them):
+// 6 fit the 96 VGPRs of 5 waves/SIMD (2.24 -> 2.20 ms at 100k clusters); 12 or 20
+// at 4 waves/SIMD measured 2.28 / 2.23 ms (fewer clusters in flight)
+constexpr int BR_KM = SPX_BR_KM;
 constexpr int BR_W32 = 2 * BM_WMAX;   // 32-bit occupancy words
 // phases C-D accumulator of one slot: (intensity, m/z) sums and the contribution count
 struct alignas(16) BinAcc {
@@ -608,6 +615,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 
   // ---- A: bins, last-in-bin, occupancy, codes (branch-free per lane)
   int32_t code[BR_NMAX];
+  double mk[BR_KM > 0 ? BR_KM : 1];  // m/z of spectra 0..BR_KM-1, kept from phase A
   uint32_t* bm32 = L.u.b.bits;
   int bad = 0;
   {
@@ -629,6 +637,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       const double m = ra[j % BR_PFA];
+      if constexpr (j < BR_KM) mk[j] = m;
       const int len = rl[j % BR_PFA];
       fetch(j + BR_PFA, ra[j % BR_PFA], rl[j % BR_PFA]);
       const bool act = fpos < len;
@@ -655,7 +664,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 #pragma unroll
   for (int j = 0; j < BR_PFC; ++j) {
     const int bo = boffb(j);
-    rm[j] = bf_load(rmz, bo, 0);
+    if (j >= BR_KM) rm[j] = bf_load(rmz, bo, 0);
     ri[j] = bf_load(rit, bo, 0);
   }
   if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
@@ -681,9 +690,12 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   // ---- C: the ordered fold (spectrum order per slot = the reference's order)
   reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    const double m = rm[j % BR_PFC], it = ri[j % BR_PFC];
+    double m;
+    if constexpr (j < BR_KM) m = mk[j];
+    else m = rm[j % BR_PFC];
+    const double it = ri[j % BR_PFC];
     const int bo = boffb(j + BR_PFC);
-    rm[j % BR_PFC] = bf_load(rmz, bo, 0);
+    if constexpr (j + BR_PFC >= BR_KM) rm[j % BR_PFC] = bf_load(rmz, bo, 0);
     ri[j % BR_PFC] = bf_load(rit, bo, 0);
     const int slot = code[j];
     BinAcc a = L.u.acc[slot];
