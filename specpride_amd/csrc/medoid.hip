@@ -166,6 +166,7 @@ struct MedoidRegSmem {
   double totals[MD_NMAX];
   int tmp[MD_BLOCK / kWave + 1];
   long long red[4];
+  int votes[2 * (MD_BLOCK / kWave)];
 };
 
 __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
@@ -280,7 +281,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     default: pass1(std::integral_constant<int, NB>{}); break;
   }
   static_assert(NB == 6, "size classes above cover MR_UMAX = 48");
-  if (__syncthreads_or(outside)) {  // m/z out of the LDS bitmap's range: general path
+  if (block_any<MD_BLOCK, true>(outside, L.votes, 0)) {  // m/z out of the LDS bitmap's range: general path
     if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
     return;
   }
