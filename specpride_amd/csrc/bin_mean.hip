@@ -478,16 +478,17 @@ constexpr int BR_NMAX = SPX_BR_NMAX;  // spectra per cluster: one code VGPR each
 #define SPX_BR_PFA 8
 #endif
 #ifndef SPX_BR_PFC
-#define SPX_BR_PFC 4
+#define SPX_BR_PFC 3
 #endif
 constexpr int BR_PFA = SPX_BR_PFA;    // phase-A m/z loads in flight per lane
 constexpr int BR_PFC = SPX_BR_PFC;    // phase-C (m/z, intensity) loads in flight per lane
 #ifndef SPX_BR_KM
-#define SPX_BR_KM 6
+#define SPX_BR_KM 8
 #endif
 // Spectra whose m/z phase A keeps in registers for phase C (no re-read for them):
-// 6 fit the 96 VGPRs of 5 waves/SIMD (2.24 -> 2.20 ms at 100k clusters); 12 or 20
-// at 4 waves/SIMD measured 2.28 / 2.23 ms (fewer clusters in flight)
+// 8 with a 3-deep phase-C ring fit the 96 VGPRs of 5 waves/SIMD (100k clusters:
+// none 2.24, 6 2.20, 8 2.14 ms); 12 or 20 at 4 waves/SIMD measured 2.28 / 2.23 ms
+// (fewer clusters in flight)
 constexpr int BR_KM = SPX_BR_KM;
 constexpr int BR_W32 = 2 * BM_WMAX;   // 32-bit occupancy words
 // phases C-D accumulator of one slot: (intensity, m/z) sums and the contribution count
