@@ -124,9 +124,9 @@ __device__ __forceinline__ void md_defer(int64_t c, int64_t s0, int n, int32_t* 
 //       in registers as packed u16 (<= MR_UMAX per thread), union bitmap in LDS
 //       (32-bit LDS atomics).  The xcorr is a set intersection: no range pass,
 //       and unsorted spectra need no special path.
-//   P2  popcount prefix -> K compact columns; bitmap word and prefix share one
-//       16-byte record, so a rank is one ds_read_b128
-//   P3  bit-packed rows from the register bins: column = rank (one LDS read),
+//   P2  popcount prefix -> K compact columns (dense word and prefix arrays:
+//       bank-conflict-light ORs and rank reads)
+//   P3  bit-packed rows from the register bins: column = rank (two LDS reads),
 //       spectrum = the wave's start-bit word and its prefix, handed out by
 //       readlane (a wave's 64 peaks of a slice are one start-bit word); rows
 //       are set by 32-bit LDS atomics (neighbouring peaks share a row word)
@@ -147,15 +147,16 @@ constexpr int MR_PMAX = MR_UMAX * MD_BLOCK;
 constexpr int MR_WMAX = 512;                 // union-bitmap words: bins < 32,768 (m/z < 3,276.8 at 0.1)
 constexpr int MR_TRI = MD_NMAX * (MD_NMAX + 1) / 2;  // packed upper triangle of the distance matrix
 
-struct MrRec {
-  unsigned long long bits;
-  uint32_t pre, pad;
-};
 
 struct MedoidRegSmem {
   union {
     struct {
-      MrRec rec[MR_WMAX];                        // occupancy word + exclusive popcount prefix
+      // occupancy words and their exclusive popcount prefixes in two dense arrays:
+      // word w's 32-bit halves sit on banks 2w, 2w+1 and its prefix on bank w, so
+      // the ORs and rank reads spread over every bank (a 16-B {word, prefix}
+      // record put them on 16 of 32 and 8 of 32 banks)
+      unsigned long long bits[MR_WMAX];
+      uint32_t pre[MR_WMAX];
       unsigned long long rows[MD_NMAX * MD_KWMAX];
       unsigned long long sbits[MR_PMAX / 64];    // bit r: peak r starts spectrum >= 1
       uint8_t spre[MR_PMAX / 64];                // spectra started before word w
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
   const int nsw = (np + 63) / 64;
   for (int w = tid; w < nsw; w += MD_BLOCK) L.u.a.sbits[w] = 0ull;
   if (tid <= n) L.soff[tid] = (int32_t)(v.spec_off[s0 + tid] - p0);
-  for (int w = tid; w < MR_WMAX; w += MD_BLOCK) L.u.a.rec[w].bits = 0ull;
+  for (int w = tid; w < MR_WMAX; w += MD_BLOCK) L.u.a.bits[w] = 0ull;
   __syncthreads();
   if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
     const bool empty_spec = tid < n && L.soff[tid + 1] == L.soff[tid];
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
             } else {
               b = (uint32_t)bb;
               // 32-bit half of the occupancy word (same-address LDS atomics serialise)
-              atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rec[b >> 6].bits) + ((b >> 5) & 1), 1u << (b & 31));
+              atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.bits[b >> 6]) + ((b >> 5) & 1), 1u << (b & 31));
             }
           }
           if (u & 1) bins[u >> 1] |= b << 16;
@@ -295,14 +296,14 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
     const int w0 = tid * RPT;
     unsigned long long b[RPT];
 #pragma unroll
-    for (int k = 0; k < RPT; ++k) b[k] = L.u.a.rec[w0 + k].bits;
+    for (int k = 0; k < RPT; ++k) b[k] = L.u.a.bits[w0 + k];
     int local = 0;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) local += __popcll(b[k]);
     int base = block_exclusive_scan<MD_BLOCK, int, true>(local, L.tmp, K);
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      L.u.a.rec[w0 + k].pre = (uint32_t)base;
+      L.u.a.pre[w0 + k] = (uint32_t)base;
       base += __popcll(b[k]);
     }
   }
@@ -334,8 +335,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidP
       const int spw = __builtin_amdgcn_readlane(my_sp, u);
       if (r < np) {
         const uint32_t b = (bins[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-        const MrRec R = L.u.a.rec[b >> 6];
-        const int col = (int)R.pre + __popcll(R.bits & ((1ull << (b & 63)) - 1ull));
+        const int col = (int)L.u.a.pre[b >> 6] + __popcll(L.u.a.bits[b >> 6] & ((1ull << (b & 63)) - 1ull));
         // empty spectra share a start bit: then the binary search
         const unsigned long long sw = ((unsigned long long)swhi << 32) | swlo;
         const int sp = has_empty ? spectrum_of(L.soff, n, r) : spw + __popcll(sw & upto);
