@@ -27,7 +27,16 @@ struct MedoidParams {
 
 constexpr int MD_BLOCK = 256;
 constexpr int MD_NMAX = 64;
-constexpr int MD_KWMAX = 31;     // row words (odd stride): <= 1,984 occupied bins per small cluster
+// 27 row words (<= 1,728 occupied bins) and 72 VGPRs: 22.6 KB of LDS, 7 workgroups
+// per CU (31 words / 6 per CU: 1.55 -> 1.48 ms at 100k clusters); a cluster with
+// more distinct bins takes the large path
+#ifndef SPX_MD_KWMAX
+#define SPX_MD_KWMAX 27
+#endif
+#ifndef SPX_MD_MINW
+#define SPX_MD_MINW 7
+#endif
+constexpr int MD_KWMAX = SPX_MD_KWMAX;  // row words (odd stride): <= 64 * MD_KWMAX occupied bins per small cluster
 
 
 __device__ __forceinline__ int64_t md_bin(double m, const MedoidParams& P) {
@@ -141,7 +150,7 @@ __device__ __forceinline__ void md_defer(int64_t c, int64_t s0, int n, int32_t* 
 //       total = (row + col)/n
 //   P6  lowest index of the minimum (:103-110), one wave
 // Deferred to the large path: n > 64, > MR_UMAX*256 peaks, a bin outside
-// [0, 65,536), > 1,984 distinct bins.
+// [0, 65,536), > 64 * MD_KWMAX distinct bins.
 constexpr int MR_UMAX = 48;                  // peaks per thread (12,288 per cluster)
 constexpr int MR_PMAX = MR_UMAX * MD_BLOCK;
 constexpr int MR_WMAX = 512;                 // union-bitmap words: bins < 32,768 (m/z < 3,276.8 at 0.1)
@@ -170,7 +179,7 @@ struct MedoidRegSmem {
   int votes[2 * (MD_BLOCK / kWave)];
 };
 
-__global__ __launch_bounds__(MD_BLOCK) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
+__global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
                                                               double* totals_out, int32_t* deferred,
                                                               int32_t* n_deferred, MedoidMeta* meta) {
   __shared__ MedoidRegSmem L;
