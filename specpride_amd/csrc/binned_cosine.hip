@@ -265,20 +265,31 @@ __device__ bool cos_body(const CsrView& v, const CosParams& P, const CosState& S
       // runs need every valid bin >= the previous valid one, and a repeated bin
       // right after its predecessor (an invalid peak between two equal bins
       // would split np.bincount's single sum)
-      int64_t pm = bm;
+      int64_t prev, raw_before, cmax, lraw;
+      if (kc < 0x7ffffff0) {  // uniform: every bin fits 32 bits -- DPP, no LDS round trips
+        const int32_t b32 = (int32_t)bm;
+        const int32_t p32 = wave_scan_dpp(b32, (int32_t)0x80000000, [](int32_t x, int32_t y) { return x > y ? x : y; });
+        prev = (int32_t)__builtin_amdgcn_update_dpp(-1, p32, 0x138, 0xF, 0xF, false);  // wave_shr:1
+        raw_before = (int32_t)__builtin_amdgcn_update_dpp(-1, b32, 0x138, 0xF, 0xF, false);
+        cmax = __builtin_amdgcn_readlane(p32, kWave - 1);
+        lraw = __builtin_amdgcn_readlane(b32, kWave - 1);
+      } else {
+        int64_t pm = bm;
 #pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) {
-        const int64_t t = __shfl_up(pm, o, kWave);
-        if (lane >= o) pm = pm > t ? pm : t;
+        for (int o = 1; o < kWave; o <<= 1) {
+          const int64_t t = __shfl_up(pm, o, kWave);
+          if (lane >= o) pm = pm > t ? pm : t;
+        }
+        prev = __shfl_up(pm, 1, kWave);
+        raw_before = __shfl_up(bm, 1, kWave);
+        cmax = __shfl(pm, kWave - 1, kWave);
+        lraw = __shfl(bm, kWave - 1, kWave);
       }
-      int64_t prev = __shfl_up(pm, 1, kWave);
-      int64_t raw_before = __shfl_up(bm, 1, kWave);
       if (lane == 0) { prev = -1; raw_before = last_raw; }
       prev = prev > lastb ? prev : lastb;
       unsorted |= __ballot(bm >= 0 && (bm < prev || (bm == prev && raw_before != bm))) != 0ull;
-      const int64_t cmax = __shfl(pm, kWave - 1, kWave);
       lastb = cmax > lastb ? cmax : lastb;
-      last_raw = __shfl(bm, kWave - 1, kWave);
+      last_raw = lraw;
       if (unsorted) continue;  // (uniform) B.B by the O(m^2) pass below
       // runs of equal bins, summed in input order; the last one may continue
       L.wk[wid][lane] = (int32_t)bm;

@@ -45,6 +45,10 @@ def main():
            "algorithmic_GBs": round(nbytes / (ms * 1e-3) / 1e9, 1),
            "status_ok": int((st == 0).sum().item()),
            "mean_avg_cos": round(float(res.avg[:b.n_clusters].mean().item()), 4)}
+    import hashlib  # order-sensitive digest of the results (A/B builds must agree)
+
+    out["digest"] = hashlib.sha1(res.cos[:b.n_spectra].cpu().numpy().tobytes() +
+                                 res.avg[:b.n_clusters].cpu().numpy().tobytes()).hexdigest()[:16]
     if args.cpu_sample > 0:
         # the reference's CPU path (dense sum-binning on ~400k edges per pair, benchmark.py:10-38),
         # restated in numpy (oracle/np_oracle.py), on 1 host core: the first clusters of the batch
