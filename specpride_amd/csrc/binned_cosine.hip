@@ -34,10 +34,22 @@ struct CosParams {
 };
 
 constexpr int CS_BLOCK = 256;
-constexpr int CS_RCAP = 1024;  // representative peaks held in LDS
+// 512 representative peaks in LDS and 1,024-bin run buckets: 25.9 KB, 6 workgroups
+// per CU.  The kernel is latency-bound (a wave walks its members chunk by chunk), so
+// occupancy is what pays: 1,024 peaks / 256-bin buckets (55 KB, 2 per CU) measured
+// 14.6 ms per 100k clusters, 640 peaks (4 per CU) 8.0 ms, this 6.15 ms.  Longer
+// representatives take the global-scratch kernel.
+#ifndef SPX_CS_RCAP
+#define SPX_CS_RCAP 512
+#endif
+constexpr int CS_RCAP = SPX_CS_RCAP;  // representative peaks held in LDS
 constexpr int CS_NW = CS_BLOCK / kWave;
-constexpr int CS_BSH = 8;      // run-index buckets of 256 bins (~1.28 Da)
-constexpr int CS_BMAX = 2048;  // buckets held in LDS: bins < 524,288 (m/z < ~2,620)
+#ifndef SPX_CS_BSH
+#define SPX_CS_BSH 10
+#endif
+constexpr int CS_BSH = SPX_CS_BSH;                 // run-index buckets of 2^CS_BSH bins (1,024: ~5.1 Da)
+constexpr int CS_BMAX = (1 << 19) >> CS_BSH;       // buckets held in LDS: bins < 524,288 (m/z < ~2,620)
+static_assert(CS_BMAX % CS_BLOCK == 0, "whole buckets per thread");
 
 // Representative state: LDS arrays (cap = CS_RCAP) in the main kernel, a
 // per-workgroup global scratch slice (cap = the largest deferred
@@ -64,7 +76,11 @@ struct CosShared {               // LDS of both kernels
 };
 
 struct CosSmem {
-  int32_t sk[CS_RCAP], pk[CS_RCAP], pidx[CS_RCAP], rb[CS_RCAP], rs[CS_RCAP + 1];
+  union {  // the rank sort's input is dead once the runs are written
+    int32_t sk[CS_RCAP];
+    int32_t rb[CS_RCAP];
+  };
+  int32_t pk[CS_RCAP], pidx[CS_RCAP], rs[CS_RCAP + 1];
   double pI[CS_RCAP], rA[CS_RCAP], rA2[CS_RCAP + 1];
   CosShared sh;
 };
@@ -195,15 +211,24 @@ __device__ bool cos_body(const CsrView& v, const CosParams& P, const CosState& S
     }
     if (tid == 0) S.rA2[nr] = tot;
     // bucket t: the first run with a bin >= t << CS_BSH (runs are sorted by bin)
-    for (int t = tid; t < CS_BMAX; t += CS_BLOCK) {
-      const int64_t b0 = (int64_t)t << CS_BSH;
+    {
+      // CS_BMAX / CS_BLOCK consecutive buckets per thread: one binary search for the
+      // first, then a forward walk (runs are sparse: ~0-1 steps per bucket)
+      constexpr int TPT = CS_BMAX / CS_BLOCK;
+      const int t0 = tid * TPT;
+      const int64_t b0 = (int64_t)t0 << CS_BSH;
       int lo = 0, hi = nr;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         if ((int64_t)S.rb[mid] < b0) lo = mid + 1;
         else hi = mid;
       }
-      L.bst[t] = lo;
+#pragma unroll
+      for (int k = 0; k < TPT; ++k) {
+        const int64_t bk = (int64_t)(t0 + k) << CS_BSH;
+        while (lo < nr && (int64_t)S.rb[lo] < bk) ++lo;
+        L.bst[t0 + k] = lo;
+      }
     }
     __syncthreads();
   }
@@ -213,6 +238,15 @@ __device__ bool cos_body(const CsrView& v, const CosParams& P, const CosState& S
   // members: one wave each
   for (int j = wid; j < n; j += CS_NW) {
     const int64_t a = v.spec_off[s0 + j], e = v.spec_off[s0 + j + 1];
+    // the member's first chunk is loaded with its last m/z, before the pair's cut is
+    // worked out, and every chunk loads the next one ahead (one HBM latency per member
+    // instead of one per chunk)
+    double xq, Iq;
+    {
+      const int64_t k0 = a + lane;
+      xq = k0 < e ? v.mz[k0] : 0.0;
+      Iq = k0 < e ? v.inten[k0] : 0.0;
+    }
     const double mem_last = v.mz[e - 1];
     const double max_mz = mem_last > rep_last ? mem_last : rep_last;  // max(rep.mz[-1], member.mz[-1])
     const int64_t Lc = (int64_t)ceil((max_mz - P.start) / P.s);      // len(np.arange(...))
@@ -259,7 +293,12 @@ __device__ bool cos_body(const CsrView& v, const CosParams& P, const CosState& S
     for (int ch = 0; ch < m; ch += kWave) {
       const int q = ch + lane;
       const bool in = q < m;
-      const double x = in ? v.mz[a + q] : 0.0, I = in ? v.inten[a + q] : 0.0;
+      const double x = in ? xq : 0.0, I = in ? Iq : 0.0;
+      {
+        const int qn = q + kWave;
+        xq = qn < m ? v.mz[a + qn] : 0.0;
+        Iq = qn < m ? v.inten[a + qn] : 0.0;
+      }
       const int64_t bm = in ? mem_bin(x) : -1;
       if (bm >= 0) ab += I * lookup(bm);
       // runs need every valid bin >= the previous valid one, and a repeated bin
