@@ -383,8 +383,8 @@ __device__ bool cos_body(const CsrView& v, const CosParams& P, const CosState& S
     } else if (carry_b >= 0 && lane == 0) {
       bb += carry_s * carry_s;
     }
-    ab = wave_sum(ab);
-    bb = wave_sum(bb);
+    ab = wave_sum_f64(ab);
+    bb = wave_sum_f64(bb);
     if (lane == 0) cos_out[s0 + j] = (aa == 0.0 || bb == 0.0) ? 0.0 : ab / sqrt(aa * bb);
   }
   __syncthreads();

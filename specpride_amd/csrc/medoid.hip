@@ -43,25 +43,6 @@ __device__ __forceinline__ int64_t md_bin(double m, const MedoidParams& P) {
   return ceil_div_exact(m, P.tol, P.inv_tol);
 }
 
-// lane l receives lane l ^ K's value (K < 32): DPP quad_perm for K = 1, 2 (no LDS),
-// ds_swizzle's bit mode for K = 4, 8 (no address VGPR, unlike ds_bpermute)
-template <int K>
-__device__ __forceinline__ double xor_f64(double x) {
-  const uint64_t u = (uint64_t)__double_as_longlong(x);
-  int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
-  if constexpr (K == 1) {
-    lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
-  } else if constexpr (K == 2) {
-    lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-    hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false);
-  } else {
-    lo = __builtin_amdgcn_ds_swizzle(lo, 0x001F | (K << 10));  // and 0x1F, xor K
-    hi = __builtin_amdgcn_ds_swizzle(hi, 0x001F | (K << 10));
-  }
-  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
-}
-
 // d(i,j) exactly as 1.0 - XQuestScores::xCorrelationPrescore(...)
 __device__ __forceinline__ double md_dist(uint32_t c, int64_t pi, int64_t pj) {
   const double x = (pi == 0 || pj == 0) ? 0.0 : (double)c / (double)(pi < pj ? pi : pj);

@@ -152,6 +152,42 @@ __device__ __forceinline__ T wave_sum(T x) {
   return x;
 }
 
+// lane l receives lane l ^ K's value: DPP quad_perm for K = 1, 2 (no LDS), ds_swizzle's
+// bit mode for K = 4, 8, 16 (no address VGPR), ds_bpermute for K = 32
+template <int K>
+__device__ __forceinline__ double xor_f64(double x) {
+  if constexpr (K == 32) {
+    return __shfl_xor(x, 32, kWave);
+  } else {
+    const uint64_t u = (uint64_t)__double_as_longlong(x);
+    int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
+    if constexpr (K == 1) {
+      lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+      hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+    } else if constexpr (K == 2) {
+      lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+      hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false);
+    } else {
+      static_assert(K == 4 || K == 8 || K == 16, "swizzle xor within 32 lanes");
+      lo = __builtin_amdgcn_ds_swizzle(lo, 0x001F | (K << 10));  // and 0x1F, xor K
+      hi = __builtin_amdgcn_ds_swizzle(hi, 0x001F | (K << 10));
+    }
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+  }
+}
+
+// wave_sum's butterfly (xor 32, 16, ..., 1: the same additions in the same order,
+// so the same bits) with DPP/swizzle moves for all but the first step
+__device__ __forceinline__ double wave_sum_f64(double x) {
+  x += xor_f64<32>(x);
+  x += xor_f64<16>(x);
+  x += xor_f64<8>(x);
+  x += xor_f64<4>(x);
+  x += xor_f64<2>(x);
+  x += xor_f64<1>(x);
+  return x;
+}
+
 __device__ __forceinline__ double wave_max(double x) {
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) {
