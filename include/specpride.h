@@ -173,7 +173,7 @@ typedef struct spx_cosine_params {
  * member, avg_out [n_clusters] = average_cos_dist (0.0 for no members).
  * status[c]: SPX_EMPTY if the representative or a member has no peaks (the
  * reference's mz[-1] raises IndexError; NaN outputs).  Representatives of up to
- * 1,024 peaks are sorted in LDS; longer ones (max_rep_peaks = an upper bound on
+ * 512 peaks are sorted in LDS; longer ones (max_rep_peaks = an upper bound on
  * every representative's length) in a global workspace slice, so any length is
  * evaluated; SPX_UNRESOLVED only if a representative exceeds max_rep_peaks. */
 size_t spx_binned_cosine_workspace_size(int64_t n_clusters, int64_t max_rep_peaks);

@@ -416,7 +416,7 @@ def binned_cosine(batch: DeviceBatch, rep_off, rep_mz, rep_int, mz_space=MZ_SPAC
     batch: cluster c's representative is the device peak list
     [rep_off[c], rep_off[c+1]) of rep_mz / rep_int, its members are its spectra.
     ``max_rep_peaks`` (an upper bound on the representatives' lengths) sizes the
-    workspace for representatives past the LDS path's 1,024 peaks; if omitted it
+    workspace for representatives past the LDS path's 512 peaks; if omitted it
     is read from ``rep_off`` (one small device reduction and host read)."""
     import torch
 
