@@ -15,9 +15,18 @@
  *                              CLI can group the records the reference's way
  *                              (average_spectrum_clustering.py:151-160,
  *                              most_similar_representative.py:48-52) before parsing
+ *   spx_mgf_index_range        the same index over one byte stripe of the file (a rank's
+ *                              share: every record is listed by the stripe its start
+ *                              line lies in), exchanged between ranks by the caller
  *   spx_mgf_parse_ranges       the same parsers over only the listed records
  *   spx_mgf_format_binning /   src/binning.py:234-245 writer (f-string of numpy floats)
  *   spx_mgf_write_binning_batch
+ *   spx_mgf_write_records      the three CLIs' writers, batched and multithreaded:
+ *                              binning.py:234-245 (style 0), the gap-average CLI's
+ *                              mgf.write (average_spectrum_clustering.py:207-208, style 1)
+ *                              and the medoid CLI's MascotGenericFile().store
+ *                              (most_similar_representative.py:115, style 2) in the
+ *                              shims' formats (the pyteomics / OpenMS text is unpinned)
  *   spx_py_repr                Python repr() of a float64
  *
  * Parse results are opaque handles: query sizes, copy the arrays into caller-owned
@@ -61,6 +70,9 @@ void spx_mgf_free(void* h);
 /* ---- record index ---- */
 
 void* spx_mgf_index(const char* path, int general);
+/* The records of spx_mgf_index whose start line begins in bytes [lo, hi) (same handle
+ * accessors).  threads <= 0: min(16, hardware threads). */
+void* spx_mgf_index_range(const char* path, int general, int64_t lo, int64_t hi, int threads);
 const char* spx_mgf_index_error(void* h);
 int64_t spx_mgf_index_n(void* h);
 /* begin[n], end[n]: byte range of each record; npk[n]: its peak lines. */
@@ -82,6 +94,13 @@ int spx_py_repr(double x, char* out);
 int spx_mgf_write_binning_batch(const char* path, int64_t C, const char* ids, const int64_t* charge,
                                 const double* prec, const int64_t* off, const double* mz, const double* it,
                                 int threads);
+/* C records, style 0 (binning.py), 1 (gap-average CLI) or 2 (medoid CLI); titles
+ * '\n'-joined; flags[c] (styles 1-2) bit0 PEPMASS, bit1 CHARGE, bit2 RTINSECONDS,
+ * bit3 TITLE present; record c's peaks [off[c], off[c+1]).  append: open "ab".
+ * Returns 0, or -1 on an I/O error or a bad argument. */
+int spx_mgf_write_records(const char* path, int append, int style, int64_t C, const char* titles,
+                          const int32_t* flags, const double* prec, const int64_t* charge, const double* rt,
+                          const int64_t* off, const double* mz, const double* it, int threads);
 
 #ifdef __cplusplus
 }

@@ -101,7 +101,8 @@ def build_mgf(force: bool = False) -> str:
     """Host C++ MGF reader/writer (csrc/mgf_io.cpp) -> specpride_amd/lib/libspx_mgf.so."""
     os.makedirs(LIB_DIR, exist_ok=True)
     src = os.path.join(CSRC, "mgf_io.cpp")
-    if not force and os.path.exists(MGF_LIB_PATH) and os.path.getmtime(MGF_LIB_PATH) >= os.path.getmtime(src):
+    newest = max(os.path.getmtime(src), os.path.getmtime(os.path.join(REPO, "include", "spx_mgf.h")))
+    if not force and os.path.exists(MGF_LIB_PATH) and os.path.getmtime(MGF_LIB_PATH) >= newest:
         return MGF_LIB_PATH
     tmp = MGF_LIB_PATH + ".tmp"
     subprocess.run([os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread",

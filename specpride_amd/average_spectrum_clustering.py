@@ -151,13 +151,9 @@ def process_maracluster_mgf(fname, get_cluster=get_cluster_id, get_pepmass=naive
     acc = kwargs.get("mz_accuracy", DIFF_THRESH)
     dyn = kwargs.get("dyn_range", DYN_RANGE)
     frac = kwargs.get("min_fraction", MIN_FRACTION)
-    if on_device and get_cluster is get_cluster_id:
-        native = _native_runs(fname)
-        if native is not None:
-            ids, csr = native
-            r = engine.gap_average(engine.DeviceBatch.from_host(csr), acc, dyn, frac, pepmass=pm_mode,
-                                   rt=rt_mode).to_host()
-            return _outputs(r, ids)
+    native = _native_pass(fname, get_cluster, get_pepmass, get_rt, **kwargs)
+    if native is not None:
+        return _outputs(*native[::-1])
     spectra = read_mgf(fname)
     runs = []
     for cluster_id, grp in groupby(spectra, lambda s: get_cluster(s["params"]["title"])):
@@ -190,6 +186,26 @@ def _outputs(r, ids):
     return outputs
 
 
+def _native_pass(fname, get_cluster=get_cluster_id, get_pepmass=naive_average_mass_and_charge, get_rt=median_rt,
+                 **kwargs):
+    """process_maracluster_mgf's device pass over the native parse: (run ids, host
+    result with the precursor fields computed on the device), or None when the
+    helpers are custom callables or the file is outside the native subset."""
+    pm_mode = {lower_median_mass: "lower_median", naive_average_mass_and_charge: "naive_average",
+               neutral_average_mass_and_charge: "neutral_average"}.get(get_pepmass)
+    rt_mode = {median_rt: "median", lower_median_mass_rt: "mass_lower_median"}.get(get_rt)
+    if pm_mode is None or rt_mode is None or get_cluster is not get_cluster_id:
+        return None
+    native = _native_runs(fname)
+    if native is None:
+        return None
+    ids, csr = native
+    r = engine.gap_average(engine.DeviceBatch.from_host(csr), kwargs.get("mz_accuracy", DIFF_THRESH),
+                           kwargs.get("dyn_range", DYN_RANGE), kwargs.get("min_fraction", MIN_FRACTION),
+                           pepmass=pm_mode, rt=rt_mode).to_host()
+    return ids, r
+
+
 def _native_runs(fname):
     """Native parse -> (run ids, CSR of the consecutive-title runs), or None when
     the file is outside the native subset or a record has no TITLE."""
@@ -203,6 +219,19 @@ def _native_runs(fname):
         return None
     ids, records, sizes = ingest.gap_average_groups(flat["titles"])
     return ids, ingest.csr_from_flat(flat, sizes)
+
+
+def write_outputs_native(r, ids, output, file_mode="w"):
+    """mgf.write of the outputs (average_spectrum_clustering.py:207-208) straight
+    from a device result: the reference's error for the first failing run, then
+    the native multithreaded writer (the same text as write_pyteomics_style)."""
+    from . import mgf_native
+
+    bad = np.flatnonzero(r["status"] != engine.STATUS_OK)
+    if len(bad):
+        _raise_for(r["status"][bad[0]])
+    mgf_native.write_records(output, mgf_native.STYLE_GAP_AVERAGE, ids, r["out_off"], r["out_mz"], r["out_int"],
+                             r["prec"], r["charge"], r["rt"], append=file_mode == "a")
 
 
 def main(argv=None):
@@ -240,6 +269,11 @@ def main(argv=None):
                                                 **kwargs)], args.output, file_mode=mode)
     elif args.encodedclusters:
         def single():
+            native = _native_pass(args.input, get_pepmass=get_pepmass, get_rt=get_rt, **kwargs) \
+                if args.output is not None else None
+            if native is not None:  # native ingest -> one device pass -> native writer
+                write_outputs_native(native[1], native[0], args.output, file_mode=mode)
+                return
             write_pyteomics_style(process_maracluster_mgf(args.input, get_pepmass=get_pepmass, get_rt=get_rt,
                                                           **kwargs), args.output, file_mode=mode)
 

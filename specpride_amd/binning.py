@@ -143,19 +143,26 @@ class RepresentativeSpectrumCreator:
         return self._combine_csr(SpectraCSR.from_clusters(clusters), clusters, minimum, maximum, binsize,
                                  apply_peak_quorum)
 
+    def _combine_host(self, csr, minimum=100, maximum=2000, binsize=0.02, apply_peak_quorum=True):
+        """The device pass over a packed batch: the dense host result of
+        :meth:`engine.PeaksResult.to_host`, after raising the reference's error for
+        the first failing cluster (AssertionError on mixed charges, binning.py:205-206)."""
+        res = engine.bin_mean(engine.DeviceBatch.from_host(csr, self.device), minimum, maximum, binsize,
+                              apply_peak_quorum).to_host()
+        bad = np.flatnonzero(res["status"] != engine.STATUS_OK)
+        if len(bad):
+            if res["status"][bad[0]] == engine.STATUS_MIXED_CHARGE:
+                raise AssertionError(MIXED_CHARGE_MSG)
+            # empty cluster: the reference fails on charges[0]
+            raise IndexError("list index out of range")
+        return res
+
     def _combine_csr(self, csr, clusters, minimum=100, maximum=2000, binsize=0.02, apply_peak_quorum=True):
         """The device pass over a packed batch; ``clusters[c]`` (peaklists) or None
         per cluster -- the output's precursor_charge is its first member's charge."""
-        res = engine.bin_mean(engine.DeviceBatch.from_host(csr, self.device), minimum, maximum, binsize,
-                              apply_peak_quorum).to_host()
+        res = self._combine_host(csr, minimum, maximum, binsize, apply_peak_quorum)
         out = []
         for c, pl in enumerate(clusters):
-            st = res["status"][c]
-            if st == engine.STATUS_MIXED_CHARGE:
-                raise AssertionError(MIXED_CHARGE_MSG)
-            if st != engine.STATUS_OK:
-                # empty cluster: the reference fails on charges[0]
-                raise IndexError("list index out of range")
             a, b = res["out_off"][c], res["out_off"][c + 1]
             out.append({"minimum": minimum, "maximum": maximum, "binsize": binsize,
                         "intensities": res["out_int"][a:b].copy(), "mzs": res["out_mz"][a:b].copy(),
@@ -246,18 +253,23 @@ def main(argv=None):
 
 def _main_mgf(mgf_file, out, verbose):
     """The single-process ``--mgf_file`` CLI body (binning.py:286-302)."""
+    from . import mgf_native
+
     rsc = RepresentativeSpectrumCreator(verbose=verbose)
     print("Reading spectra...")
     flat = _flat_clusters(mgf_file)
-    if flat is not None:  # native parse straight to the cluster-segmented CSR
+    if flat is not None:  # native parse straight to the cluster-segmented CSR, native writer
         ids, csr = flat
         print("Clustering...")
-        merged = rsc._combine_csr(csr, [None] * len(ids), minimum=100, maximum=2000, binsize=0.02)
-    else:  # the reference's own line loop decides (malformed or unusual input)
-        clusters = rsc.read_spectra_clustered_mgf(mgf_file)
-        print("Clustering...")
-        ids = list(clusters.keys())
-        merged = rsc.combine_bin_mean_batch([clusters[k] for k in ids], minimum=100, maximum=2000, binsize=0.02)
+        res = rsc._combine_host(csr, minimum=100, maximum=2000, binsize=0.02)
+        mgf_native.write_records(out, mgf_native.STYLE_BINNING, ids, res["out_off"], res["out_mz"], res["out_int"],
+                                 res["prec"], res["charge"])
+        return
+    # the reference's own line loop decides (malformed or unusual input)
+    clusters = rsc.read_spectra_clustered_mgf(mgf_file)
+    print("Clustering...")
+    ids = list(clusters.keys())
+    merged = rsc.combine_bin_mean_batch([clusters[k] for k in ids], minimum=100, maximum=2000, binsize=0.02)
     for cid, spec in zip(ids, merged):
         spec["cluster_id"] = cid
     with open(out, "wt") as fh:

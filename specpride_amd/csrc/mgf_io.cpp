@@ -24,6 +24,11 @@
 // Writer: Python repr() of a float64 (numpy's str() of np.float64 is the same):
 // shortest round-trip digits (std::to_chars), positional for 1e-4 <= |x| < 1e16,
 // else d.ddde+XX.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <charconv>
 #include <cmath>
@@ -35,6 +40,8 @@
 #include <thread>
 #include <type_traits>
 #include <vector>
+
+#include "../../include/spx_mgf.h"
 
 namespace {
 
@@ -390,18 +397,31 @@ void parse_range_general(const char* b, const char* e, GenChunk& C) {
   C.it.resize(mark);
 }
 
-bool read_file(const char* path, std::string& data, std::string& err) {
-  FILE* f = std::fopen(path, "rb");
-  if (!f) { err = std::string("cannot open ") + path; return false; }
-  std::fseek(f, 0, SEEK_END);
-  long sz = std::ftell(f);
-  std::fseek(f, 0, SEEK_SET);
-  data.resize(sz > 0 ? (size_t)sz : 0);
-  size_t got = sz > 0 ? std::fread(&data[0], 1, (size_t)sz, f) : 0;
-  std::fclose(f);
-  if (got != data.size()) { err = "short read"; return false; }
-  return true;
-}
+// Read-only mapping of a whole file: pages are read on first touch, so a rank
+// that indexes one byte stripe of a large MGF reads only that stripe.
+struct MappedFile {
+  const char* data = nullptr;
+  size_t size = 0;
+  std::string error;
+  explicit MappedFile(const char* path) {
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) { error = std::string("cannot open ") + path; return; }
+    struct stat st;
+    if (::fstat(fd, &st) != 0) { error = "fstat failed"; ::close(fd); return; }
+    size = (size_t)st.st_size;
+    if (size > 0) {
+      void* m = ::mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+      if (m == MAP_FAILED) { error = "mmap failed"; size = 0; }
+      else data = static_cast<const char*>(m);
+    }
+    ::close(fd);
+  }
+  ~MappedFile() {
+    if (data) ::munmap(const_cast<char*>(data), size);
+  }
+  MappedFile(const MappedFile&) = delete;
+  MappedFile& operator=(const MappedFile&) = delete;
+};
 
 // ------------------------------------------------------------ repr writer
 // Python repr(float) into out; returns bytes written.
@@ -486,6 +506,133 @@ int64_t format_binning(char* buf, int64_t cap, const char* cid, const char* char
   return (int64_t)(o - buf);
 }
 
+// ------------------------------------------------------------ record writers
+// One output record per cluster, in three text styles:
+//   0  binning.py:234-245 -- TITLE=<id>, PEPMASS=repr, CHARGE=<int>+, peaks with
+//      NaN intensities skipped (the f-string of numpy floats);
+//   1  the gap-average CLI (average_spectrum_clustering.py:207-208 via the shims'
+//      write_pyteomics_style): TITLE (if non-empty), PEPMASS, RTINSECONDS,
+//      CHARGE=<|z|><+|->, every peak;
+//   2  the medoid CLI (most_similar_representative.py:115 via write_record):
+//      TITLE, PEPMASS, CHARGE, RTINSECONDS, every peak.
+// flags[c] (styles 1-2): bit0 PEPMASS, bit1 CHARGE, bit2 RTINSECONDS, bit3 TITLE
+// present (absent fields are omitted).  Floats are Python repr().
+struct RecordsIn {
+  int style = 0;
+  std::vector<const char*> tp;
+  std::vector<size_t> tl;
+  const int32_t* flags = nullptr;
+  const double* prec = nullptr;
+  const int64_t* charge = nullptr;
+  const double* rt = nullptr;
+  const int64_t* off = nullptr;
+  const double* mz = nullptr;
+  const double* it = nullptr;
+};
+
+inline char* put(char* o, const char* s, size_t k) {
+  std::memcpy(o, s, k);
+  return o + k;
+}
+inline char* put_int(char* o, long long v) {
+  auto r = std::to_chars(o, o + 24, v);
+  return r.ptr;
+}
+inline char* put_repr(char* o, double x) { return o + py_repr(x, o); }
+
+size_t record_cap(size_t title_len, int64_t n) { return 192 + title_len + (size_t)n * 52; }
+
+char* format_record(const RecordsIn& R, int64_t c, char* o) {
+  const size_t tl = R.tl[(size_t)c];
+  const char* t = R.tp[(size_t)c];
+  const int32_t f = R.flags ? R.flags[c] : 0xf;
+  const int64_t a = R.off[c], b = R.off[c + 1];
+  o = put(o, "BEGIN IONS\n", 11);
+  auto title = [&]() { o = put(o, "TITLE=", 6); o = put(o, t, tl); *o++ = '\n'; };
+  auto pepmass = [&]() { o = put(o, "PEPMASS=", 8); o = put_repr(o, R.prec[c]); *o++ = '\n'; };
+  auto rtsec = [&]() { o = put(o, "RTINSECONDS=", 12); o = put_repr(o, R.rt[c]); *o++ = '\n'; };
+  auto charge = [&]() {  // format_charge: |z| then the sign
+    const int64_t z = R.charge[c];
+    o = put(o, "CHARGE=", 7);
+    o = put_int(o, z < 0 ? -z : z);
+    *o++ = z < 0 ? '-' : '+';
+    *o++ = '\n';
+  };
+  if (R.style == 0) {
+    title();
+    pepmass();
+    o = put(o, "CHARGE=", 7);
+    o = put_int(o, R.charge[c]);
+    o = put(o, "+\n", 2);
+  } else if (R.style == 1) {
+    if ((f & 8) && tl > 0) title();
+    if (f & 1) pepmass();
+    if (f & 4) rtsec();
+    if (f & 2) charge();
+  } else {
+    if (f & 8) title();
+    if (f & 1) pepmass();
+    if (f & 2) charge();
+    if (f & 4) rtsec();
+  }
+  const bool skip_nan = R.style == 0;
+  for (int64_t k = a; k < b; ++k) {
+    if (skip_nan && std::isnan(R.it[k])) continue;
+    o = put_repr(o, R.mz[k]);
+    *o++ = ' ';
+    o = put_repr(o, R.it[k]);
+    *o++ = '\n';
+  }
+  return put(o, "END IONS\n\n", 10);
+}
+
+// '\n'-joined strings -> pointers and lengths (C entries)
+void split_lines(const char* s, int64_t C, std::vector<const char*>& p, std::vector<size_t>& l) {
+  p.resize((size_t)C);
+  l.resize((size_t)C);
+  for (int64_t c = 0; c < C; ++c) {
+    const char* nl = std::strchr(s, '\n');
+    p[(size_t)c] = s;
+    l[(size_t)c] = nl ? (size_t)(nl - s) : std::strlen(s);
+    s = nl ? nl + 1 : s + l[(size_t)c];
+  }
+}
+
+// Format clusters [0, C) on T threads in blocks, write them in order; the write
+// of one round overlaps the formatting of the next.  0, or -1 on an I/O error.
+int write_records(FILE* f, const RecordsIn& R, int64_t C, int T) {
+  constexpr int64_t kBlock = 2048;
+  std::vector<std::string> parts[2];
+  parts[0].resize((size_t)T);
+  parts[1].resize((size_t)T);
+  std::thread writer;
+  int rc = 0;
+  int cur = 0;
+  for (int64_t c0 = 0; c0 < C; c0 += kBlock * T, cur ^= 1) {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < T; ++t) {
+      pool.emplace_back([&, t, c0, cur]() {
+        const int64_t a = std::min(C, c0 + t * kBlock), b = std::min(C, a + kBlock);
+        std::string& out = parts[cur][(size_t)t];
+        size_t cap = 0;
+        for (int64_t c = a; c < b; ++c) cap += record_cap(R.tl[(size_t)c], R.off[c + 1] - R.off[c]);
+        out.resize(cap);
+        char* o = &out[0];
+        for (int64_t c = a; c < b; ++c) o = format_record(R, c, o);
+        out.resize((size_t)(o - out.data()));
+      });
+    }
+    for (auto& th : pool) th.join();
+    if (writer.joinable()) writer.join();
+    writer = std::thread([&, cur]() {
+      for (auto& s : parts[cur])
+        if (!s.empty() && std::fwrite(s.data(), 1, s.size(), f) != s.size()) rc = -1;
+    });
+  }
+  if (writer.joinable()) writer.join();
+  return rc;
+}
+
 // Spectrum record start lines: "TITLE=" (binning.py's parser starts a peaklist
 // there) or a stripped "BEGIN IONS" (general MGF).
 inline bool record_start(const char* q, const char* e, int general) {
@@ -551,32 +698,105 @@ struct Index {
   std::string titles, error;
 };
 
+// Is `q` (inside [b, e)) the start of a line?  Lines end at \n, \r\n or \r
+// (Python's universal newlines, as the parsers split them).
+inline bool line_start(const char* b, const char* e, const char* q) {
+  if (q == b) return true;
+  if (q[-1] == '\n') return true;
+  return q[-1] == '\r' && (q == e || *q != '\n');
+}
+
+// Index the records whose start line begins in [b + lo, b + hi) of the file
+// [b, b + size); a record runs to the next record start (possibly past hi) or EOF.
+void index_span(const char* b, size_t size, size_t lo, size_t hi, int general, Index& X) {
+  const char* e = b + size;
+  const char* p = b + lo;
+  const char* stop = b + hi;
+  while (p < e && !line_start(b, e, p)) ++p;  // resync to a line start
+  int64_t rb = -1, np = 0;
+  bool has_end = false;
+  std::string title;
+  auto close = [&](int64_t at) {
+    if (rb >= 0 && has_end) {
+      X.begin.push_back(rb);
+      X.end.push_back(at);
+      X.npk.push_back(np);
+      X.titles += title;
+      X.titles += '\n';
+    }
+  };
+  while (p < e) {
+    const char* ls = p;
+    const char* le = p;
+    while (le < e && *le != '\n' && *le != '\r') ++le;
+    p = le;
+    if (p < e) {
+      if (*p == '\r') { ++p; if (p < e && *p == '\n') ++p; }
+      else ++p;
+    }
+    if (record_start(ls, le, general)) {
+      if (ls >= stop) { close(ls - b); return; }  // the next stripe's first record
+      close(ls - b);
+      rb = ls - b;
+      np = 0;
+      has_end = false;
+      title.clear();
+    }
+    if (rb < 0) continue;  // before this stripe's first record: the previous stripe's
+    const char *sb = ls, *se = le;
+    strip(sb, se);
+    if (!has_end && se - sb >= 6 && (general ? (std::tolower((unsigned char)sb[0]) == 't' && std::tolower((unsigned char)sb[1]) == 'i' &&
+                                    std::tolower((unsigned char)sb[2]) == 't' && std::tolower((unsigned char)sb[3]) == 'l' &&
+                                    std::tolower((unsigned char)sb[4]) == 'e' && sb[5] == '=')
+                                 : std::memcmp(ls, "TITLE=", 6) == 0)) {
+      const char *tb = (general ? sb : ls) + 6, *te = general ? se : le;
+      if (!general) strip(tb, te);
+      title.assign(tb, te);
+    } else if (se - sb == 8 && std::memcmp(sb, "END IONS", 8) == 0) {
+      has_end = true;
+    } else if (se > sb && ((*(general ? sb : ls) >= '0' && *(general ? sb : ls) <= '9') ||
+                           (general && (*sb == '+' || *sb == '-' || *sb == '.') && se - sb > 1 && sb[1] >= '0' &&
+                            sb[1] <= '9'))) {
+      ++np;
+    }
+  }
+  close(e - b);
+}
+
+// [lo, hi) indexed by T threads over sub-stripes (they compose: every record is
+// listed by the sub-stripe its start line lies in), merged in file order.
+void index_stripes(const char* b, size_t size, size_t lo, size_t hi, int general, int T, Index& X) {
+  T = std::max(1, T);
+  std::vector<Index> parts((size_t)T);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < T; ++t) {
+    const size_t a = lo + (hi - lo) * (size_t)t / (size_t)T, z = lo + (hi - lo) * (size_t)(t + 1) / (size_t)T;
+    if (T == 1) index_span(b, size, a, z, general, parts[0]);
+    else pool.emplace_back(index_span, b, size, a, z, general, std::ref(parts[(size_t)t]));
+  }
+  for (auto& th : pool) th.join();
+  for (auto& x : parts) {
+    X.begin.insert(X.begin.end(), x.begin.begin(), x.begin.end());
+    X.end.insert(X.end.end(), x.end.begin(), x.end.end());
+    X.npk.insert(X.npk.end(), x.npk.begin(), x.npk.end());
+    X.titles += x.titles;
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
 void* spx_mgf_parse(const char* path, int threads) {
   Result* R = new Result();
-  std::string data;
-  if (!read_file(path, data, R->error)) return R;
-  const char* b = data.data();
-  const char* e = b + data.size();
-  int T = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  if (data.size() < (1u << 20)) T = 1;
-  // split points at "TITLE=" line starts
-  std::vector<const char*> cuts{b};
-  for (int t = 1; t < T; ++t) {
-    const char* q = b + data.size() * (size_t)t / (size_t)T;
-    if (q <= cuts.back()) continue;
-    while (q < e) {
-      const char* nl = (const char*)std::memchr(q, '\n', (size_t)(e - q));
-      if (!nl) { q = e; break; }
-      q = nl + 1;
-      if (e - q >= 6 && std::memcmp(q, "TITLE=", 6) == 0) break;
-    }
-    if (q < e && q > cuts.back()) cuts.push_back(q);
-  }
-  cuts.push_back(e);
+  MappedFile mf(path);
+  if (!mf.error.empty()) { R->error = mf.error; return R; }
+  const char* b = mf.data;
+  const char* e = b + mf.size;
+  int T = default_threads(threads);
+  if (mf.size < (1u << 20)) T = 1;
+  // per-thread ranges start at "TITLE=" lines (the reference resets its state there)
+  const std::vector<const char*> cuts = split_records(b, e, T, 0);
   const int nc = (int)cuts.size() - 1;
   std::vector<Chunk> chunks((size_t)nc);
   std::vector<std::thread> pool;
@@ -613,12 +833,12 @@ void spx_mgf_copy_rt(void* h, double* rt) {
 // NaN without PEPMASS; flags bit0 PEPMASS, bit1 CHARGE, bit2 RTINSECONDS, bit3 TITLE.
 void* spx_mgf_parse_general(const char* path, int threads) {
   Result* R = new Result();
-  std::string data;
-  if (!read_file(path, data, R->error)) return R;
-  const char* b = data.data();
-  const char* e = b + data.size();
+  MappedFile mf(path);
+  if (!mf.error.empty()) { R->error = mf.error; return R; }
+  const char* b = mf.data;
+  const char* e = b + mf.size;
   int T = default_threads(threads);
-  if (data.size() < (1u << 20)) T = 1;
+  if (mf.size < (1u << 20)) T = 1;
   const std::vector<const char*> cuts = split_records(b, e, T, 1);
   const int nc = (int)cuts.size() - 1;
   std::vector<GenChunk> chunks((size_t)nc);
@@ -635,59 +855,26 @@ void* spx_mgf_parse_general(const char* path, int threads) {
 // general == 0, binning.py's reader; "BEGIN IONS" for general == 1) to the next
 // record's start, its title (the TITLE= value, stripped) and its peak-line count.
 // Only records holding an END IONS line are listed (the ones a parser stores).
+// threads <= 0: min(16, hardware threads); the file is indexed in byte stripes.
 void* spx_mgf_index(const char* path, int general) {
   Index* X = new Index();
-  std::string data;
-  if (!read_file(path, data, X->error)) return X;
-  const char* b = data.data();
-  const char* e = b + data.size();
-  const char* p = b;
-  int64_t rb = -1, np = 0;
-  bool has_end = false;
-  std::string title;
-  auto close = [&](int64_t at) {
-    if (rb >= 0 && has_end) {
-      X->begin.push_back(rb);
-      X->end.push_back(at);
-      X->npk.push_back(np);
-      X->titles += title;
-      X->titles += '\n';
-    }
-  };
-  while (p < e) {
-    const char* ls = p;
-    const char* le = p;
-    while (le < e && *le != '\n' && *le != '\r') ++le;
-    p = le;
-    if (p < e) {
-      if (*p == '\r') { ++p; if (p < e && *p == '\n') ++p; }
-      else ++p;
-    }
-    if (record_start(ls, le, general)) {
-      close(ls - b);
-      rb = ls - b;
-      np = 0;
-      has_end = false;
-      title.clear();
-    }
-    const char *sb = ls, *se = le;
-    strip(sb, se);
-    if (rb >= 0 && !has_end && se - sb >= 6 && (general ? (std::tolower((unsigned char)sb[0]) == 't' && std::tolower((unsigned char)sb[1]) == 'i' &&
-                                    std::tolower((unsigned char)sb[2]) == 't' && std::tolower((unsigned char)sb[3]) == 'l' &&
-                                    std::tolower((unsigned char)sb[4]) == 'e' && sb[5] == '=')
-                                 : std::memcmp(ls, "TITLE=", 6) == 0)) {
-      const char *tb = (general ? sb : ls) + 6, *te = general ? se : le;
-      if (!general) strip(tb, te);
-      title.assign(tb, te);
-    } else if (se - sb == 8 && std::memcmp(sb, "END IONS", 8) == 0) {
-      has_end = true;
-    } else if (se > sb && ((*(general ? sb : ls) >= '0' && *(general ? sb : ls) <= '9') ||
-                           (general && (*sb == '+' || *sb == '-' || *sb == '.') && se - sb > 1 && sb[1] >= '0' &&
-                            sb[1] <= '9'))) {
-      ++np;
-    }
-  }
-  close(e - b);
+  MappedFile mf(path);
+  if (!mf.error.empty()) { X->error = mf.error; return X; }
+  index_stripes(mf.data, mf.size, 0, mf.size, general, mf.size < (1u << 20) ? 1 : default_threads(0), *X);
+  return X;
+}
+
+// The records of spx_mgf_index whose start line begins in bytes [lo, hi) -- a
+// rank-local slice of the index: ranks indexing [k*size/W, (k+1)*size/W) list
+// every record exactly once, and each reads its stripe plus the tail of its last
+// record.  hi is clamped to the file size.
+void* spx_mgf_index_range(const char* path, int general, int64_t lo, int64_t hi, int threads) {
+  Index* X = new Index();
+  MappedFile mf(path);
+  if (!mf.error.empty()) { X->error = mf.error; return X; }
+  if (lo < 0 || hi < lo) { X->error = "bad byte range"; return X; }
+  const size_t l = std::min((size_t)lo, mf.size), h = std::min((size_t)hi, mf.size);
+  index_stripes(mf.data, mf.size, l, h, general, (h - l) < (1u << 20) ? 1 : default_threads(threads), *X);
   return X;
 }
 
@@ -773,45 +960,32 @@ int spx_py_repr(double x, char* out) { return py_repr(x, out); }
 int spx_mgf_write_binning_batch(const char* path, int64_t C, const char* ids, const int64_t* charge,
                                 const double* prec, const int64_t* off, const double* mz, const double* it,
                                 int threads) {
-  std::vector<const char*> idp((size_t)C);
-  std::vector<size_t> idl((size_t)C);
-  const char* q = ids;
-  for (int64_t c = 0; c < C; ++c) {
-    const char* nl = std::strchr(q, '\n');
-    idp[(size_t)c] = q;
-    idl[(size_t)c] = nl ? (size_t)(nl - q) : std::strlen(q);
-    q = nl ? nl + 1 : q + idl[(size_t)c];
-  }
-  int T = threads > 0 ? threads : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  FILE* f = std::fopen(path, "wb");
+  return spx_mgf_write_records(path, 0, 0, C, ids, nullptr, prec, charge, nullptr, off, mz, it, threads);
+}
+
+// C records in one of the styles of format_record (0 binning, 1 gap-average,
+// 2 medoid), titles '\n'-joined, record c's peaks [off[c], off[c+1]) of mz / it.
+// append: open with "ab" (the gap-average CLI's --append).  0, or -1 on an I/O
+// error or a bad argument.
+int spx_mgf_write_records(const char* path, int append, int style, int64_t C, const char* titles,
+                          const int32_t* flags, const double* prec, const int64_t* charge, const double* rt,
+                          const int64_t* off, const double* mz, const double* it, int threads) {
+  if (C < 0 || style < 0 || style > 2 || (C > 0 && (!titles || !prec || !charge || !off || !mz || !it)) ||
+      (style != 0 && C > 0 && (!flags || !rt)))
+    return -1;
+  RecordsIn R;
+  R.style = style;
+  split_lines(titles ? titles : "", C, R.tp, R.tl);
+  R.flags = flags;
+  R.prec = prec;
+  R.charge = charge;
+  R.rt = rt;
+  R.off = off;
+  R.mz = mz;
+  R.it = it;
+  FILE* f = std::fopen(path, append ? "ab" : "wb");
   if (!f) return -1;
-  const int64_t block = 4096;
-  int rc = 0;
-  for (int64_t c0 = 0; c0 < C && rc == 0; c0 += block * T) {
-    std::vector<std::string> parts((size_t)T);
-    std::vector<std::thread> pool;
-    for (int t = 0; t < T; ++t) {
-      pool.emplace_back([&, t]() {
-        const int64_t a = c0 + t * block, b = std::min(C, a + block);
-        std::string& out = parts[(size_t)t];
-        std::vector<char> buf;
-        for (int64_t c = a; c < b; ++c) {
-          std::string cid(idp[(size_t)c], idl[(size_t)c]);
-          char zs[32];
-          std::snprintf(zs, sizeof(zs), "%lld", (long long)charge[c]);
-          const int64_t n = off[c + 1] - off[c];
-          const size_t cap = 128 + cid.size() + (size_t)n * 52;
-          if (buf.size() < cap) buf.resize(cap);
-          const int64_t w = format_binning(buf.data(), (int64_t)cap, cid.c_str(), zs, prec[c], mz + off[c],
-                                           it + off[c], n, 1);
-          out.append(buf.data(), (size_t)w);
-        }
-      });
-    }
-    for (auto& th : pool) th.join();
-    for (auto& s : parts)
-      if (!s.empty() && std::fwrite(s.data(), 1, s.size(), f) != s.size()) rc = -1;
-  }
+  int rc = write_records(f, R, C, default_threads(threads));
   if (std::fclose(f) != 0) rc = -1;
   return rc;
 }

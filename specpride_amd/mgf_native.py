@@ -53,6 +53,11 @@ def _native():
         L.spx_mgf_index_titles.restype = ctypes.c_char_p
         L.spx_mgf_index_titles.argtypes = [ctypes.c_void_p]
         L.spx_mgf_index_free.argtypes = [ctypes.c_void_p]
+        L.spx_mgf_index_range.restype = ctypes.c_void_p
+        L.spx_mgf_index_range.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+        L.spx_mgf_write_records.restype = ctypes.c_int
+        L.spx_mgf_write_records.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                            ctypes.c_char_p] + [ctypes.c_void_p] * 7 + [ctypes.c_int]
         L.spx_mgf_parse_ranges.restype = ctypes.c_void_p
         L.spx_mgf_parse_ranges.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                            ctypes.c_int, ctypes.c_int]
@@ -138,16 +143,7 @@ def parse_general(path, threads: int = 0):
     return _take_result(L, L.spx_mgf_parse_general(os.fsencode(path), int(threads)), True)
 
 
-def index(path, general: bool):
-    """Record index of an MGF without parsing any number: dict(begin, end, npk,
-    titles) -- record r is bytes [begin[r], end[r]) (from its TITLE= line for the
-    binning reader, from BEGIN IONS for the general one, to the next record's
-    start), npk its peak-line count.  Only records with an END IONS are listed.
-    None when the library is absent."""
-    L = _native()
-    if L is None:
-        return None
-    h = L.spx_mgf_index(os.fsencode(path), int(bool(general)))
+def _take_index(L, h):
     try:
         err = L.spx_mgf_index_error(h)
         if err:
@@ -159,6 +155,29 @@ def index(path, general: bool):
     finally:
         L.spx_mgf_index_free(h)
     return dict(begin=begin, end=end, npk=npk, titles=titles)
+
+
+def index(path, general: bool):
+    """Record index of an MGF without parsing any number: dict(begin, end, npk,
+    titles) -- record r is bytes [begin[r], end[r]) (from its TITLE= line for the
+    binning reader, from BEGIN IONS for the general one, to the next record's
+    start), npk its peak-line count.  Only records with an END IONS are listed.
+    None when the library is absent."""
+    L = _native()
+    if L is None:
+        return None
+    return _take_index(L, L.spx_mgf_index(os.fsencode(path), int(bool(general))))
+
+
+def index_range(path, general: bool, lo: int, hi: int, threads: int = 0):
+    """The records of :func:`index` whose start line lies in bytes [lo, hi): the
+    stripes [k*size/W, (k+1)*size/W) of W ranks list every record exactly once,
+    and each reads only its stripe (plus the tail of its last record)."""
+    L = _native()
+    if L is None:
+        raise RuntimeError(f"native MGF library missing ({MGF_LIB}); run __graft_entry__.build()")
+    return _take_index(L, L.spx_mgf_index_range(os.fsencode(path), int(bool(general)), int(lo), int(hi),
+                                                 int(threads)))
 
 
 def parse_ranges(path, begin, end, general: bool, threads: int = 0):
@@ -225,3 +244,43 @@ CHARGE={spectrum['precursor_charge']}+
         text += "".join(f"{mz} {intensity}\n" for mz, intensity in zip(mzs, ints) if not np.isnan(intensity))
         text += "END IONS\n\n"
         mgf_file.write(text)
+
+
+STYLE_BINNING, STYLE_GAP_AVERAGE, STYLE_MEDOID = 0, 1, 2
+FLAG_PEPMASS, FLAG_CHARGE, FLAG_RT, FLAG_TITLE = 1, 2, 4, 8
+
+
+def write_records(path, style: int, titles, off, mz, inten, prec, charge, rt=None, flags=None,
+                  append: bool = False, threads: int = 0) -> None:
+    """Write len(titles) MGF records with the native multithreaded writer
+    (``spx_mgf_write_records``): style 0 = binning.py:234-245 text, 1 = the
+    gap-average CLI's (:func:`specpride_amd.mgf.write_pyteomics_style`), 2 = the
+    medoid CLI's (:func:`specpride_amd.most_similar_representative.write_record`);
+    record c's peaks are ``mz/inten[off[c]:off[c+1]]``; ``flags`` (styles 1-2) say
+    which of PEPMASS / CHARGE / RTINSECONDS / TITLE are present.  Byte-identical
+    to the Python writers (tests/test_mgf_native.py)."""
+    L = _native()
+    if L is None:
+        raise RuntimeError(f"native MGF library missing ({MGF_LIB}); run __graft_entry__.build()")
+    C = len(titles)
+    if any("\n" in t for t in titles):
+        raise ValueError("record titles cannot contain a newline")
+    off = np.ascontiguousarray(off, np.int64)
+    if len(off) != C + 1:
+        raise ValueError("off must have len(titles) + 1 entries")
+    mz = np.ascontiguousarray(mz, np.float64)
+    inten = np.ascontiguousarray(inten, np.float64)
+    if C and (off[0] < 0 or off[-1] > len(mz) or len(inten) < off[-1] or np.any(np.diff(off) < 0)):
+        raise ValueError("peak offsets out of range")
+    prec = np.ascontiguousarray(prec, np.float64)
+    charge = np.ascontiguousarray(charge, np.int64)
+    rt = np.ascontiguousarray(rt if rt is not None else np.full(C, np.nan), np.float64)
+    flags = np.ascontiguousarray(flags if flags is not None else np.full(C, 15), np.int32)
+    for a in (prec, charge, rt, flags):
+        if len(a) != C:
+            raise ValueError("per-record arrays must have len(titles) entries")
+    joined = "\n".join(titles).encode("utf-8", errors="surrogateescape")
+    rc = L.spx_mgf_write_records(os.fsencode(path), int(bool(append)), int(style), C, joined, _ptr(flags),
+                                 _ptr(prec), _ptr(charge), _ptr(rt), _ptr(off), _ptr(mz), _ptr(inten), int(threads))
+    if rc != 0:
+        raise OSError(f"spx_mgf_write_records failed writing {path}")

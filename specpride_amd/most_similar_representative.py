@@ -146,33 +146,59 @@ def _main_native(inputfile, outputfile):
     runs = [(cl, m) for cl, m in _first_runs([t.split(";")[0] for t in titles]) if m]
     records = np.asarray([i for _cl, m in runs for i in m], np.int64)
     csr = ingest.csr_from_flat(flat, [len(m) for _cl, m in runs], records)
-    so = flat["spec_off"]
     chosen = []
     for cl, members, best in _choose(csr, runs):
         print(cl)
         print(len(members))
         chosen.append(best)
     print(len(chosen))
-    with open(outputfile, "w") as fh:
-        for s in chosen:
-            write_record(fh, titles[s], flat["prec_mz"][s] if flat["has_prec"][s] else None,
-                         int(flat["charge"][s]) if flat["has_charge"][s] else None,
-                         flat["rt"][s] if flat["has_rt"][s] else None,
-                         flat["mz"][so[s]:so[s + 1]], flat["inten"][so[s]:so[s + 1]])
+    write_chosen(outputfile, flat, np.asarray(chosen, np.int64))
     return True
 
 
-def _main_dicts(inputfile, outputfile):
-    from . import sharded_cli
+def write_chosen(outputfile, flat, chosen):
+    """The chosen records of a native parse, verbatim, through the native
+    multithreaded writer (the text of :func:`write_record`)."""
+    from . import mgf_native
+    from .csr import concat_ranges
 
-    if sharded_cli.launched_distributed():  # torchrun: rank-local ingest, one GPU per rank
-        sharded_cli.run_cli(sharded_cli.medoid, lambda: main_single(inputfile, outputfile), inputfile, outputfile)
-        return
-    main_single(inputfile, outputfile)
+    so = flat["spec_off"]
+    lens = so[chosen + 1] - so[chosen]
+    off = np.zeros(len(chosen) + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    idx = concat_ranges(so[chosen], lens)
+    flags = (flat["has_prec"][chosen].astype(np.int32) * mgf_native.FLAG_PEPMASS |
+             flat["has_charge"][chosen].astype(np.int32) * mgf_native.FLAG_CHARGE |
+             flat["has_rt"][chosen].astype(np.int32) * mgf_native.FLAG_RT | mgf_native.FLAG_TITLE)
+    mgf_native.write_records(outputfile, mgf_native.STYLE_MEDOID, [flat["titles"][s] for s in chosen], off,
+                             flat["mz"][idx], flat["inten"][idx], flat["prec_mz"][chosen], flat["charge"][chosen],
+                             flat["rt"][chosen], flags)
+
+
+def _main_dicts(inputfile, outputfile):
+    """main() over the dict reader (``specpride_amd.mgf.read_mgf``): the path for
+    input outside the native parser's subset.  Same cluster scan, prints and
+    output as :func:`_main_native`; a record without TITLE fails as the
+    reference's ``getMetaValue("TITLE").decode()`` does (:50)."""
+    spectra = read_mgf(inputfile)
+    names = []
+    for sp in spectra:
+        title = sp["params"].get("title")
+        if title is None:
+            raise AttributeError("'NoneType' object has no attribute 'decode'")
+        names.append(title.split(";")[0])
+    chosen = []
+    for cl, members, best in representatives(spectra, names):
+        print(cl)
+        print(len(members))
+        chosen.append(spectra[best])
+    print(len(chosen))
+    _write_spectra(chosen, outputfile)
 
 
 def main_single(inputfile, outputfile):
-    """The single-process CLI body: native ingest, else the dict path."""
+    """The single-process CLI body: native ingest, else the dict path (never
+    re-enters the torchrun dispatch: the sharded CLI's rank-0 fallback runs this)."""
     if not _main_native(inputfile, outputfile):
         _main_dicts(inputfile, outputfile)
 
@@ -198,12 +224,6 @@ def main(argv):
         sharded_cli.run_cli(sharded_cli.medoid, lambda: main_single(inputfile, outputfile), inputfile, outputfile)
         return
     main_single(inputfile, outputfile)
-
-
-def main_single(inputfile, outputfile):
-    """The single-process CLI body: native ingest, else the dict path."""
-    if not _main_native(inputfile, outputfile):
-        _main_dicts(inputfile, outputfile)
 
 
 if __name__ == "__main__":

@@ -124,6 +124,34 @@ def gatherv(tensors: list, root: int = 0, group=None) -> Optional[list]:
     return out
 
 
+def allgatherv(arrays: list, group=None) -> list:
+    """All-gather a list of 1-D numpy arrays (same dtypes on every rank, any
+    lengths): returns ``out[rank][i]`` on every rank.  Lengths travel first, then
+    one padded all_gather per array (device tensors under ``nccl``)."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = world_rank(group)
+    if world == 1:
+        return [list(arrays)]
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    lens = torch.tensor([len(a) for a in arrays], dtype=torch.int64, device=dev)
+    all_lens = [torch.empty_like(lens) for _ in range(world)]
+    dist.all_gather(all_lens, lens, group=group)
+    all_lens = [x.cpu().tolist() for x in all_lens]
+    out = [[None] * len(arrays) for _ in range(world)]
+    for i, a in enumerate(arrays):
+        m = max(max(lr[i] for lr in all_lens), 1)
+        buf = torch.zeros(m, dtype=torch.from_numpy(np.zeros(0, a.dtype)).dtype, device=dev)
+        if len(a):
+            buf[:len(a)] = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        bufs = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(bufs, buf, group=group)
+        for r in range(world):
+            out[r][i] = bufs[r][:all_lens[r][i]].cpu().numpy()
+    return out
+
+
 # ------------------------------------------------------------ default compute
 def _engine_consensus(method: str, params: dict, device):
     def run(sub: SpectraCSR) -> dict:

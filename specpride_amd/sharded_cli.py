@@ -3,9 +3,11 @@
 Under ``torchrun`` (WORLD_SIZE > 1) ``binning.main``, ``average_spectrum_clustering
 .main --encodedclusters`` and ``most_similar_representative.main`` run here:
 
-1. every rank indexes the input MGF (``mgf_native.index``: per-record byte range,
-   title, peak-line count -- no number is parsed) and derives the reference's
-   cluster grouping from the titles (:mod:`specpride_amd.ingest`);
+1. rank k indexes only byte stripe [k*size/W, (k+1)*size/W) of the input MGF
+   (``mgf_native.index_range``: the records whose start line lies in it -- byte
+   range, title, peak-line count; no number is parsed; multithreaded), and one
+   all-gather of that metadata gives every rank the whole index, from which it
+   derives the reference's cluster grouping (:mod:`specpride_amd.ingest`);
 2. the clusters are LPT-planned over the ranks from the index's spectrum and
    peak counts (:func:`specpride_amd.shard.plan_costs`) -- every rank computes
    the same plan, no exchange;
@@ -15,7 +17,8 @@ Under ``torchrun`` (WORLD_SIZE > 1) ``binning.main``, ``average_spectrum_cluster
 4. the results (consensus peaks, or the chosen representative spectra) are
    gathered to rank 0 (:func:`specpride_amd.shard.gatherv`: RCCL point-to-point
    over xGMI under ``nccl``, ``gloo`` on CPU), which writes the output file in
-   the reference's order, byte-identical to the single-process run.
+   the reference's order with the native multithreaded writer
+   (``mgf_native.write_records``), byte-identical to the single-process run.
 
 Per-rank compute is injectable (``compute=``: CSR -> dict of tensors, the
 :mod:`specpride_amd.shard` contract) so the CPU test suite drives the same code
@@ -79,15 +82,30 @@ def run_cli(driver: Callable, fallback: Callable, *args, **kwargs):
 
 
 # ------------------------------------------------------------------ shared steps
+def rank_index(path, general: bool, group=None):
+    """The whole file's record index, built rank-locally: this rank indexes its
+    byte stripe and the stripes' metadata is all-gathered (stripes are in file
+    order, so their concatenation is ``mgf_native.index(path, general)``)."""
+    world, rank = shard.world_rank(group)
+    size = os.path.getsize(path)
+    mine = mgf_native.index_range(path, general, rank * size // world, (rank + 1) * size // world)
+    if world == 1:
+        return mine
+    titles = "\n".join(mine["titles"]).encode("utf-8", errors="surrogateescape")
+    got = shard.allgatherv([mine["begin"], mine["end"], mine["npk"], np.frombuffer(titles, np.uint8)], group)
+    X = {k: np.concatenate([g[i] for g in got]) for i, k in enumerate(("begin", "end", "npk"))}
+    X["titles"] = [t for g in got if len(g[0])
+                   for t in g[3].tobytes().decode("utf-8", errors="surrogateescape").split("\n")]
+    return X
+
+
 def _load_my_clusters(path, general: bool, groups: Callable, method: str, group):
     """Index -> grouping -> plan -> parse own records.  Returns (ids, records,
     sizes, parts, mine, X, flat, ok): cluster ids, record indices in CSR order,
     members per cluster, the plan, this rank's clusters, the index, this rank's
     parse (None if outside the native subset) and whether it is usable."""
     world, rank = shard.world_rank(group)
-    X = mgf_native.index(path, general)
-    if X is None:
-        raise RuntimeError("native MGF library missing; run __graft_entry__.build()")
+    X = rank_index(path, general, group)
     ids, records, sizes = groups(X["titles"])
     starts = ingest.cluster_starts(sizes)
     peaks = np.add.reduceat(X["npk"][records], starts[:-1]) if len(records) else np.zeros(0, np.int64)
@@ -125,20 +143,13 @@ def binning(mgf_file: str, out: str, group=None, device=None, compute: Optional[
     r = shard.gather_consensus(res, parts, len(ids), group)
     if r is None:
         return None
-    merged = []
-    for c, cid in enumerate(ids):
-        st = r["status"][c]
-        if st == STATUS_MIXED_CHARGE:
+    bad = np.flatnonzero(r["status"] != STATUS_OK)
+    if len(bad):
+        if r["status"][bad[0]] == STATUS_MIXED_CHARGE:
             raise AssertionError(MIXED_CHARGE_MSG)
-        if st != STATUS_OK:
-            raise IndexError("list index out of range")
-        a, b = r["out_off"][c], r["out_off"][c + 1]
-        merged.append({"minimum": minimum, "maximum": maximum, "binsize": binsize,
-                       "intensities": r["out_int"][a:b], "mzs": r["out_mz"][a:b],
-                       "precursor_mz": np.float64(r["prec"][c]), "precursor_charge": int(r["charge"][c]),
-                       "cluster_id": cid})
-    with open(out, "wt") as fh:
-        mgf_native.write_binning_mgf(merged, fh)
+        raise IndexError("list index out of range")
+    mgf_native.write_records(out, mgf_native.STYLE_BINNING, ids, r["out_off"], r["out_mz"], r["out_int"], r["prec"],
+                             r["charge"])
     return None
 
 
@@ -147,7 +158,7 @@ def gap_average(input_mgf: str, output, group=None, device=None, compute: Option
                 mz_accuracy=0.01, dyn_range=1000.0, min_fraction=0.5, pepmass="lower_median",
                 rt="mass_lower_median", file_mode="w"):
     """average_spectrum_clustering.py ``--encodedclusters`` (:151-165, :201-203), rank-local."""
-    from .average_spectrum_clustering import _raise_for
+    from .average_spectrum_clustering import _raise_for, write_outputs_native
     from .engine import STATUS_OK
     from .mgf import write_pyteomics_style
 
@@ -161,6 +172,9 @@ def gap_average(input_mgf: str, output, group=None, device=None, compute: Option
     res = (compute or _engine_compute("gap_average", params, device))(sub)
     r = shard.gather_consensus(res, parts, len(ids), group)
     if r is None:
+        return None
+    if output is not None:
+        write_outputs_native(r, ids, output, file_mode=file_mode)
         return None
     outputs = []
     for c, cid in enumerate(ids):
@@ -180,8 +194,6 @@ def medoid(inputfile: str, outputfile: str, group=None, device=None, compute: Op
     """most_similar_representative.py main (:22-115), rank-local: each rank sends
     rank 0 only the representative spectra it chose."""
     import torch
-
-    from .most_similar_representative import write_record
 
     ids, records, sizes, parts, mine, X, flat, ok = _load_my_clusters(inputfile, True, ingest.medoid_groups,
                                                                       "medoid", group)
@@ -226,14 +238,10 @@ def medoid(inputfile: str, outputfile: str, group=None, device=None, compute: Op
             mz[dst] = got[r][6].cpu().numpy()
             inten[dst] = got[r][7].cpu().numpy()
     starts = ingest.cluster_starts(sizes)
-    with open(outputfile, "w") as fh:
-        for c, cl in enumerate(ids):
-            if verbose:
-                print(cl)
-                print(int(sizes[c]))
-            title = X["titles"][records[starts[c] + member[c]]]
-            write_record(fh, title, prec[c] if flags[c] & 1 else None, int(charge[c]) if flags[c] & 2 else None,
-                         rt[c] if flags[c] & 4 else None, mz[off[c]:off[c + 1]], inten[off[c]:off[c + 1]])
     if verbose:
+        print("".join(f"{cl}\n{int(sizes[c])}\n" for c, cl in enumerate(ids)), end="")
         print(C)
+    titles = [X["titles"][records[starts[c] + member[c]]] for c in range(C)]
+    mgf_native.write_records(outputfile, mgf_native.STYLE_MEDOID, titles, off, mz, inten, prec, charge, rt,
+                             flags.astype(np.int32) | mgf_native.FLAG_TITLE)
     return None

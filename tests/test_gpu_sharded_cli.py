@@ -85,19 +85,49 @@ def test_gap_average_cli_native_dict_sharded_identical(gpu, rccl_world1, syn, tm
 
 
 @pytest.mark.parametrize("which", ["golden", "syn"])
-def test_medoid_cli_native_dict_sharded_identical(gpu, rccl_world1, syn, tmp_path, which):
+def test_medoid_cli_native_dict_sharded_identical(gpu, rccl_world1, syn, tmp_path, which, monkeypatch):
+    from specpride_amd import mgf_native
+
     src = _src(which, syn, "medoid_noncontiguous.mgf")
     native, dicts, sharded = tmp_path / "n.mgf", tmp_path / "d.mgf", tmp_path / "s.mgf"
     out_n = io.StringIO()
     with contextlib.redirect_stdout(out_n):
         msr.main(["-i", src, "-o", str(native)])
-    out_d = io.StringIO()
-    with contextlib.redirect_stdout(out_d):
-        msr._main_dicts(src, str(dicts))
     out_s = io.StringIO()
     with contextlib.redirect_stdout(out_s):
         assert sharded_cli.medoid(src, str(sharded), device=gpu) is None
+    # dict leg: the native reader is switched off, so main() must take read_mgf
+    seen = []
+    real_read = msr.read_mgf
+    monkeypatch.setattr(mgf_native, "parse_general", lambda *a, **k: None)
+    monkeypatch.setattr(msr, "read_mgf", lambda path: seen.append(path) or real_read(path))
+    out_d = io.StringIO()
+    with contextlib.redirect_stdout(out_d):
+        msr.main(["-i", src, "-o", str(dicts)])
+    assert seen == [src], "the dict path did not run"
     assert out_n.getvalue() == out_d.getvalue() == out_s.getvalue()
     want = native.read_bytes()
     assert dicts.read_bytes() == want
     assert sharded.read_bytes() == want
+
+
+def test_medoid_cli_outside_native_subset(gpu, tmp_path):
+    """A record with two charges ("2+ and 3+") is outside the native reader's
+    subset: main() takes the dict path and still picks the reference's
+    representatives (tests/golden/medoid_noncontiguous.json)."""
+    import json
+
+    from specpride_amd import mgf_native
+    from specpride_amd.mgf import read_mgf
+
+    text = open(os.path.join(GOLDEN, "medoid_noncontiguous.mgf")).read().replace("CHARGE=2+", "CHARGE=2+ and 3+", 1)
+    src = tmp_path / "multi_charge.mgf"
+    src.write_text(text)
+    with pytest.raises(ValueError, match="fallback"):
+        mgf_native.parse_general(str(src))
+    out = tmp_path / "o.mgf"
+    _quiet(msr.main, ["-i", str(src), "-o", str(out)])
+    gold = json.load(open(os.path.join(GOLDEN, "medoid_noncontiguous.json")))
+    got = read_mgf(str(out))
+    assert [s["params"]["title"] for s in got] == gold["titles"]
+    assert got[0]["params"]["charge"] == [2, 3]

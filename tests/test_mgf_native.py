@@ -115,3 +115,114 @@ def test_groupings_match_cli_dict_paths():
     order = list(dict.fromkeys(t.split(";")[0] for t in titles))
     assert ids == order
     assert [titles[i].split(";")[0] for i in records] == sorted((t.split(";")[0] for t in titles), key=order.index)
+
+
+# ------------------------------------------------------------------ striped index
+def _index_concat(path, general, cuts):
+    parts = [mgf_native.index_range(path, general, a, b) for a, b in zip(cuts[:-1], cuts[1:])]
+    return {k: (sum((p[k] for p in parts), []) if k == "titles" else np.concatenate([p[k] for p in parts]))
+            for k in ("begin", "end", "npk", "titles")}
+
+
+@pytest.mark.parametrize("general", [False, True])
+def test_index_range_stripes_compose(tmp_path, general):
+    """Byte stripes at ANY cut points (mid-line, between CR and LF, inside a
+    record) list every record of the whole-file index exactly once, in order --
+    the sharded CLIs' rank-local indexing (sharded_cli.rank_index)."""
+    text = ("junk\r\n" + "".join(
+        f"BEGIN IONS\r\nTITLE=c{k % 7};u{k}\r\nPEPMASS={400 + k}.5\r\nCHARGE=2+\r\n"
+        + "".join(f"{100 + j}.25 {j + 1}.0\r\n" for j in range(k % 5)) + "END IONS\r\n\n" for k in range(40))
+        + "BEGIN IONS\nTITLE=x;no_end\n1 2\n")
+    p = tmp_path / "s.mgf"
+    p.write_bytes(text.encode())
+    whole = mgf_native.index(str(p), general)
+    size = len(text)
+    rng = np.random.default_rng(1)
+    for world in (1, 2, 3, 7, 16):
+        cuts = [w * size // world for w in range(world + 1)]
+        got = _index_concat(str(p), general, cuts)
+        assert got["titles"] == whole["titles"]
+        for k in ("begin", "end", "npk"):
+            np.testing.assert_array_equal(got[k], whole[k])
+    for _ in range(20):
+        cuts = [0] + sorted(rng.integers(0, size, 5).tolist()) + [size]
+        got = _index_concat(str(p), general, cuts)
+        assert got["titles"] == whole["titles"]
+        np.testing.assert_array_equal(got["begin"], whole["begin"])
+        np.testing.assert_array_equal(got["end"], whole["end"])
+    # a CR/LF boundary exactly at the cut
+    cr = text.index("\r\n", 30) + 1
+    got = _index_concat(str(p), general, [0, cr, size])
+    np.testing.assert_array_equal(got["begin"], whole["begin"])
+
+
+# ------------------------------------------------------------------ native writers
+def _py_binning(ids, off, mz, it, prec, charge):
+    """binning.py:234-245's f-string text (numpy floats; NaN intensities skipped)."""
+    out = []
+    for c, cid in enumerate(ids):
+        t = f"BEGIN IONS\nTITLE={cid}\nPEPMASS={np.float64(prec[c])}\nCHARGE={int(charge[c])}+\n"
+        for a, b in zip(mz[off[c]:off[c + 1]], it[off[c]:off[c + 1]]):
+            if not np.isnan(b):
+                t += f"{a} {b}\n"
+        out.append(t + "END IONS\n\n")
+    return "".join(out)
+
+
+def _writer_case(C=9000, seed=0):
+    rng = np.random.default_rng(seed)
+    n = rng.integers(0, 6, C)
+    n[::97] = 0
+    off = np.zeros(C + 1, np.int64)
+    np.cumsum(n, out=off[1:])
+    P = int(off[-1])
+    vals = np.concatenate([[0.0, -0.0, 1e16, 1e-5, 1e-4, 123456789012345.6, 1.0 / 3, np.nan, np.inf, -np.inf,
+                            5e-324, 1.7976931348623157e308, 100.0, 2.5e-7]], axis=None)
+    mz = np.where(rng.random(P) < 0.1, rng.choice(vals, P), np.round(rng.uniform(100, 2000, P) * 10.0 ** (d := rng.integers(0, 12, P))) / 10.0 ** d)
+    it = np.where(rng.random(P) < 0.1, rng.choice(vals, P), rng.lognormal(5, 2, P))
+    prec = np.where(rng.random(C) < 0.1, rng.choice(vals, C), rng.uniform(400, 1200, C))
+    charge = rng.integers(-3, 5, C)
+    rt = np.where(rng.random(C) < 0.1, np.nan, rng.uniform(0, 3600, C))
+    flags = rng.integers(0, 16, C).astype(np.int32)
+    titles = [("" if k % 13 == 0 else f"cluster-{k};mzspec:X:{k}") for k in range(C)]
+    return titles, off, mz, it, prec, charge, rt, flags
+
+
+def test_write_records_binning_style_matches_reference_fstring(tmp_path):
+    titles, off, mz, it, prec, charge, _rt, _f = _writer_case()
+    p = tmp_path / "b.mgf"
+    mgf_native.write_records(str(p), mgf_native.STYLE_BINNING, titles, off, mz, it, prec, charge)
+    assert p.read_text() == _py_binning(titles, off, mz, it, prec, charge)
+
+
+def test_write_records_gap_average_style_matches_python_writer(tmp_path):
+    titles, off, mz, it, prec, charge, rt, _f = _writer_case(seed=1)
+    specs = [{"params": {"title": t, "pepmass": float(prec[c]), "rtinseconds": float(rt[c]), "charge": int(charge[c])},
+              "m/z array": mz[off[c]:off[c + 1]], "intensity array": it[off[c]:off[c + 1]]}
+             for c, t in enumerate(titles)]
+    want = tmp_path / "w.mgf"
+    mgf.write_pyteomics_style(specs, str(want))
+    got = tmp_path / "g.mgf"
+    mgf_native.write_records(str(got), mgf_native.STYLE_GAP_AVERAGE, titles, off, mz, it, prec, charge, rt)
+    assert got.read_bytes() == want.read_bytes()
+    # --append (average_spectrum_clustering.py:183-184, file_mode 'a')
+    mgf.write_pyteomics_style(specs[:50], str(want), file_mode="a")
+    mgf_native.write_records(str(got), mgf_native.STYLE_GAP_AVERAGE, titles[:50], off[:51], mz, it, prec[:50],
+                             charge[:50], rt[:50], append=True)
+    assert got.read_bytes() == want.read_bytes()
+
+
+def test_write_records_medoid_style_matches_write_record(tmp_path):
+    import io
+
+    from specpride_amd.most_similar_representative import write_record
+
+    titles, off, mz, it, prec, charge, rt, flags = _writer_case(seed=2)
+    buf = io.StringIO()
+    for c, t in enumerate(titles):
+        f = int(flags[c])
+        write_record(buf, t if f & 8 else None, prec[c] if f & 1 else None, int(charge[c]) if f & 2 else None,
+                     rt[c] if f & 4 else None, mz[off[c]:off[c + 1]], it[off[c]:off[c + 1]])
+    got = tmp_path / "m.mgf"
+    mgf_native.write_records(str(got), mgf_native.STYLE_MEDOID, titles, off, mz, it, prec, charge, rt, flags)
+    assert got.read_text() == buf.getvalue()
