@@ -200,72 +200,6 @@ def cpu_baseline_parallel(n_clusters: int, seed: int):
                        f"cluster-parallel): {dt:.2f} s")}
 
 
-class Gatherer:
-    """Per-step gather of a rank's results to rank 0 over RCCL, on its own stream.
-
-    Each rank compacts its consensus peaks (capacity layout -> dense) and sends
-    counts, representatives and peaks; rank 0 receives every peer's shard into
-    its own buffers (reordering into global cluster order is a host-side index,
-    not part of the device pass).  The gather of step k runs on `self.stream`
-    while step k+1's kernels run on the compute stream; the results of step k
-    are double-buffered so step k+1 never overwrites what is in flight."""
-
-    def __init__(self, batch, rank, world):
-        import torch
-
-        self.rank, self.world, self.batch = rank, world, batch
-        self.stream = torch.cuda.Stream()
-        self.dev = batch.device
-        self.recv = {}
-
-    def launch(self, bm, md, done_event):
-        """Enqueue the gather of one step's results (after `done_event`); returns
-        an event that completes when this rank's part of the gather has."""
-        import torch
-        import torch.distributed as dist
-
-        with torch.cuda.stream(self.stream):
-            self.stream.wait_event(done_event)
-            if self.rank == 0:
-                ops = []
-                for r in range(1, self.world):
-                    c_r, p_r = self.recv_sizes[r]
-                    bufs = self.recv.get(r)
-                    if bufs is None:
-                        bufs = (torch.empty(c_r, dtype=torch.int64, device=self.dev),
-                                torch.empty(c_r, dtype=torch.int64, device=self.dev),
-                                torch.empty(max(p_r, 1), dtype=torch.float64, device=self.dev),
-                                torch.empty(max(p_r, 1), dtype=torch.float64, device=self.dev))
-                        self.recv[r] = bufs
-                    ops += [dist.P2POp(dist.irecv, b, r) for b in bufs]
-            else:
-                # device-side compaction of this rank's consensus peaks (count known: no sync)
-                _, dmz, dint = bm.compact(stream=self.stream, total=self.send_peaks)
-                n = self.batch.n_clusters
-                one = lambda x: x if x.numel() else torch.zeros(1, dtype=x.dtype, device=x.device)  # noqa: E731
-                ops = [dist.P2POp(dist.isend, bm.count[:n].contiguous(), 0),
-                       dist.P2POp(dist.isend, md.rep[:n].contiguous(), 0),
-                       dist.P2POp(dist.isend, one(dmz), 0), dist.P2POp(dist.isend, one(dint), 0)]
-            for q in (dist.batch_isend_irecv(ops) if ops else []):
-                q.wait()
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-        return ev
-
-    def plan(self, kept_peaks: int):
-        """Exchange the (fixed) per-rank cluster and kept-peak counts once, so
-        every step's receive buffers are sized without a per-step handshake."""
-        import torch
-        import torch.distributed as dist
-
-        sizes = torch.tensor([self.batch.n_clusters, kept_peaks], dtype=torch.int64, device=self.dev)
-        allsz = [torch.empty_like(sizes) for _ in range(self.world)]
-        dist.all_gather(allsz, sizes)
-        self.recv_sizes = [tuple(int(v) for v in t.cpu()) for t in allsz]
-        self.send_peaks = kept_peaks
-        return sum(s[0] for s in self.recv_sizes), sum(s[1] for s in self.recv_sizes)
-
-
 def headline(args, rank, world, local, out):
     import torch
 
@@ -293,8 +227,10 @@ def headline(args, rank, world, local, out):
     bufs = [(bm, md)]
     gat = None
     if world > 1:
+        from specpride_amd.shard import StepGatherer
+
         bufs.append((engine.bin_mean(batch), engine.medoid(batch, check=False)))
-        gat = Gatherer(batch, rank, world)
+        gat = StepGatherer(batch.n_clusters, rank, world, batch.device)
         total_c, total_p = gat.plan(kept)
 
     inflight = [None] * len(bufs)  # per buffer: the event of the gather reading it
@@ -309,7 +245,7 @@ def headline(args, rank, world, local, out):
         if gat is not None:
             ev = torch.cuda.Event()
             ev.record(stream)
-            inflight[i] = gat.launch(b, m, ev)
+            inflight[i] = gat.launch(b, m.rep, ev)
 
     for k in range(args.warmup):
         step(k)

@@ -152,6 +152,87 @@ def allgatherv(arrays: list, group=None) -> list:
     return out
 
 
+class StepGatherer:
+    """Per-step gather of a rank's results to rank 0 (bench.py's multi-GPU step),
+    on its own stream so step k's gather overlaps step k+1's kernels.
+
+    Each rank compacts its consensus peaks (capacity layout -> dense, through the
+    result's ``compact(stream=, total=)``) and sends counts, representatives and
+    peaks point-to-point (RCCL over xGMI under ``nccl``); rank 0 receives every
+    peer's shard into buffers of its own, kept in :attr:`recv` (reordering into
+    global cluster order is a host-side index, not part of the device pass).  The
+    per-rank cluster and kept-peak counts are exchanged once (:meth:`plan`).
+    On a CPU group (``gloo``, the test suite) the stream and events are skipped
+    and the P2P ops are the same."""
+
+    def __init__(self, n_clusters: int, rank: int, world: int, device, group=None):
+        import torch
+
+        self.rank, self.world, self.n, self.group = rank, world, int(n_clusters), group
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.stream = torch.cuda.Stream(device=self.dev) if self.cuda else None
+        self.recv = {}
+        self.recv_sizes = None
+        self.send_peaks = 0
+
+    def plan(self, kept_peaks: int):
+        """Exchange the (fixed) per-rank cluster and kept-peak counts once, so
+        every step's receive buffers are sized without a per-step handshake.
+        Returns the totals over ranks (clusters, kept peaks)."""
+        import torch
+        import torch.distributed as dist
+
+        sizes = torch.tensor([self.n, int(kept_peaks)], dtype=torch.int64, device=self.dev)
+        allsz = [torch.empty_like(sizes) for _ in range(self.world)]
+        dist.all_gather(allsz, sizes, group=self.group)
+        self.recv_sizes = [tuple(int(v) for v in t.cpu()) for t in allsz]
+        self.send_peaks = int(kept_peaks)
+        return sum(x[0] for x in self.recv_sizes), sum(x[1] for x in self.recv_sizes)
+
+    def launch(self, bm, rep, done_event=None):
+        """Enqueue the gather of one step's results (consensus ``bm`` with
+        ``.count`` and ``.compact``, representatives ``rep``) after
+        ``done_event``; returns an event that completes when this rank's part of
+        the gather has (None on CPU, where the call blocks until it has)."""
+        import contextlib
+
+        import torch
+        import torch.distributed as dist
+
+        ctx = torch.cuda.stream(self.stream) if self.cuda else contextlib.nullcontext()
+        with ctx:
+            if self.cuda and done_event is not None:
+                self.stream.wait_event(done_event)
+            if self.rank == 0:
+                ops = []
+                for r in range(1, self.world):
+                    c_r, p_r = self.recv_sizes[r]
+                    bufs = self.recv.get(r)
+                    if bufs is None:
+                        bufs = (torch.empty(max(c_r, 1), dtype=torch.int64, device=self.dev),
+                                torch.empty(max(c_r, 1), dtype=torch.int64, device=self.dev),
+                                torch.empty(max(p_r, 1), dtype=torch.float64, device=self.dev),
+                                torch.empty(max(p_r, 1), dtype=torch.float64, device=self.dev))
+                        self.recv[r] = bufs
+                    ops += [dist.P2POp(dist.irecv, b, r, group=self.group) for b in bufs]
+            else:
+                # device-side compaction of this rank's consensus peaks (count known: no sync)
+                _, dmz, dint = bm.compact(stream=self.stream, total=self.send_peaks)
+                one = lambda x: x if x.numel() else torch.zeros(1, dtype=x.dtype, device=x.device)  # noqa: E731
+                ops = [dist.P2POp(dist.isend, one(bm.count[:self.n].contiguous()), 0, group=self.group),
+                       dist.P2POp(dist.isend, one(rep[:self.n].contiguous()), 0, group=self.group),
+                       dist.P2POp(dist.isend, one(dmz), 0, group=self.group),
+                       dist.P2POp(dist.isend, one(dint), 0, group=self.group)]
+            for q in (dist.batch_isend_irecv(ops) if ops else []):
+                q.wait()
+            if not self.cuda:
+                return None
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return ev
+
+
 # ------------------------------------------------------------ default compute
 def _engine_consensus(method: str, params: dict, device):
     def run(sub: SpectraCSR) -> dict:

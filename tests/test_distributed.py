@@ -100,3 +100,76 @@ def test_plan_is_balanced_partition():
         loads = np.array([cost[p].sum() for p in parts])
         assert loads.max() <= loads.mean() + cost.max()  # LPT bound
     assert [len(p) for p in shard.plan(csr, 1)] == [csr.n_clusters]
+
+
+# ------------------------------------------------ bench.py's per-step gatherer
+class _FakeConsensus:
+    """A consensus result in the capacity layout (cluster c's kept peaks at its
+    input peak offset), as engine.PeaksResult holds it; compact() on the host."""
+
+    def __init__(self, count, cap_off, mz, inten):
+        self.count, self.cap_off, self.mz, self.inten = count, cap_off, mz, inten
+
+    def compact(self, stream=None, total=None):
+        idx = torch.cat([torch.arange(int(a), int(a) + int(n)) for a, n in zip(self.cap_off[:-1], self.count)])
+        off = torch.zeros(len(self.count) + 1, dtype=torch.int64)
+        off[1:] = torch.cumsum(self.count, 0)
+        assert total is None or total == int(off[-1])
+        return off, self.mz[idx], self.inten[idx]
+
+
+def _step_result(rank, step, n_clusters):
+    g = torch.Generator().manual_seed(1000 * rank + 17)
+    cap = torch.randint(1, 9, (n_clusters,), generator=g)
+    count = torch.minimum(cap, torch.randint(0, 9, (n_clusters,), generator=g))  # fixed over steps
+    cap_off = torch.zeros(n_clusters + 1, dtype=torch.int64)
+    cap_off[1:] = torch.cumsum(cap, 0)
+    P = int(cap_off[-1])
+    mz = torch.arange(P, dtype=torch.float64) + 0.25 * step + 1e4 * rank
+    inten = -mz
+    rep = cap_off[:-1] + step % 2
+    return _FakeConsensus(count, cap_off, mz, inten), rep
+
+
+def _gatherer_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 5 + 3 * rank
+        bm, _ = _step_result(rank, 0, n)
+        gat = shard.StepGatherer(n, rank, world, "cpu")
+        totals = gat.plan(int(bm.count.sum()))
+        ok = True
+        for step in range(3):
+            bm, rep = _step_result(rank, step, n)
+            assert gat.launch(bm, rep) is None
+            if rank == 0:
+                for r in range(1, world):
+                    wbm, wrep = _step_result(r, step, 5 + 3 * r)
+                    _, wmz, wint = wbm.compact()
+                    cnt, rp, mz, it = gat.recv[r]
+                    ok &= torch.equal(cnt[:len(wbm.count)], wbm.count) and torch.equal(rp[:len(wrep)], wrep)
+                    ok &= torch.equal(mz[:len(wmz)], wmz) and torch.equal(it[:len(wint)], wint)
+        q.put((rank, ok, totals))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_step_gatherer_gloo(world):
+    """bench.py's multi-GPU step gather (shard.StepGatherer: sizes exchanged once,
+    then per step counts + representatives + compacted peaks point-to-point to
+    rank 0) under gloo: rank 0 holds every peer's step results, step after step."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gatherer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (ok, tot)) for r, ok, tot in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for ok, _ in got.values())
+    want_c = sum(5 + 3 * r for r in range(world))
+    assert all(tot[0] == want_c for _, tot in got.values())
