@@ -18,7 +18,9 @@ over RCCL inside the timed region, on a second stream that overlaps the next
 step's kernels.  value = all ranks' clusters / max-over-ranks time.
 
 Extra keys (single GPU): the gap-average consensus on the same batch, the
-north-star run (1M clusters on one MI355X) and the configs[3] skewed medoid.
+north-star run (1M clusters on one MI355X), the configs[3] skewed medoid, bin-mean
+off the headline's shape and the host-inclusive tier 2 (pageable host CSR -> H2D
+-> kernels -> D2H) at the headline's size.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--clusters C] [--ns-clusters 1000000]
 
@@ -396,6 +398,49 @@ def bin_mean_shapes(args, out):
     out["bin_mean_shapes"] = res
 
 
+def tier2(args, out):
+    """SURVEY.md §8(d) tier 2 at the headline's size (configs[4], 385k clusters, a
+    32 GB packed host CSR in pageable memory): H2D (engine.DeviceBatch.from_host:
+    spx_copy_h2d's pinned staging pool) -> spx_bin_mean + spx_medoid -> compaction
+    and D2H of the consensus peaks and representatives.  Never `value`."""
+    import torch
+
+    from specpride_amd import engine
+    from specpride_amd.csr import SpectraCSR
+    from specpride_amd.synthetic import make_clusters_torch
+
+    t = make_clusters_torch(args.clusters, seed=args.seed + 11)
+    h = {k: engine.to_host_array(t[k]) for k in ("cluster_off", "spec_off", "mz", "inten", "prec_mz", "charge", "rt")}
+    del t
+    torch.cuda.empty_cache()
+    csr = SpectraCSR(h["cluster_off"], h["spec_off"], h["mz"], h["inten"], h["prec_mz"], h["charge"], h["rt"])
+    nbytes = sum(a.nbytes for a in h.values())
+    best = None
+    for _ in range(2):  # the first pass allocates the staging pool and the device memory
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        batch = engine.DeviceBatch.from_host(csr)
+        t1 = time.perf_counter()
+        bm = engine.bin_mean(batch)
+        md = engine.medoid(batch)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        r = bm.to_host()
+        rep, _ = md.to_host()
+        t3 = time.perf_counter()
+        ok = bool(np.all(r["status"] == 0) and np.all(rep >= 0))
+        cur = {"clusters": batch.n_clusters, "host_bytes": int(nbytes), "h2d_s": round(t1 - t0, 4),
+               "h2d_GBs": round(nbytes / (t1 - t0) / 1e9, 2), "kernels_s": round(t2 - t1, 4),
+               "d2h_s": round(t3 - t2, 4), "d2h_bytes": int(16 * r["out_off"][-1] + 8 * len(rep)),
+               "clusters_per_s": round(batch.n_clusters / (t3 - t0), 1), "all_ok": ok}
+        if best is None or cur["clusters_per_s"] > best["clusters_per_s"]:
+            best = cur
+        del batch, bm, md, r, rep
+        torch.cuda.empty_cache()
+    out["tier2_host_inclusive"] = best
+    del csr, h
+
+
 def main():
     args = parse()
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
@@ -407,6 +452,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         config3(args, out)
         bin_mean_shapes(args, out)
+        tier2(args, out)
         if args.ns_clusters > 0:
             north_star(args, out)
     if rank == 0 and want_cpu:

@@ -19,6 +19,8 @@
  *   spx_best_score   <- src/best_spectrum.py:67-100  get_best_representative
  *                       (called per cluster from best_spectrum():170-174)
  *   spx_compact_peaks   (packing helper for the shims' output writers)
+ *   spx_copy_h2d / spx_copy_d2h  (host transfers of pageable batches: the reference
+ *                       holds its spectra in host memory, binning.py:122-167)
  *
  * Conventions
  *   - Every array pointer inside spx_csr / outputs is a DEVICE pointer (HBM),
@@ -199,6 +201,16 @@ int spx_best_score(const spx_csr *csr, const double *score, const int64_t *rank,
  * for k < count[c]; out_off is the exclusive prefix sum of count (device array [C+1]). */
 int spx_compact_peaks(const spx_csr *csr, const spx_peaks_out *src, const int64_t *out_off,
                       double *dst_mz, double *dst_inten, void *stream);
+
+/* Host <-> device copies of batches in PAGEABLE host memory (SURVEY.md §8(d) tier 2).
+ * The bytes are staged through a process-wide pool of pinned buffers by several host
+ * threads, each chunk's DMA (on `stream`) overlapping the next chunk's staging copy.
+ * Unlike the compute entry points these use host threads and a staging pool that is
+ * allocated on first use and shared (calls are serialised).  spx_copy_h2d returns once
+ * the source has been consumed; the device copy is ordered on `stream`.  spx_copy_d2h
+ * returns with dst_host complete (after the work already on `stream`). */
+int spx_copy_h2d(void *dst_device, const void *src_host, size_t nbytes, void *stream);
+int spx_copy_d2h(void *dst_host, const void *src_device, size_t nbytes, void *stream);
 
 int spx_abi_version(void);
 const char *spx_last_error(void); /* thread-local text of the last failure */

@@ -10,6 +10,9 @@
  *                              :200) and OpenMS MascotGenericFile().load
  *                              (most_similar_representative.py:41-43); one well-formed
  *                              subset, checked against the Python reader the shims use
+ *   spx_mgf_group              the three CLIs' cluster groupings (binning.py:160-165,
+ *                              average_spectrum_clustering.py:158,
+ *                              most_similar_representative.py:49-75) from the titles
  *   spx_mgf_index              no reference counterpart: record byte ranges, titles and
  *                              peak-line counts (no number parsed), so ranks of a sharded
  *                              CLI can group the records the reference's way
@@ -65,6 +68,15 @@ void spx_mgf_copy(void* h, int64_t* spec_off, double* mz, double* it, double* pr
 void spx_mgf_copy_rt(void* h, double* rt);
 /* '\n'-joined titles, one per spectrum. */
 const char* spx_mgf_titles(void* h);
+/* title s = bytes [off[s], off[s+1] - 1) of spx_mgf_titles' string; off[S+1]. */
+void spx_mgf_title_offsets(void* h, int64_t* off);
+/* The CLIs' cluster groupings from the titles' ids (TITLE up to the first ';'):
+ * mode 0 binning.py:160-165 (first-appearance ordinal), 1 average_spectrum_clustering.py:158
+ * (consecutive-run ordinal), 2 most_similar_representative.py:49-75 (ordinal inside the id's
+ * first contiguous run, else -1).  key[S]; returns the number of groups (-1: bad mode). */
+int64_t spx_mgf_group(void* h, int mode, int64_t* key);
+/* '\n'-joined ids of the groups of the last spx_mgf_group call, in ordinal order. */
+const char* spx_mgf_group_ids(void* h);
 void spx_mgf_free(void* h);
 
 /* ---- record index ---- */

@@ -66,7 +66,7 @@ class SpxCosineParams(ctypes.Structure):
 # every symbol include/specpride.h declares (checked by tests/test_host.py)
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_gap_average_workspace_size", "spx_gap_average",
             "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
-            "spx_compact_peaks",
+            "spx_compact_peaks", "spx_copy_h2d", "spx_copy_d2h",
             "spx_abi_version", "spx_last_error"]
 
 SPX_ABI_VERSION = 2
@@ -141,6 +141,8 @@ def lib():
     L.spx_binned_cosine_workspace_size.argtypes = [_i64, _i64]
     L.spx_binned_cosine.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _p, _sz, _p]
     L.spx_best_score.argtypes = [_p, _p, _p, _p, _p, _p]
+    L.spx_copy_h2d.argtypes = [_p, _p, _sz, _p]
+    L.spx_copy_d2h.argtypes = [_p, _p, _sz, _p]
     if L.spx_abi_version() != SPX_ABI_VERSION:
         raise RuntimeError(f"libspecpride_hip ABI {L.spx_abi_version()} != {SPX_ABI_VERSION}")
     _lib = L

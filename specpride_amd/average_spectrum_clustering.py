@@ -212,13 +212,13 @@ def _native_runs(fname):
     from . import ingest, mgf_native
 
     try:
-        flat = mgf_native.parse_general(fname)
+        flat = mgf_native.parse_general(fname, group=mgf_native.GROUP_RUNS)
     except ValueError:
         return None
     if flat is None or not flat["has_title"].all():
         return None
-    ids, records, sizes = ingest.gap_average_groups(flat["titles"])
-    return ids, ingest.csr_from_flat(flat, sizes)
+    ids = flat["group_ids"]  # itertools.groupby runs of get_cluster_id(title), in file order
+    return ids, ingest.csr_from_flat(flat, np.bincount(flat["key"], minlength=len(ids)))
 
 
 def write_outputs_native(r, ids, output, file_mode="w"):

@@ -182,37 +182,35 @@ class RepresentativeSpectrumCreator:
 
 def _flat_clusters(path):
     """read_spectra_clustered_mgf + packing without per-spectrum Python objects:
-    the native parser's flat arrays regrouped by cluster (first appearance, members
-    in file order: binning.py:122-167).  None when the file is
-    outside the native subset or a spectrum lacks the fields the reference indexes
-    (the dict path then raises exactly as the reference does)."""
+    the native parser's flat arrays grouped by cluster natively (first appearance,
+    members in file order: binning.py:122-167) -- no copy when the
+    clusters are contiguous in the file.  None when the file is outside the native
+    subset or a spectrum lacks the fields the reference indexes (the dict path then
+    raises exactly as the reference does)."""
     from . import mgf_native
     from .csr import concat_ranges
 
     try:
-        flat = mgf_native.parse_native(path)
-    except ValueError:
+        flat = mgf_native.parse_native(path, group=mgf_native.GROUP_BINNING)
+    except ValueError:  # includes a TITLE without ';' (the reference's parts[1] raises)
         return None
-    if flat is None or not flat["titles"] or not (flat["has_prec"].all() and flat["has_charge"].all()):
+    if flat is None or len(flat["spec_off"]) < 2 or not (flat["has_prec"].all() and flat["has_charge"].all()):
         return None
-    order, cl = {}, []
-    for title in flat["titles"]:
-        parts = title.split(";")
-        if len(parts) < 2:  # the reference's parts[1] raises: let the dict path do it
-            return None
-        cl.append(order.setdefault(parts[0], len(order)))
-    cl = np.asarray(cl, np.int64)
-    perm = np.argsort(cl, kind="stable")
+    key, ids = flat["key"], flat["group_ids"]
+    cluster_off = np.zeros(len(ids) + 1, np.int64)
+    np.cumsum(np.bincount(key, minlength=len(ids)), out=cluster_off[1:])
+    if np.all(key[1:] >= key[:-1]):  # contiguous clusters: the parse order is the CSR order
+        return ids, SpectraCSR(cluster_off, flat["spec_off"], flat["mz"], flat["inten"], flat["prec_mz"],
+                               flat["charge"].astype(np.int32), np.full(len(key), np.nan))
+    perm = np.argsort(key, kind="stable")
     so = flat["spec_off"]
     lens = (so[1:] - so[:-1])[perm]
     spec_off = np.zeros(len(perm) + 1, np.int64)
     np.cumsum(lens, out=spec_off[1:])
     idx = concat_ranges(so[:-1][perm], lens)
-    cluster_off = np.zeros(len(order) + 1, np.int64)
-    np.cumsum(np.bincount(cl, minlength=len(order)), out=cluster_off[1:])
     csr = SpectraCSR(cluster_off, spec_off, flat["mz"][idx], flat["inten"][idx], flat["prec_mz"][perm],
                      flat["charge"][perm].astype(np.int32), np.full(len(perm), np.nan))
-    return list(order.keys()), csr
+    return ids, csr
 
 
 def main(argv=None):

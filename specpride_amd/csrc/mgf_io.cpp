@@ -37,29 +37,44 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/spx_mgf.h"
 
 namespace {
 
+// One thread's parse of a byte range (either grammar): per spectrum its peak
+// count, precursor fields and title; the peaks in file order.
 struct Chunk {
   std::vector<int64_t> npk;     // peaks per spectrum
-  std::vector<double> mz, it, prec;
+  std::vector<double> mz, it, prec, rt;  // rt: general reader only
   std::vector<int64_t> charge;
-  std::vector<int32_t> flags;   // bit0 PEPMASS seen, bit1 CHARGE seen
+  std::vector<int32_t> flags;   // bit0 PEPMASS, bit1 CHARGE (general: bit2 RTINSECONDS, bit3 TITLE)
   std::string titles;           // '\n'-joined
   std::string error;
+  void reserve_for(size_t bytes) {  // a peak line is >= ~8 bytes; most are ~18
+    mz.reserve(bytes / 16);
+    it.reserve(bytes / 16);
+  }
 };
+using GenChunk = Chunk;
 
+// A parse: the threads' chunks kept as they are (no merge copy); the accessors
+// copy them out in parallel.
 struct Result {
-  std::vector<int64_t> spec_off;
-  std::vector<double> mz, it, prec, rt;
-  std::vector<int64_t> charge;
-  std::vector<int32_t> flags;
-  std::string titles, error;
+  std::vector<Chunk> parts;
+  std::vector<int64_t> s_base, p_base;  // first spectrum / peak of each part
+  int64_t S = 0, P = 0;
+  bool with_rt = false;
+  std::string error;
+  std::string titles;  // joined on first request
+  bool titles_built = false;
+  std::vector<int64_t> title_off;  // [S+1] offsets into `titles` (with the '\n's)
+  std::string group_ids;           // '\n'-joined ids of the last spx_mgf_group
 };
 
 inline bool is_py_space(unsigned char c) {
@@ -164,6 +179,7 @@ bool parse_charge(const char* b, const char* e, int64_t& out) {
 }
 
 void parse_range(const char* b, const char* e, Chunk& C) {
+  C.reserve_for((size_t)(e - b));
   bool have = false, stored = true;  // `stored`: END IONS already taken for this TITLE
   int64_t cur_np = 0;
   double cur_prec = 0.0;
@@ -260,15 +276,6 @@ void parse_range(const char* b, const char* e, Chunk& C) {
 // TITLE (string), PEPMASS (mz [intensity]), CHARGE (one charge, "2+", "3-", "2"),
 // RTINSECONDS (float); other params are ignored (the writers do not emit them).
 // Anything else (several charges, non-decimal numbers, non-ASCII) -> fallback.
-struct GenChunk {
-  std::vector<int64_t> npk;
-  std::vector<double> mz, it, prec, rt;
-  std::vector<int64_t> charge;
-  std::vector<int32_t> flags;  // bit0 PEPMASS, bit1 CHARGE, bit2 RTINSECONDS, bit3 TITLE
-  std::string titles;
-  std::string error;
-};
-
 inline bool is_ws(unsigned char c) { return c == ' ' || c == '\t'; }
 
 bool parse_one_charge(const char* b, const char* e, int64_t& out) {
@@ -289,6 +296,7 @@ bool parse_one_charge(const char* b, const char* e, int64_t& out) {
 }
 
 void parse_range_general(const char* b, const char* e, GenChunk& C) {
+  C.reserve_for((size_t)(e - b));
   bool inside = false;
   int64_t cur_np = 0;
   double cur_prec = 0.0, cur_rt = 0.0;
@@ -663,29 +671,41 @@ std::vector<const char*> split_records(const char* b, const char* e, int T, int 
   return cuts;
 }
 
-template <class ChunkT>
-void merge_chunks(std::vector<ChunkT>& chunks, Result* R, bool with_rt) {
-  size_t S = 0, P = 0;
-  for (auto& c : chunks) {
+// Take the threads' chunks as the result (first error wins; no copy).
+void adopt(std::vector<Chunk>&& chunks, Result* R, bool with_rt) {
+  for (auto& c : chunks)
     if (!c.error.empty()) { R->error = c.error; return; }
-    S += c.npk.size();
-    P += c.mz.size();
+  R->parts = std::move(chunks);
+  R->with_rt = with_rt;
+  R->s_base.assign(R->parts.size() + 1, 0);
+  R->p_base.assign(R->parts.size() + 1, 0);
+  for (size_t i = 0; i < R->parts.size(); ++i) {
+    R->s_base[i + 1] = R->s_base[i] + (int64_t)R->parts[i].npk.size();
+    R->p_base[i + 1] = R->p_base[i] + (int64_t)R->parts[i].mz.size();
   }
-  R->spec_off.assign(S + 1, 0);
-  R->mz.reserve(P);
-  R->it.reserve(P);
-  size_t s = 0;
-  for (auto& c : chunks) {
-    for (size_t k = 0; k < c.npk.size(); ++k, ++s) R->spec_off[s + 1] = R->spec_off[s] + c.npk[k];
-    R->mz.insert(R->mz.end(), c.mz.begin(), c.mz.end());
-    R->it.insert(R->it.end(), c.it.begin(), c.it.end());
-    R->prec.insert(R->prec.end(), c.prec.begin(), c.prec.end());
-    R->charge.insert(R->charge.end(), c.charge.begin(), c.charge.end());
-    R->flags.insert(R->flags.end(), c.flags.begin(), c.flags.end());
-    if constexpr (std::is_same<ChunkT, GenChunk>::value) R->rt.insert(R->rt.end(), c.rt.begin(), c.rt.end());
-    R->titles += c.titles;
-  }
-  if (!with_rt) R->rt.assign(S, std::nan(""));
+  R->S = R->s_base.back();
+  R->P = R->p_base.back();
+}
+
+// f(part index) on one thread per part
+template <class F>
+void for_parts(const Result* R, F&& f) {
+  std::vector<std::thread> pool;
+  for (size_t i = 0; i < R->parts.size(); ++i) pool.emplace_back(f, i);
+  for (auto& th : pool) th.join();
+}
+
+void build_titles(Result* R) {
+  if (R->titles_built) return;
+  size_t n = 0;
+  for (auto& c : R->parts) n += c.titles.size();
+  R->titles.reserve(n);
+  for (auto& c : R->parts) R->titles += c.titles;
+  R->title_off.assign((size_t)R->S + 1, 0);
+  int64_t s = 0;
+  for (size_t k = 0; k < R->titles.size(); ++k)
+    if (R->titles[k] == '\n') R->title_off[(size_t)++s] = (int64_t)k + 1;
+  R->titles_built = true;
 }
 
 int default_threads(int threads) {
@@ -802,7 +822,7 @@ void* spx_mgf_parse(const char* path, int threads) {
   std::vector<std::thread> pool;
   for (int i = 0; i < nc; ++i) pool.emplace_back(parse_range, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
   for (auto& th : pool) th.join();
-  merge_chunks(chunks, R, false);
+  adopt(std::move(chunks), R, false);
   return R;
 }
 
@@ -810,22 +830,99 @@ const char* spx_mgf_error(void* h) {
   Result* R = static_cast<Result*>(h);
   return R->error.empty() ? nullptr : R->error.c_str();
 }
-int64_t spx_mgf_n_spectra(void* h) { return (int64_t)static_cast<Result*>(h)->prec.size(); }
-int64_t spx_mgf_n_peaks(void* h) { return (int64_t)static_cast<Result*>(h)->mz.size(); }
+int64_t spx_mgf_n_spectra(void* h) { return static_cast<Result*>(h)->S; }
+int64_t spx_mgf_n_peaks(void* h) { return static_cast<Result*>(h)->P; }
 void spx_mgf_copy(void* h, int64_t* spec_off, double* mz, double* it, double* prec, int64_t* charge, int32_t* flags) {
   Result* R = static_cast<Result*>(h);
-  std::copy(R->spec_off.begin(), R->spec_off.end(), spec_off);
-  std::copy(R->mz.begin(), R->mz.end(), mz);
-  std::copy(R->it.begin(), R->it.end(), it);
-  std::copy(R->prec.begin(), R->prec.end(), prec);
-  std::copy(R->charge.begin(), R->charge.end(), charge);
-  std::copy(R->flags.begin(), R->flags.end(), flags);
+  spec_off[0] = 0;
+  for_parts(R, [&](size_t i) {  // each part straight into its slice of the caller's arrays
+    const Chunk& c = R->parts[i];
+    const int64_t sb = R->s_base[i], pb = R->p_base[i];
+    int64_t o = pb;
+    for (size_t k = 0; k < c.npk.size(); ++k) spec_off[sb + (int64_t)k + 1] = (o += c.npk[k]);
+    if (!c.mz.empty()) {
+      std::memcpy(mz + pb, c.mz.data(), c.mz.size() * sizeof(double));
+      std::memcpy(it + pb, c.it.data(), c.it.size() * sizeof(double));
+    }
+    std::copy(c.prec.begin(), c.prec.end(), prec + sb);
+    std::copy(c.charge.begin(), c.charge.end(), charge + sb);
+    std::copy(c.flags.begin(), c.flags.end(), flags + sb);
+  });
 }
-const char* spx_mgf_titles(void* h) { return static_cast<Result*>(h)->titles.c_str(); }
+const char* spx_mgf_titles(void* h) {
+  Result* R = static_cast<Result*>(h);
+  build_titles(R);
+  return R->titles.c_str();
+}
 void spx_mgf_free(void* h) { delete static_cast<Result*>(h); }
 void spx_mgf_copy_rt(void* h, double* rt) {
   Result* R = static_cast<Result*>(h);
-  std::copy(R->rt.begin(), R->rt.end(), rt);
+  for (size_t i = 0; i < R->parts.size(); ++i) {
+    const Chunk& c = R->parts[i];
+    if (R->with_rt) std::copy(c.rt.begin(), c.rt.end(), rt + R->s_base[i]);
+    else std::fill(rt + R->s_base[i], rt + R->s_base[i + 1], std::nan(""));
+  }
+}
+
+// The three CLIs' cluster groupings of a parse, from the titles' cluster ids
+// (TITLE up to the first ';'), without handing every title to the
+// caller.  key[s] per spectrum:
+//   mode 0 (binning.py:160-165): the id's ordinal in first-appearance order;
+//   mode 1 (average_spectrum_clustering.py:158, itertools.groupby): the ordinal of
+//          the consecutive run s is in;
+//   mode 2 (most_similar_representative.py:49-75): the id's ordinal if s lies in the
+//          id's FIRST contiguous run (the run the reference's range_start scan finds:
+//          ids are taken in first-appearance order, so each scan starts before that
+//          id's first appearance), else -1.
+// Returns the number of groups (ids available from spx_mgf_group_ids), -1 on a bad mode.
+int64_t spx_mgf_group(void* h, int mode, int64_t* key) {
+  Result* R = static_cast<Result*>(h);
+  if (mode < 0 || mode > 2) return -1;
+  build_titles(R);
+  R->group_ids.clear();
+  std::unordered_map<std::string_view, int64_t> seen;
+  seen.reserve((size_t)R->S / 4 + 16);
+  std::string_view prev;
+  int64_t n = 0, cur = -1, run = -1;
+  for (int64_t s = 0; s < R->S; ++s) {
+    const char* t = R->titles.data() + R->title_off[(size_t)s];
+    const size_t len = (size_t)(R->title_off[(size_t)s + 1] - R->title_off[(size_t)s] - 1);
+    const char* semi = static_cast<const char*>(std::memchr(t, ';', len));
+    const std::string_view id(t, semi ? (size_t)(semi - t) : len);
+    if (mode == 1) {
+      if (s == 0 || id != prev) {
+        ++run;
+        R->group_ids.append(id.data(), id.size());
+        R->group_ids += '\n';
+      }
+      key[s] = run;
+      prev = id;
+      continue;
+    }
+    auto it = seen.find(id);
+    if (it == seen.end()) {
+      it = seen.emplace(id, n++).first;
+      R->group_ids.append(id.data(), id.size());
+      R->group_ids += '\n';
+      cur = it->second;  // a new id's first run starts here
+      key[s] = it->second;
+    } else if (mode == 0) {
+      key[s] = it->second;
+    } else if (it->second == cur) {
+      key[s] = cur;  // its first run goes on
+    } else {
+      key[s] = -1;  // a later run: the reference never reaches it
+      cur = -1;
+    }
+  }
+  return mode == 1 ? run + 1 : n;
+}
+const char* spx_mgf_group_ids(void* h) { return static_cast<Result*>(h)->group_ids.c_str(); }
+// Title offsets into spx_mgf_titles' string: title s = [off[s], off[s+1] - 1).
+void spx_mgf_title_offsets(void* h, int64_t* off) {
+  Result* R = static_cast<Result*>(h);
+  build_titles(R);
+  std::copy(R->title_off.begin(), R->title_off.end(), off);
 }
 
 // General MGF (pyteomics-shaped subset, see parse_range_general): same result
@@ -846,7 +943,7 @@ void* spx_mgf_parse_general(const char* path, int threads) {
   for (int i = 0; i < nc; ++i)
     pool.emplace_back(parse_range_general, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
   for (auto& th : pool) th.join();
-  merge_chunks(chunks, R, true);
+  adopt(std::move(chunks), R, true);
   return R;
 }
 
@@ -936,14 +1033,14 @@ void* spx_mgf_parse_ranges(const char* path, const int64_t* begin, const int64_t
     for (int i = 0; i < nc; ++i)
       pool.emplace_back(parse_range_general, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
     for (auto& th : pool) th.join();
-    merge_chunks(chunks, R, true);
+    adopt(std::move(chunks), R, true);
   } else {
     std::vector<Chunk> chunks((size_t)nc);
     for (int i = 0; i < nc; ++i) pool.emplace_back(parse_range, cuts[i], cuts[i + 1], std::ref(chunks[(size_t)i]));
     for (auto& th : pool) th.join();
-    merge_chunks(chunks, R, false);
+    adopt(std::move(chunks), R, false);
   }
-  if (R->error.empty() && (int64_t)R->prec.size() != n) R->error = "fallback: records and parsed spectra differ";
+  if (R->error.empty() && R->S != n) R->error = "fallback: records and parsed spectra differ";
   return R;
 }
 

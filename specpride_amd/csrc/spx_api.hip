@@ -20,6 +20,7 @@
 #include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
+#include "transfer.hip"
 
 namespace {
 
@@ -466,4 +467,29 @@ extern "C" int spx_compact_peaks(const spx_csr* csr, const spx_peaks_out* src, c
   hipLaunchKernelGGL(spx::compact_kernel, dim3(g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), view(csr),
                      src->mz, src->inten, src->count, out_off, dst_mz, dst_inten);
   return check_launch("compact_kernel");
+}
+
+// ------------------------------------------------------------ host transfers
+extern "C" int spx_copy_h2d(void* dst_device, const void* src_host, size_t nbytes, void* stream) {
+  if (nbytes == 0) return SPX_SUCCESS;
+  if (!dst_device || !src_host) return fail(SPX_EINVAL, "spx_copy_h2d: null pointer");
+  const hipError_t e = spx::staged_copy(static_cast<char*>(dst_device), static_cast<const char*>(src_host), nbytes,
+                                        reinterpret_cast<hipStream_t>(stream), true);
+  if (e != hipSuccess) {
+    std::snprintf(g_err, sizeof(g_err), "spx_copy_h2d: %s", hipGetErrorString(e));
+    return SPX_EHIP;
+  }
+  return SPX_SUCCESS;
+}
+
+extern "C" int spx_copy_d2h(void* dst_host, const void* src_device, size_t nbytes, void* stream) {
+  if (nbytes == 0) return SPX_SUCCESS;
+  if (!dst_host || !src_device) return fail(SPX_EINVAL, "spx_copy_d2h: null pointer");
+  const hipError_t e = spx::staged_copy(static_cast<char*>(dst_host), static_cast<const char*>(src_device), nbytes,
+                                        reinterpret_cast<hipStream_t>(stream), false);
+  if (e != hipSuccess) {
+    std::snprintf(g_err, sizeof(g_err), "spx_copy_d2h: %s", hipGetErrorString(e));
+    return SPX_EHIP;
+  }
+  return SPX_SUCCESS;
 }

@@ -105,10 +105,10 @@ class DeviceBatch:
                  ("inten", csr.inten), ("prec_mz", csr.prec_mz), ("charge", csr.charge), ("rt", csr.rt)]
         off, total = _layout(items)
         if total > PACKED_MAX_BYTES:
-            tensors = csr.to_device(device)
+            tensors = _staged_to_device(items, off, total, device)
         else:
             tensors = _packed_to_device(items, off, total, device)
-            tensors.update(n_clusters=csr.n_clusters, n_spectra=csr.n_spectra, n_peaks=csr.n_peaks)
+        tensors.update(n_clusters=csr.n_clusters, n_spectra=csr.n_spectra, n_peaks=csr.n_peaks)
         return cls(tensors, csr.cluster_off, csr.spec_off, span, cluster_ids=csr.cluster_ids, titles=csr.titles)
 
     @classmethod
@@ -153,11 +153,52 @@ def _packed_to_device(items, off, total, device):
     # ordered before later work on this stream, and waited for here like the
     # pageable copies it replaces (so any stream may consume the batch)
     torch.cuda.current_stream(dev.device).synchronize()
-    out = {}
-    for name, a in items:
-        dt = {np.dtype(np.int64): torch.int64, np.dtype(np.float64): torch.float64,
-              np.dtype(np.int32): torch.int32}[a.dtype]
-        out[name] = dev[off[name]:off[name] + a.nbytes].view(dt)
+    return _views(dev, items, off)
+
+
+_TORCH_DT = {np.dtype(np.int64): "int64", np.dtype(np.float64): "float64", np.dtype(np.int32): "int32"}
+
+
+def _views(dev, items, off):
+    import torch
+
+    return {name: dev[off[name]:off[name] + a.nbytes].view(getattr(torch, _TORCH_DT[a.dtype]))
+            for name, a in items}
+
+
+def _staged_to_device(items, off, total, device):
+    """Large batches: one device allocation, each array copied by spx_copy_h2d
+    (pinned staging pool, several host threads, DMA overlapped with the staging
+    copies) straight from the caller's pageable numpy memory; waited for here
+    like the pageable copies it replaces."""
+    import torch
+
+    dev = torch.empty(max(total, 256), dtype=torch.uint8, device=device)
+    stream = torch.cuda.current_stream(dev.device)
+    L = _lib.lib()
+    with torch.cuda.device(dev.device):
+        for name, a in items:
+            a = np.ascontiguousarray(a)
+            _lib.check(L.spx_copy_h2d(dev.data_ptr() + off[name], a.ctypes.data, a.nbytes, stream.cuda_stream),
+                       "spx_copy_h2d")
+    stream.synchronize()
+    return _views(dev, items, off)
+
+
+def to_host_array(t) -> np.ndarray:
+    """A device tensor's contents as a new numpy array: spx_copy_d2h (pinned
+    staging, overlapped) above PACKED_MAX_BYTES, ``.cpu()`` below."""
+    import torch
+
+    n = t.numel() * t.element_size()
+    if n <= PACKED_MAX_BYTES or t.device.type != "cuda":
+        return t.cpu().numpy()
+    t = t.contiguous()
+    np_dt = {torch.int64: np.int64, torch.float64: np.float64, torch.int32: np.int32}[t.dtype]
+    out = np.empty(t.numel(), np_dt)
+    with torch.cuda.device(t.device):
+        _lib.check(_lib.lib().spx_copy_d2h(out.ctypes.data, t.data_ptr(), n,
+                                           torch.cuda.current_stream(t.device).cuda_stream), "spx_copy_d2h")
     return out
 
 
@@ -219,11 +260,15 @@ class PeaksResult:
         return out_off, dmz[:n], dint[:n]
 
     def to_host(self) -> dict:
+        import torch
+
         C, P = self.batch.n_clusters, self.batch.n_peaks
         if 16 * P + 32 * C <= PACKED_MAX_BYTES:
             return self._to_host_small()
         out_off, mz, inten = self.compact()
-        d = dict(out_off=out_off.cpu().numpy(), out_mz=mz.cpu().numpy(), out_int=inten.cpu().numpy(),
+        if self.stream is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        d = dict(out_off=out_off.cpu().numpy(), out_mz=to_host_array(mz), out_int=to_host_array(inten),
                  status=self.status.cpu().numpy(), prec=self.prec.cpu().numpy(), charge=self.charge.cpu().numpy())
         if self.rt is not None:
             d["rt"] = self.rt.cpu().numpy()

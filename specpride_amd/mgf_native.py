@@ -33,8 +33,13 @@ def _native():
             getattr(L, f).restype = ctypes.c_int64
             getattr(L, f).argtypes = [ctypes.c_void_p]
         L.spx_mgf_copy.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 6
-        L.spx_mgf_titles.restype = ctypes.c_char_p
+        L.spx_mgf_titles.restype = ctypes.c_void_p  # raw pointer: sliced with the title offsets
         L.spx_mgf_titles.argtypes = [ctypes.c_void_p]
+        L.spx_mgf_title_offsets.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.spx_mgf_group.restype = ctypes.c_int64
+        L.spx_mgf_group.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.spx_mgf_group_ids.restype = ctypes.c_char_p
+        L.spx_mgf_group_ids.argtypes = [ctypes.c_void_p]
         L.spx_mgf_free.argtypes = [ctypes.c_void_p]
         L.spx_mgf_format_binning.restype = ctypes.c_int64
         L.spx_mgf_format_binning.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
@@ -73,8 +78,33 @@ def _split_titles(raw, n):
     return raw.decode("utf-8", errors="surrogateescape").split("\n")[:n] if n else []
 
 
-def _take_result(L, h, general):
-    """Copy a parse handle's arrays out and free it (ValueError on an error/fallback)."""
+GROUP_BINNING, GROUP_RUNS, GROUP_FIRST_RUNS = 0, 1, 2  # spx_mgf_group modes
+
+
+class Flat(dict):
+    """A native parse: dict(spec_off, mz, inten, prec_mz, charge, has_prec,
+    has_charge[, rt, has_rt, has_title]); ``flat["titles"]`` (every title, a
+    list) is decoded on first use from the raw '\n'-joined bytes, and
+    :meth:`title` decodes one -- a CLI that groups natively never builds the list."""
+
+    def __missing__(self, key):
+        if key != "titles":
+            raise KeyError(key)
+        raw, S = self["_titles_raw"], len(self["spec_off"]) - 1
+        v = raw.decode("utf-8", errors="surrogateescape").split("\n")[:S] if S else []
+        self["titles"] = v
+        return v
+
+    def title(self, s: int) -> str:
+        if "titles" in self:
+            return self["titles"][s]
+        o = self["_title_off"]
+        return self["_titles_raw"][o[s]:o[s + 1] - 1].decode("utf-8", errors="surrogateescape")
+
+
+def _take_result(L, h, general, group=None):
+    """Copy a parse handle's arrays out and free it (ValueError on an error/fallback).
+    ``group`` (a GROUP_* mode): also ``key`` [S] and ``group_ids`` (spx_mgf_group)."""
     try:
         err = L.spx_mgf_error(h)
         if err:
@@ -87,11 +117,19 @@ def _take_result(L, h, general):
         flags = np.empty(S, np.int32)
         L.spx_mgf_copy(h, _ptr(spec_off), _ptr(mz), _ptr(inten), _ptr(prec), _ptr(charge), _ptr(flags))
         L.spx_mgf_copy_rt(h, _ptr(rt))
-        titles = _split_titles(L.spx_mgf_titles(h), S)
+        toff = np.zeros(S + 1, np.int64)
+        L.spx_mgf_title_offsets(h, _ptr(toff))
+        raw = ctypes.string_at(L.spx_mgf_titles(h), int(toff[-1])) if S else b""
+        extra = {}
+        if group is not None:
+            key = np.empty(S, np.int64)
+            n = L.spx_mgf_group(h, int(group), _ptr(key))
+            ids = L.spx_mgf_group_ids(h).decode("utf-8", errors="surrogateescape").split("\n")[:n] if n else []
+            extra = dict(key=key, group_ids=ids)
     finally:
         L.spx_mgf_free(h)
-    d = dict(spec_off=spec_off, mz=mz, inten=inten, prec_mz=prec, charge=charge,
-             has_prec=(flags & 1) != 0, has_charge=(flags & 2) != 0, titles=titles)
+    d = Flat(spec_off=spec_off, mz=mz, inten=inten, prec_mz=prec, charge=charge,
+             has_prec=(flags & 1) != 0, has_charge=(flags & 2) != 0, _titles_raw=raw, _title_off=toff, **extra)
     if general:
         d.update(rt=rt, has_rt=(flags & 4) != 0, has_title=(flags & 8) != 0)
     return d
@@ -120,17 +158,18 @@ def _read_binning_py(clustered_mgf_file):
     return all_spectra
 
 
-def parse_native(path, threads: int = 0):
+def parse_native(path, threads: int = 0, group=None):
     """Native parse into flat arrays; returns None when the library is absent.
-    Result: dict(spec_off, mz, inten, prec_mz, charge, has_prec, has_charge, titles).
-    Raises ValueError where the reference would raise on a line."""
+    Result: dict(spec_off, mz, inten, prec_mz, charge, has_prec, has_charge, titles)
+    (+ key, group_ids with ``group``).  Raises ValueError where the reference would
+    raise on a line."""
     L = _native()
     if L is None:
         return None
-    return _take_result(L, L.spx_mgf_parse(os.fsencode(path), int(threads)), False)
+    return _take_result(L, L.spx_mgf_parse(os.fsencode(path), int(threads)), False, group)
 
 
-def parse_general(path, threads: int = 0):
+def parse_general(path, threads: int = 0, group=None):
     """Native parse of a general (pyteomics-shaped) MGF -- the subset of
     :func:`specpride_amd.mgf.iter_mgf` whose meaning is unambiguous -- into flat
     arrays: dict(spec_off, mz, inten, prec_mz (NaN if absent), charge (0 if
@@ -140,7 +179,7 @@ def parse_general(path, threads: int = 0):
     L = _native()
     if L is None:
         return None
-    return _take_result(L, L.spx_mgf_parse_general(os.fsencode(path), int(threads)), True)
+    return _take_result(L, L.spx_mgf_parse_general(os.fsencode(path), int(threads)), True, group)
 
 
 def _take_index(L, h):

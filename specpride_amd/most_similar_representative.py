@@ -131,28 +131,28 @@ def _choose(csr, runs):
 
 
 def _main_native(inputfile, outputfile):
-    """main() over the native parse: records straight into the CSR, the chosen
-    records written from the flat arrays.  False when the file is outside the
-    native subset or a record has no TITLE (the dict path then decides)."""
+    """main() over the native parse: records straight into the CSR, the reference's
+    cluster scan done natively (spx_mgf_group mode 2), the chosen records written
+    from the flat arrays.  False when the file is outside the native subset or a
+    record has no TITLE (the dict path then decides)."""
     from . import ingest, mgf_native
 
     try:
-        flat = mgf_native.parse_general(inputfile)
+        flat = mgf_native.parse_general(inputfile, group=mgf_native.GROUP_FIRST_RUNS)
     except ValueError:
         return False
     if flat is None or not flat["has_title"].all():
         return False
-    titles = flat["titles"]
-    runs = [(cl, m) for cl, m in _first_runs([t.split(";")[0] for t in titles]) if m]
-    records = np.asarray([i for _cl, m in runs for i in m], np.int64)
-    csr = ingest.csr_from_flat(flat, [len(m) for _cl, m in runs], records)
-    chosen = []
-    for cl, members, best in _choose(csr, runs):
-        print(cl)
-        print(len(members))
-        chosen.append(best)
-    print(len(chosen))
-    write_chosen(outputfile, flat, np.asarray(chosen, np.int64))
+    key, ids = flat["key"], flat["group_ids"]
+    records = np.flatnonzero(key >= 0)  # each id's first run, runs in file order
+    sizes = np.bincount(key[records], minlength=len(ids))
+    csr = ingest.csr_from_flat(flat, sizes, None if len(records) == len(key) else records)
+    rep, _ = engine.medoid(engine.DeviceBatch.from_host(csr), TOLERANCE).to_host()
+    if np.any(rep < 0):
+        raise RuntimeError("medoid engine could not resolve a cluster (see DESIGN.md limits)")
+    print("".join(f"{cl}\n{n}\n" for cl, n in zip(ids, sizes.tolist())), end="")
+    print(len(ids))
+    write_chosen(outputfile, flat, records[rep])
     return True
 
 
@@ -170,7 +170,7 @@ def write_chosen(outputfile, flat, chosen):
     flags = (flat["has_prec"][chosen].astype(np.int32) * mgf_native.FLAG_PEPMASS |
              flat["has_charge"][chosen].astype(np.int32) * mgf_native.FLAG_CHARGE |
              flat["has_rt"][chosen].astype(np.int32) * mgf_native.FLAG_RT | mgf_native.FLAG_TITLE)
-    mgf_native.write_records(outputfile, mgf_native.STYLE_MEDOID, [flat["titles"][s] for s in chosen], off,
+    mgf_native.write_records(outputfile, mgf_native.STYLE_MEDOID, [flat.title(s) for s in chosen], off,
                              flat["mz"][idx], flat["inten"][idx], flat["prec_mz"][chosen], flat["charge"][chosen],
                              flat["rt"][chosen], flags)
 

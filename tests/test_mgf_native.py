@@ -226,3 +226,40 @@ def test_write_records_medoid_style_matches_write_record(tmp_path):
     got = tmp_path / "m.mgf"
     mgf_native.write_records(str(got), mgf_native.STYLE_MEDOID, titles, off, mz, it, prec, charge, rt, flags)
     assert got.read_text() == buf.getvalue()
+
+
+# ------------------------------------------------------------------ native grouping
+def _groupings_from_key(key, ids, mode):
+    """(ids, records, sizes) of ingest.*_groups from spx_mgf_group's key."""
+    if mode == mgf_native.GROUP_FIRST_RUNS:
+        records = np.flatnonzero(key >= 0)
+    else:
+        records = np.argsort(key, kind="stable")
+    return ids, records, np.bincount(key[records], minlength=len(ids))
+
+
+@pytest.mark.parametrize("name", FILES + ["SYN"])
+def test_native_grouping_equals_ingest_groupings(name, tmp_path):
+    """spx_mgf_group's three modes == the CLIs' own groupings (ingest.binning_groups,
+    gap_average_groups, medoid_groups, which restate binning.py:160-165,
+    average_spectrum_clustering.py:158, most_similar_representative.py:49-75)."""
+    if name == "SYN":
+        from test_sharded_cli import synthetic_mgf
+
+        path = synthetic_mgf(str(tmp_path / "syn.mgf"), n_clusters=40, seed=9)
+        # a later run of an earlier cluster, and a cluster that recurs after others
+        text = open(path).read()
+        recs = text.split("BEGIN IONS\n")[1:]
+        path = str(tmp_path / "syn2.mgf")
+        open(path, "w").write("".join("BEGIN IONS\n" + r for r in recs + recs[:3] + recs[10:12]))
+    else:
+        path = os.path.join(GOLD, name)
+    for mode, fn in ((mgf_native.GROUP_BINNING, ingest.binning_groups), (mgf_native.GROUP_RUNS,
+                     ingest.gap_average_groups), (mgf_native.GROUP_FIRST_RUNS, ingest.medoid_groups)):
+        flat = mgf_native.parse_general(path, group=mode)
+        want = fn(flat["titles"])
+        got = _groupings_from_key(flat["key"], flat["group_ids"], mode)
+        assert got[0] == want[0]
+        np.testing.assert_array_equal(got[1], want[1])
+        np.testing.assert_array_equal(got[2], want[2])
+        assert [flat.title(s) for s in range(len(flat["key"]))] == flat["titles"]
