@@ -367,6 +367,33 @@ def config3(args, out):
     torch.cuda.empty_cache()
 
 
+def medoid_shapes(args, out):
+    """Medoid on 600-peak spectra: U{2..50} clusters whose
+    peaks (> 12,288) or distinct 0.1-bins (> 1,728) exceed the register kernel's
+    caps from n ~ 20 on, so the MFMA Gram path runs at mid-size n."""
+    import torch
+
+    from specpride_amd import engine
+    from specpride_amd.synthetic import make_clusters_torch
+
+    t = make_clusters_torch(20000, seed=6, n_template=600)
+    batch = engine.DeviceBatch.from_device(t)
+    md = engine.medoid(batch, check=True)
+    torch.cuda.synchronize()
+    ok = bool(np.all(md.rep.cpu().numpy()[:batch.n_clusters] >= 0))
+    ms = time_launches(lambda: engine.medoid(batch, out=md, check=False), 5, torch.cuda.current_stream())
+    co, so = batch.host_cluster_off, batch.host_spec_off
+    sizes, peaks = np.diff(co), so[co[1:]] - so[co[:-1]]
+    large = (sizes > 64) | (peaks > 12288)
+    out["medoid_shapes"] = {"long_spectra_600": {
+        "clusters": batch.n_clusters, "spectra": batch.n_spectra, "peaks": batch.n_peaks,
+        "large_path_by_size": int(large.sum()), "ms": round(ms, 3),
+        "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1), "all_resolved": ok,
+        "roofline": roofline("spx_medoid", "all medoid kernels", medoid_bytes(batch), ms)}}
+    del md, batch, t
+    torch.cuda.empty_cache()
+
+
 def bin_mean_shapes(args, out):
     """Bin-mean off the headline's shape: the configs[3]
     skewed size law (clusters up to n = 5,000: the LDS and global-scratch paths)
@@ -452,6 +479,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras:
         config3(args, out)
         bin_mean_shapes(args, out)
+        medoid_shapes(args, out)
         tier2(args, out)
         if args.ns_clusters > 0:
             north_star(args, out)

@@ -490,6 +490,20 @@ constexpr int BR_PFC = SPX_BR_PFC;    // phase-C (m/z, intensity) loads in fligh
 // none 2.24, 6 2.20, 8 2.14 ms); 12 or 20 at 4 waves/SIMD measured 2.28 / 2.23 ms
 // (fewer clusters in flight)
 constexpr int BR_KM = SPX_BR_KM;
+// Phase A walks the spectra LAST to first (it has no order constraint), so the m/z
+// phase C re-reads first -- spectrum BR_KM, BR_KM+1, ... -- are the ones phase A
+// read most recently: the re-read runs LIFO against the L2 instead of cycling
+// through it (forward, every re-read line was the oldest of the cluster's)
+#ifndef SPX_BR_REV
+#define SPX_BR_REV 0
+#endif
+#if SPX_BR_REV && SPX_BR_KM != 0
+#error "the reversed phase A keeps no m/z in registers: build with -DSPX_BR_KM=0"
+#endif
+// phase C's loads are the last use of their lines: non-temporal (nt) policy
+#ifndef SPX_BR_NT
+#define SPX_BR_NT 0
+#endif
 constexpr int BR_W32 = 2 * BM_WMAX;   // 32-bit occupancy words
 // phases C-D accumulator of one slot: (intensity, m/z) sums and the contribution count
 struct alignas(16) BinAcc {
@@ -632,15 +646,10 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       m = bf_load(rmz, k * 8, 0);
     };
 #pragma unroll
-    for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
-#pragma unroll
     for (int j = 0; j < BR_NMAX; ++j) code[j] = -1;
-    reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
+    auto body = [&](auto jc, const double m, const int len) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      const double m = ra[j % BR_PFA];
-      if constexpr (j < BR_KM) mk[j] = m;
-      const int len = rl[j % BR_PFA];
-      fetch(j + BR_PFA, ra[j % BR_PFA], rl[j % BR_PFA]);
+      if constexpr (j < BR_KM && !SPX_BR_REV) mk[j] = m;  // (reversed: no register-kept m/z)
       const bool act = fpos < len;
       const bool inr = act & (m >= P.minimum) & (m < P.maximum);
       const int32_t kb = bin_small(m, P);  // used only where inr
@@ -657,7 +666,49 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       // opaque to the compiler: phase B re-tests code >= 0 by a compare instead of
       // keeping each step's 64-bit valid mask live (50 SGPR pairs: spills)
       asm volatile("" : "+v"(code[j]));
+    };
+#if SPX_BR_REV
+    // step t reads spectrum n-1-t into code[t] (compile-time slots, the forward
+    // ring); the codes are put back in spectrum order after the loop
+#pragma unroll
+    for (int t = 0; t < BR_PFA; ++t) fetch(n - 1 - t < 0 ? 0 : n - 1 - t, ra[t], rl[t]);
+    reg_steps(n, [&](auto tc) __attribute__((always_inline)) {
+      constexpr int t = decltype(tc)::value;
+      const double m = ra[t % BR_PFA];
+      const int len = rl[t % BR_PFA];
+      const int nx = n - 1 - (t + BR_PFA);
+      fetch(nx < 0 ? 0 : nx, ra[t % BR_PFA], rl[t % BR_PFA]);
+      body(tc, m, len);
     });
+    {
+      // spectrum j's code is code[n-1-j] = rev[j + (BR_NMAX - n)] with rev[i] =
+      // code[BR_NMAX-1-i]: a compile-time reversal, then a left shift by the
+      // uniform BR_NMAX - n in binary steps
+      int32_t rv[BR_NMAX];
+#pragma unroll
+      for (int i = 0; i < BR_NMAX; ++i) rv[i] = code[BR_NMAX - 1 - i];
+      const int sh = __builtin_amdgcn_readfirstlane(BR_NMAX - n);
+#pragma unroll
+      for (int k = 32; k >= 1; k >>= 1) {
+        if (k < BR_NMAX && (sh & k)) {
+#pragma unroll
+          for (int i = 0; i + k < BR_NMAX; ++i) rv[i] = rv[i + k];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < BR_NMAX; ++i) code[i] = rv[i];
+    }
+#else
+#pragma unroll
+    for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
+    reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      const double m = ra[j % BR_PFA];
+      const int len = rl[j % BR_PFA];
+      fetch(j + BR_PFA, ra[j % BR_PFA], rl[j % BR_PFA]);
+      body(jc, m, len);
+    });
+#endif
   }
   // phase C's first (m/z, intensity) loads go out now and land during phase B
   // (whose barriers are LDS-only, so they stay in flight)
@@ -665,8 +716,8 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 #pragma unroll
   for (int j = 0; j < BR_PFC; ++j) {
     const int bo = boffb(j);
-    if (j >= BR_KM) rm[j] = bf_load(rmz, bo, 0);
-    ri[j] = bf_load(rit, bo, 0);
+    if (j >= BR_KM) rm[j] = SPX_BR_NT ? bf_load_nt(rmz, bo, 0) : bf_load(rmz, bo, 0);
+    ri[j] = SPX_BR_NT ? bf_load_nt(rit, bo, 0) : bf_load(rit, bo, 0);
   }
   if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
   SPX_STAMP(2);
@@ -696,8 +747,8 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     else m = rm[j % BR_PFC];
     const double it = ri[j % BR_PFC];
     const int bo = boffb(j + BR_PFC);
-    if constexpr (j + BR_PFC >= BR_KM) rm[j % BR_PFC] = bf_load(rmz, bo, 0);
-    ri[j % BR_PFC] = bf_load(rit, bo, 0);
+    if constexpr (j + BR_PFC >= BR_KM) rm[j % BR_PFC] = SPX_BR_NT ? bf_load_nt(rmz, bo, 0) : bf_load(rmz, bo, 0);
+    ri[j % BR_PFC] = SPX_BR_NT ? bf_load_nt(rit, bo, 0) : bf_load(rit, bo, 0);
     const int slot = code[j];
     BinAcc a = L.u.acc[slot];
     a.i = (float)((double)a.i + it);

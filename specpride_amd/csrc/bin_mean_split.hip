@@ -80,6 +80,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_split_plan_kernel(
         charge_out[c] = 0;
         status[c] = kMixedCharge;
       }
+      lds_barrier();  // every wave has read the votes before the next cluster's vote reuses them
       continue;
     }
     // occupancy of the whole cluster (any order, NaN not in range)
@@ -127,17 +128,19 @@ __global__ __launch_bounds__(BM_BLOCK) void bin_mean_split_plan_kernel(
     int ropen = block_exclusive_scan<BM_BLOCK, int, true>(opens, L.tmp, nr);
     // a cluster without in-range peaks needs no range (its output is empty)
     if (tot == 0) nr = 0;
-    if (tid == 0) {
-      int base = -1;
-      if (nr > 0) {
-        base = atomicAdd(n_ranges, nr);
-        if (base + nr > range_cap) base = -2;
-      }
-      L.base = base;
-    }
+    if (tid == 0) L.base = nr > 0 ? atomicAdd(n_ranges, nr) : -1;
     lds_barrier();
     const int base = L.base;
-    if (base == -2) {  // out of range records: the global kernel
+    if (base >= 0 && base + nr > range_cap) {
+      // out of range records: the global kernel takes the cluster; the records it
+      // reserved below the cap are marked dropped, so the fold (which walks every
+      // record under min(n_ranges, range_cap)) never reads one left unwritten
+      for (int r = base + tid; r < range_cap; r += BM_BLOCK) {
+        SplitRange R;
+        R.cl = -1;
+        R.w0 = R.w1 = R.slot_base = R.kept = R.pad = 0;
+        ranges[r] = R;
+      }
       if (tid == 0) glist[atomicAdd(n_glist, 1)] = (int32_t)c;
       lds_barrier();
       continue;

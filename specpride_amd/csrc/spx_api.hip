@@ -122,8 +122,14 @@ const char* spx_last_error(void) { return g_err; }
 // range records of the split path: every range holds >= SP_CAPW occupied bins
 // except each cluster's last, so C + P / SP_CAPW bounds them (capped; clusters past
 // the cap take the global kernel)
+// SPX_SPLIT_RANGE_CAP (environment, tests only) lowers the cap so the overflow
+// path -- clusters handed to the global kernel -- runs on small batches
 int32_t split_range_cap(const spx_csr* csr) {
-  const int64_t r = csr->n_clusters + csr->n_peaks / spx::SP_CAPW + 1;
+  int64_t r = csr->n_clusters + csr->n_peaks / spx::SP_CAPW + 1;
+  if (const char* e = std::getenv("SPX_SPLIT_RANGE_CAP")) {
+    const long v = std::strtol(e, nullptr, 10);
+    if (v > 0) r = std::min<int64_t>(r, v);
+  }
   return (int32_t)std::max<int64_t>(1, std::min<int64_t>(r, int64_t(1) << 20));
 }
 

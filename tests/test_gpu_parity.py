@@ -451,3 +451,14 @@ def test_bin_mean_split_path(gpu):
     want = c_oracle.bin_mean(csr)
     assert_bin_mean_equal(got, want)
     assert np.any(want["status"] == engine.STATUS_MIXED_CHARGE)
+    # a tiny range-record cap (SPX_SPLIT_RANGE_CAP, read by the library per call): the
+    # clusters that overflow it -- one straddling the cap among them -- go to the
+    # global kernel and their reserved records are dropped, never read unwritten
+    import os
+
+    for cap in ("1", "3", "7"):
+        os.environ["SPX_SPLIT_RANGE_CAP"] = cap
+        try:
+            assert_bin_mean_equal(_bin_mean(csr), want)
+        finally:
+            del os.environ["SPX_SPLIT_RANGE_CAP"]

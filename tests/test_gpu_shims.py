@@ -240,7 +240,7 @@ def test_staged_host_transfers_round_trip(gpu):
         got = engine.to_host_array(b.t[k])
         np.testing.assert_array_equal(got, getattr(csr, k), err_msg=k)
     rng = np.random.default_rng(3)
-    for n in (1, 8 << 20 // 8 + 3, (9 << 20) + 7, 17 * (8 << 20) // 8 + 1):
+    for n in (1, (1 << 20) + 3, (9 << 20) + 7, 17 * (1 << 20) + 1):  # f64 elements
         a = rng.standard_normal(n)
         d = torch.empty(n, dtype=torch.float64, device="cuda")
         from specpride_amd import _lib
