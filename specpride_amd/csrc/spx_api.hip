@@ -17,10 +17,15 @@
 #include "best_score.hip"
 #include "bin_mean.hip"
 #include "bin_mean_split.hip"
+#include "bin_mean_wide.hip"
 #include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
 #include "transfer.hip"
+
+#ifndef SPX_BM_WIDE
+#define SPX_BM_WIDE 1  // the register kernel's leftovers: bin_mean_wide_kernel (0: the older bin_mean_lds_kernel)
+#endif
 
 namespace {
 
@@ -188,9 +193,15 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                      charge_out, status, rest, n_rest, def, n_def);
   if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
+#if SPX_BM_WIDE
+  hipLaunchKernelGGL(spx::bin_mean_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),
+                     dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
+  if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
+#else
   hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),
                      dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
   if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
+#endif
   const dim3 gsplit((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048)));
   hipLaunchKernelGGL(spx::bin_mean_split_plan_kernel, gsplit, dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                      charge_out, status, def, n_def, scl, n_scl, ranges, n_ranges, range_cap, glist, n_glist);

@@ -318,6 +318,35 @@ def test_bin_mean_edge_shapes(gpu):
     assert_bin_mean_equal(_bin_mean(csr), np_oracle.bin_mean(csr))
 
 
+def test_bin_mean_chunk_boundaries(gpu):
+    """bin_mean_wide_kernel walks long spectra in 252-position chunks: runs of one
+    bin straddling a chunk boundary (positions 251/252, 503/504), spectra of exactly
+    252 and 504 peaks, an empty spectrum between long ones, 128 spectra of 260 peaks
+    (the most a cluster may have there) -- bit-exact against the C oracle."""
+    rng = np.random.default_rng(5)
+
+    def spec(mz):
+        mz = np.asarray(mz, np.float64)
+        return {"m/z array": mz, "intensity array": np.round(rng.lognormal(4, 1, len(mz)), 2),
+                "precursor mz": 500.0, "precursor charge": 2}
+
+    def straddle(n, cuts):
+        m = np.sort(rng.uniform(120.0, 1900.0, n))
+        for k in cuts:  # positions k-2 .. k+1 in one 0.02 bin
+            b = 100.0 + 0.02 * np.floor((m[k] - 100.0) / 0.02)
+            m[k - 2:k + 2] = b + np.array([0.001, 0.005, 0.009, 0.013])
+        return np.sort(m)
+
+    clusters = [
+        [spec(straddle(600, [252, 504])), spec(straddle(700, [252, 504])), spec(straddle(300, [252]))],
+        [spec(np.sort(rng.uniform(100, 2000, 252))), spec(np.sort(rng.uniform(100, 2000, 504))),
+         spec(np.zeros(0)), spec(np.sort(rng.uniform(100, 2000, 253)))],
+        [spec(straddle(260, [252])) for _ in range(128)],
+    ]
+    csr = SpectraCSR.from_clusters(clusters)
+    assert_bin_mean_equal(_bin_mean(csr), c_oracle.bin_mean(csr))
+
+
 def test_bin_mean_skewed_and_unsorted(gpu):
     """Skewed sizes (>128 spectra -> deferred) and shuffled spectra (deferred) mixed
     with regular clusters in one launch: bit-exact against the oracle."""
