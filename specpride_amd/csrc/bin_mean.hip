@@ -140,17 +140,17 @@ __device__ __forceinline__ void sorted_lane(const BinMeanState<PrefixT, CountT>&
 // earlier stripes + kept in earlier waves of its stripe + earlier lanes of its wave
 // (ballot).  Per-(stripe, wave) counts go to `wcnt` (the dead bitmap): one barrier.
 // Returns the number of peaks written.
-template <class Cnt, class AccI, class AccM>
+template <int BLOCK = BM_BLOCK, class Cnt, class AccI, class AccM>
 __device__ __forceinline__ int emit_striped_f(const Cnt& cnt, const AccI& acc_i, const AccM& acc_m, int* wcnt,
                                               int D, uint32_t quorum, double* __restrict__ omz,
                                               double* __restrict__ oint) {
-  constexpr int NW = BM_BLOCK / kWave;
+  constexpr int NW = BLOCK / kWave;
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
-  const int per = (D + BM_BLOCK - 1) / BM_BLOCK;  // <= BM_DCAP / BM_BLOCK
+  const int per = (D + BLOCK - 1) / BLOCK;  // <= 32 stripes
   const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t keep = 0u;  // bit j: slot j*256 + tid is emitted
   for (int j = 0; j < per; ++j) {
-    const int d = j * BM_BLOCK + tid;
+    const int d = j * BLOCK + tid;
     const bool k = d < D && (uint32_t)cnt(d) >= quorum && !isnan(acc_i(d));  // cnt >= 1: mean NaN iff sum NaN
     const unsigned long long b = __ballot(k);
     if (lane == 0) wcnt[j * NW + wid] = __popcll(b);
@@ -169,7 +169,7 @@ __device__ __forceinline__ int emit_striped_f(const Cnt& cnt, const AccI& acc_i,
     const bool k = (keep >> j) & 1u;
     const unsigned long long b = __ballot(k);
     if (k) {
-      const int d = j * BM_BLOCK + tid;
+      const int d = j * BLOCK + tid;
       const int o = base + before + __popcll(b & below);
       const double cn = (double)cnt(d);
       const float si = acc_i(d), sm = acc_m(d);
@@ -180,11 +180,11 @@ __device__ __forceinline__ int emit_striped_f(const Cnt& cnt, const AccI& acc_i,
   }
   return base;
 }
-template <class CountT, class AccI, class AccM>
+template <int BLOCK = BM_BLOCK, class CountT, class AccI, class AccM>
 __device__ __forceinline__ int emit_striped(const CountT* cnt, const AccI& acc_i, const AccM& acc_m, int* wcnt,
                                             int D, uint32_t quorum, double* __restrict__ omz,
                                             double* __restrict__ oint) {
-  return emit_striped_f([&](int d) { return (uint32_t)cnt[d]; }, acc_i, acc_m, wcnt, D, quorum, omz, oint);
+  return emit_striped_f<BLOCK>([&](int d) { return (uint32_t)cnt[d]; }, acc_i, acc_m, wcnt, D, quorum, omz, oint);
 }
 
 template <bool kSmall, class PrefixT, class CountT>
@@ -490,20 +490,6 @@ constexpr int BR_PFC = SPX_BR_PFC;    // phase-C (m/z, intensity) loads in fligh
 // none 2.24, 6 2.20, 8 2.14 ms); 12 or 20 at 4 waves/SIMD measured 2.28 / 2.23 ms
 // (fewer clusters in flight)
 constexpr int BR_KM = SPX_BR_KM;
-// Phase A walks the spectra LAST to first (it has no order constraint), so the m/z
-// phase C re-reads first -- spectrum BR_KM, BR_KM+1, ... -- are the ones phase A
-// read most recently: the re-read runs LIFO against the L2 instead of cycling
-// through it (forward, every re-read line was the oldest of the cluster's)
-#ifndef SPX_BR_REV
-#define SPX_BR_REV 0
-#endif
-#if SPX_BR_REV && SPX_BR_KM != 0
-#error "the reversed phase A keeps no m/z in registers: build with -DSPX_BR_KM=0"
-#endif
-// phase C's loads are the last use of their lines: non-temporal (nt) policy
-#ifndef SPX_BR_NT
-#define SPX_BR_NT 0
-#endif
 constexpr int BR_W32 = 2 * BM_WMAX;   // 32-bit occupancy words
 // phases C-D accumulator of one slot: (intensity, m/z) sums and the contribution count
 struct alignas(16) BinAcc {
@@ -649,7 +635,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     for (int j = 0; j < BR_NMAX; ++j) code[j] = -1;
     auto body = [&](auto jc, const double m, const int len) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      if constexpr (j < BR_KM && !SPX_BR_REV) mk[j] = m;  // (reversed: no register-kept m/z)
+      if constexpr (j < BR_KM) mk[j] = m;
       const bool act = fpos < len;
       const bool inr = act & (m >= P.minimum) & (m < P.maximum);
       const int32_t kb = bin_small(m, P);  // used only where inr
@@ -667,38 +653,6 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       // keeping each step's 64-bit valid mask live (50 SGPR pairs: spills)
       asm volatile("" : "+v"(code[j]));
     };
-#if SPX_BR_REV
-    // step t reads spectrum n-1-t into code[t] (compile-time slots, the forward
-    // ring); the codes are put back in spectrum order after the loop
-#pragma unroll
-    for (int t = 0; t < BR_PFA; ++t) fetch(n - 1 - t < 0 ? 0 : n - 1 - t, ra[t], rl[t]);
-    reg_steps(n, [&](auto tc) __attribute__((always_inline)) {
-      constexpr int t = decltype(tc)::value;
-      const double m = ra[t % BR_PFA];
-      const int len = rl[t % BR_PFA];
-      const int nx = n - 1 - (t + BR_PFA);
-      fetch(nx < 0 ? 0 : nx, ra[t % BR_PFA], rl[t % BR_PFA]);
-      body(tc, m, len);
-    });
-    {
-      // spectrum j's code is code[n-1-j] = rev[j + (BR_NMAX - n)] with rev[i] =
-      // code[BR_NMAX-1-i]: a compile-time reversal, then a left shift by the
-      // uniform BR_NMAX - n in binary steps
-      int32_t rv[BR_NMAX];
-#pragma unroll
-      for (int i = 0; i < BR_NMAX; ++i) rv[i] = code[BR_NMAX - 1 - i];
-      const int sh = __builtin_amdgcn_readfirstlane(BR_NMAX - n);
-#pragma unroll
-      for (int k = 32; k >= 1; k >>= 1) {
-        if (k < BR_NMAX && (sh & k)) {
-#pragma unroll
-          for (int i = 0; i + k < BR_NMAX; ++i) rv[i] = rv[i + k];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < BR_NMAX; ++i) code[i] = rv[i];
-    }
-#else
 #pragma unroll
     for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
     reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
@@ -708,7 +662,6 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       fetch(j + BR_PFA, ra[j % BR_PFA], rl[j % BR_PFA]);
       body(jc, m, len);
     });
-#endif
   }
   // phase C's first (m/z, intensity) loads go out now and land during phase B
   // (whose barriers are LDS-only, so they stay in flight)
@@ -716,8 +669,8 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 #pragma unroll
   for (int j = 0; j < BR_PFC; ++j) {
     const int bo = boffb(j);
-    if (j >= BR_KM) rm[j] = SPX_BR_NT ? bf_load_nt(rmz, bo, 0) : bf_load(rmz, bo, 0);
-    ri[j] = SPX_BR_NT ? bf_load_nt(rit, bo, 0) : bf_load(rit, bo, 0);
+    if (j >= BR_KM) rm[j] = bf_load(rmz, bo, 0);
+    ri[j] = bf_load(rit, bo, 0);
   }
   if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
   SPX_STAMP(2);
@@ -747,8 +700,8 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     else m = rm[j % BR_PFC];
     const double it = ri[j % BR_PFC];
     const int bo = boffb(j + BR_PFC);
-    if constexpr (j + BR_PFC >= BR_KM) rm[j % BR_PFC] = SPX_BR_NT ? bf_load_nt(rmz, bo, 0) : bf_load(rmz, bo, 0);
-    ri[j % BR_PFC] = SPX_BR_NT ? bf_load_nt(rit, bo, 0) : bf_load(rit, bo, 0);
+    if constexpr (j + BR_PFC >= BR_KM) rm[j % BR_PFC] = bf_load(rmz, bo, 0);
+    ri[j % BR_PFC] = bf_load(rit, bo, 0);
     const int slot = code[j];
     BinAcc a = L.u.acc[slot];
     a.i = (float)((double)a.i + it);

@@ -1,6 +1,6 @@
 // Bin-mean for the clusters the register kernel does not take: up to 128
 // spectra of ANY length and up to BW_DCAP distinct bins (reference:
-// src/binning.py:170-231, combine_bin_mean).  One 256-thread
+// src/binning.py:170-231, combine_bin_mean).  One 512-thread
 // workgroup per cluster, grid-stride over the register kernel's leftovers:
 //
 //   set-up  spectrum offsets and precursors into LDS, the mixed-charge vote
@@ -8,7 +8,7 @@
 //   1  one flat coalesced pass over the cluster's m/z (16 loads in flight per
 //      thread, any order): occupied bins into the LDS bitmap
 //   2  popcount prefix -> every occupied bin's slot, in ascending bin order
-//   3  the ordered fold over WORK ITEMS = (spectrum, 252-position chunk) in file
+//   3  the ordered fold over WORK ITEMS = (spectrum, 504-position chunk) in file
 //      order, a register ring BW_PF items deep: wave w's lanes 0..62 own positions
 //      63w..63w+62 of the chunk and lane 63 reads position 63w+63 only to hand lane
 //      62 its neighbour key (for the last wave that is the NEXT chunk's first
@@ -38,48 +38,38 @@ namespace spx {
 #define SPX_BW_PF 8
 #endif
 #ifndef SPX_BW_MINW
-#define SPX_BW_MINW 2
+#define SPX_BW_MINW 4
+#endif
+#ifndef SPX_BW_BLOCK
+#define SPX_BW_BLOCK 512
 #endif
 constexpr int BW_DCAP = SPX_BW_DCAP;  // distinct occupied bins per cluster (10 B of LDS each)
 constexpr int BW_PF = SPX_BW_PF;      // items in flight per lane
-constexpr int BW_CHUNK = 4 * (kWave - 1);  // positions per item (252)
-static_assert(BW_DCAP % BM_BLOCK == 0 && BW_DCAP / BM_BLOCK <= 32, "emit_striped keeps one bit per stripe");
+constexpr int BW_BLOCK = SPX_BW_BLOCK;  // threads per workgroup (8 waves: 2 workgroups per CU = 4 waves per SIMD)
+constexpr int BW_CHUNK = (BW_BLOCK / kWave) * (kWave - 1);  // positions per item (504)
+static_assert(BW_DCAP % BW_BLOCK == 0 && BW_DCAP / BW_BLOCK <= 32, "emit_striped keeps one bit per stripe");
+static_assert(BM_NMAX <= BW_BLOCK, "one thread per spectrum lays out the work items");
+
+#ifndef SPX_BW_IMAX
+#define SPX_BW_IMAX 1024
+#endif
+constexpr int BW_IMAX = SPX_BW_IMAX;  // work items per cluster (the table in LDS)
 
 struct BinWideSmem {
   unsigned long long bitmap[BM_WMAX];
   uint16_t wprefix[BM_WMAX];
-  float acc_i[BW_DCAP];
-  float acc_m[BW_DCAP];
+  float2 acc[BW_DCAP];    // (intensity, m/z) sums: one b64 read + one b64 write per contribution
   uint16_t cnt[BW_DCAP];  // <= BM_NMAX contributions per slot
+  // work item i: x = cluster-relative index of its first position, y = positions
+  // left in its spectrum from there, bit 31 of y: the item starts a spectrum;
+  // entries past the last item are null ({0, 0}: nothing active)
+  int2 item[BW_IMAX + BW_PF];
   double prec[BM_NMAX];
   int32_t soff[BM_NMAX + 1];
-  int wcnt[(BW_DCAP / BM_BLOCK) * (BM_BLOCK / kWave)];
-  int votes[2 * (BM_BLOCK / kWave)];
-  int tmp[BM_BLOCK / kWave + 1];
+  int wcnt[(BW_DCAP / BW_BLOCK) * (BW_BLOCK / kWave)];
+  int votes[2 * (BW_BLOCK / kWave)];
+  int tmp[BW_BLOCK / kWave + 1];
 };
-
-// Uniform cursor over a cluster's work items: spectrum j, chunk start c0.
-// Empty spectra have no item.  Past the last item j == n.
-struct ItemCursor {
-  int j, c0;
-};
-
-__device__ __forceinline__ int bw_len(const BinWideSmem& L, int j) { return L.soff[j + 1] - L.soff[j]; }
-
-__device__ __forceinline__ void bw_skip_empty(const BinWideSmem& L, int n, ItemCursor& q) {
-  while (q.j < n && bw_len(L, q.j) == 0) ++q.j;
-}
-
-// the next item; past the last one the cursor stays at j == n (null items)
-__device__ __forceinline__ void bw_next(const BinWideSmem& L, int n, ItemCursor& q) {
-  if (q.j >= n) return;
-  q.c0 += BW_CHUNK;
-  if (q.c0 >= bw_len(L, q.j)) {
-    ++q.j;
-    q.c0 = 0;
-    bw_skip_empty(L, n, q);
-  }
-}
 
 __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const BinMeanParams& P, BinWideSmem& L,
                                                       int64_t c, const PeaksOut& out, double* prec_out,
@@ -94,13 +84,13 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
   if (n64 > BM_NMAX || P.n_words > BM_WMAX || p1 - p0 >= (int64_t(1) << 28)) return kDeferred;
   const int n = (int)n64;
   const int np = (int)(p1 - p0);
-  for (int j = tid; j <= n; j += BM_BLOCK) L.soff[j] = (int32_t)(v.spec_off[s0 + j] - p0);
-  for (int j = tid; j < n; j += BM_BLOCK) L.prec[j] = v.prec_mz[s0 + j];
+  for (int j = tid; j <= n; j += BW_BLOCK) L.soff[j] = (int32_t)(v.spec_off[s0 + j] - p0);
+  for (int j = tid; j < n; j += BW_BLOCK) L.prec[j] = v.prec_mz[s0 + j];
   const int32_t z0 = v.charge[s0];
   int mixed = 0;
-  for (int j = 1 + tid; j < n; j += BM_BLOCK) mixed |= v.charge[s0 + j] != z0;
-  for (int w = tid; w < P.n_words; w += BM_BLOCK) L.bitmap[w] = 0ull;
-  if (block_any<BM_BLOCK, true>(mixed, L.votes, 0)) {  // binning.py:205-206: nothing emitted
+  for (int j = 1 + tid; j < n; j += BW_BLOCK) mixed |= v.charge[s0 + j] != z0;
+  for (int w = tid; w < P.n_words; w += BW_BLOCK) L.bitmap[w] = 0ull;
+  if (block_any<BW_BLOCK, true>(mixed, L.votes, 0)) {  // binning.py:205-206: nothing emitted
     if (tid == 0) { out.count[c] = 0; prec_out[c] = __longlong_as_double(0x7ff8000000000000ll); charge_out[c] = 0; }
     return kMixedCharge;
   }
@@ -108,16 +98,16 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
   // 1: occupancy from one flat pass (every in-range bin has a last peak)
   const char* __restrict__ mzb = reinterpret_cast<const char*>(v.mz + p0);
   constexpr int U1 = 16;
-  for (int r0 = tid; r0 < np; r0 += U1 * BM_BLOCK) {
+  for (int r0 = tid; r0 < np; r0 += U1 * BW_BLOCK) {
     double m[U1];
 #pragma unroll
     for (int u = 0; u < U1; ++u) {
-      const int r = r0 + u * BM_BLOCK;
+      const int r = r0 + u * BW_BLOCK;
       m[u] = *reinterpret_cast<const double*>(mzb + (uint32_t)(r < np ? r : 0) * 8u);
     }
 #pragma unroll
     for (int u = 0; u < U1; ++u) {
-      if (r0 + u * BM_BLOCK < np && in_range(m[u], P)) {
+      if (r0 + u * BW_BLOCK < np && in_range(m[u], P)) {
         const int32_t b = bin_small(m[u], P);
         atomicOr(&L.bitmap[b >> 6], 1ull << (b & 63));
       }
@@ -126,13 +116,26 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
   lds_barrier();
 
   // 2: slots in bin order
-  const int D = bitmap_prefix<BM_BLOCK, uint16_t, true>(L.bitmap, L.wprefix, P.n_words, L.tmp);
+  const int D = bitmap_prefix<BW_BLOCK, uint16_t, true>(L.bitmap, L.wprefix, P.n_words, L.tmp);
   if (D > BW_DCAP) return kDeferred;
-  for (int d = tid; d < D; d += BM_BLOCK) {
+  for (int d = tid; d < D; d += BW_BLOCK) {
     L.cnt[d] = 0;
-    L.acc_i[d] = 0.0f;
-    L.acc_m[d] = 0.0f;
+    L.acc[d] = make_float2(0.0f, 0.0f);
   }
+  // the work items: ceil(len / BW_CHUNK) per spectrum, in file order (thread j < n <= 128
+  // lays out spectrum j's; empty spectra have none)
+  int ni;
+  {
+    const int len = tid < n ? L.soff[tid + 1] - L.soff[tid] : 0;
+    const int mine = (len + BW_CHUNK - 1) / BW_CHUNK;
+    const int base = block_exclusive_scan<BW_BLOCK, int, true>(mine, L.tmp, ni);
+    if (ni <= BW_IMAX) {
+      for (int k = 0; k < mine; ++k)
+        L.item[base + k] = make_int2(L.soff[tid] + k * BW_CHUNK, (len - k * BW_CHUNK) | (k == 0 ? (int)0x80000000 : 0));
+      if (tid < BW_PF) L.item[ni + tid] = make_int2(0, 0);
+    }
+  }
+  if (ni > BW_IMAX) return kDeferred;
   lds_barrier();
 
   // 3: the ordered fold over the work items
@@ -142,42 +145,35 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
   const __amdgpu_buffer_rsrc_t rit = bf_rsrc(v.inten + p0, np);
   struct Pk {
     double m, it;
+    int rem;  // positions left in the spectrum (bit 31: a new spectrum)
   };
-  // item (j, c0) -> this lane's peak; j == n (past the end) reads out of range: 0
-  auto fetch = [&](const ItemCursor& q) __attribute__((always_inline)) {
-    const int jj = q.j < n ? q.j : n - 1;
-    const int a = L.soff[jj], e = L.soff[jj + 1];
-    const int k = a + q.c0 + fpos;
-    const int bo = (q.j < n && k < e) ? k * 8 : np * 8;
-    return Pk{bf_load(rmz, bo, 0), bf_load(rit, bo, 0)};
+  // item i -> this lane's peak (past the spectrum or a null item: out of the
+  // descriptor's range, the load returns 0)
+  auto fetch = [&](int i) __attribute__((always_inline)) {
+    const int2 d = L.item[i];
+    const int rem = d.y & 0x7fffffff;
+    const int bo = fpos < rem ? (d.x + fpos) * 8 : np * 8;
+    return Pk{bf_load(rmz, bo, 0), bf_load(rit, bo, 0), d.y};
   };
-  ItemCursor fq{0, 0}, cq{0, 0};  // fetch and consume cursors (uniform)
-  bw_skip_empty(L, n, fq);
-  bw_skip_empty(L, n, cq);
   Pk ring[BW_PF];
 #pragma unroll
-  for (int q = 0; q < BW_PF; ++q) {
-    ring[q] = fetch(fq);
-    bw_next(L, n, fq);
-  }
-  int bad = 0, pslot = -1, pj = -1;
+  for (int q = 0; q < BW_PF; ++q) ring[q] = fetch(q);
+  int bad = 0, pslot = -1;
   double pm = 0.0, pit = 0.0;
-  // whole groups of BW_PF steps: past the last item the steps are null items
-  // (nothing active, one extra barrier), so no step is guarded and no ring
-  // register is ever a merge of a fresh load and an old value
-  while (cq.j < n) {  // uniform
+  // whole groups of BW_PF steps (the table's null tail): no step is guarded, so
+  // no ring register is ever a merge of a fresh load and an old value
+  for (int i0 = 0; i0 < ni; i0 += BW_PF) {  // uniform
 #pragma unroll
     for (int q = 0; q < BW_PF; ++q) {
       // item i-1's accumulator reads first (every lane; non-owners read slot 0)
       const int ps = pslot >= 0 ? pslot : 0;
-      const float e_ai = L.acc_i[ps], e_am = L.acc_m[ps];
+      const float2 e_a = L.acc[ps];
       const uint16_t e_cn = L.cnt[ps];
       const Pk pk = ring[q];
-      ring[q] = fetch(fq);
-      bw_next(L, n, fq);
-      const int len = cq.j < n ? bw_len(L, cq.j) : 0;
-      const int pos = cq.c0 + fpos;
-      const bool act = pos < len;
+      const int inext = i0 + q + BW_PF;
+      ring[q] = fetch(inext < ni ? inext : ni);  // past the end: the null entry
+      const int rem = __builtin_amdgcn_readfirstlane(pk.rem);
+      const bool act = fpos < (rem & 0x7fffffff);
       const bool inr = act && in_range(pk.m, P);
       int32_t key = (act && pk.m < P.minimum) ? -1 : 0x7fffffff;
       int slot = -1;
@@ -190,28 +186,25 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
       const bool last = kn != key;
       if (pslot >= 0) {  // finish item i-1
         L.cnt[pslot] = (uint16_t)(e_cn + 1u);
-        L.acc_i[pslot] = (float)((double)e_ai + pit);
-        L.acc_m[pslot] = (float)((double)e_am + pm);
+        L.acc[pslot] = make_float2((float)((double)e_a.x + pit), (float)((double)e_a.y + pm));
       }
       // a new spectrum may touch item i-1's slots: its writes land first
-      if (cq.j != pj) lds_barrier();
-      pj = cq.j;
+      if (rem < 0) lds_barrier();
       pslot = (owner && inr && last) ? slot : -1;
       pm = pk.m;
       pit = pk.it;
-      bw_next(L, n, cq);
     }
   }
   if (pslot >= 0) {
     L.cnt[pslot] = (uint16_t)(L.cnt[pslot] + 1u);
-    L.acc_i[pslot] = (float)((double)L.acc_i[pslot] + pit);
-    L.acc_m[pslot] = (float)((double)L.acc_m[pslot] + pm);
+    const float2 a = L.acc[pslot];
+    L.acc[pslot] = make_float2((float)((double)a.x + pit), (float)((double)a.y + pm));
   }
-  if (block_any<BM_BLOCK, true>(bad, L.votes, 1)) return kDeferred;  // unsorted / NaN: the general paths
+  if (block_any<BW_BLOCK, true>(bad, L.votes, 1)) return kDeferred;  // unsorted / NaN: the general paths
 
   // 4: quorum filter and ordered output (binning.py:181-183, 209-222)
   const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
-  const int total = emit_striped(L.cnt, [&](int d) { return L.acc_i[d]; }, [&](int d) { return L.acc_m[d]; },
+  const int total = emit_striped<BW_BLOCK>(L.cnt, [&](int d) { return L.acc[d].x; }, [&](int d) { return L.acc[d].y; },
                                  L.wcnt, D, quorum, out.mz + p0, out.inten + p0);
   if (tid == 0) {
     out.count[c] = total;
@@ -222,7 +215,7 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
 }
 
 // The register kernel's leftovers, grid-stride over the list.
-__global__ __launch_bounds__(BM_BLOCK, SPX_BW_MINW) void bin_mean_wide_kernel(CsrView v, BinMeanParams P,
+__global__ __launch_bounds__(BW_BLOCK, SPX_BW_MINW) void bin_mean_wide_kernel(CsrView v, BinMeanParams P,
                                                                               PeaksOut out, double* prec_out,
                                                                               int32_t* charge_out, int32_t* status,
                                                                               const int32_t* list,

@@ -195,7 +195,7 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
 #if SPX_BM_WIDE
   hipLaunchKernelGGL(spx::bin_mean_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),
-                     dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
+                     dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
   if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
 #else
   hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),

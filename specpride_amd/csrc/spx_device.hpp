@@ -69,10 +69,6 @@ enum : int32_t { kOk = 0, kMixedCharge = 1, kNoGap = 2, kEmpty = 3, kNonFinite =
 __device__ __forceinline__ double bf_load(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
-// the same with the nt (non-temporal: last use, streamed past the caches) policy
-__device__ __forceinline__ double bf_load_nt(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 2));
-}
 
 // buffer descriptor over n doubles at p, built from readfirstlane'd halves so
 // the compiler sees it wave-uniform (readfirstlane returns int: zero-extend the
