@@ -1,0 +1,464 @@
+// Bin-mean for the clusters past the wide kernel -- more than 128 spectra (the
+// configs[3] long tail, up to 5,000 spectra and ~1M peaks) or more than BW_DCAP
+// distinct bins -- as a grid-parallel SEGMENTED FOLD (reference:
+// src/binning.py:170-231).
+//
+// The reference's per-bin accumulation f32(f64(acc) + v) runs in spectrum order
+// and does not reassociate, so each bin's contributions must meet in that order.
+// Instead of walking the cluster's spectra one after another (a serial chain as
+// long as the cluster), the contributions are sorted by (bin, spectrum) with a
+// stable counting sort and every bin is then folded by one thread over its own
+// contiguous segment:
+//
+//   setup    (WG per cluster)   mixed-charge check; bitmap from the arena;
+//                               work items = blocks of SG_SB = 64 spectra
+//   occupy   (grid, per block)  occupied bins (LDS bitmap per block, ORed into
+//                               the cluster's) and the sortedness / NaN check
+//   prefix   (WG per cluster)   bin -> slot (popcount prefix); the D-sized tables
+//   mask     (grid, per block)  mask[b][slot] bit s: the block's spectrum s holds
+//                               the last peak of that bin (numpy fancy-index +=
+//                               keeps the last, binning.py:197-199)
+//   count    (grid, per slot)   boff[b][slot] = contributions of earlier blocks;
+//                               tot[slot]
+//   scan     (WG per cluster)   seg[slot] = contributions of earlier slots
+//   place    (grid, per block)  value of (s, slot) -> seg[slot] + boff[b][slot] +
+//                               popcount(mask[b][slot] below s): spectrum order
+//   fold     (grid, per slot)   one thread per bin over its segment, in order
+//   emit     (WG per cluster)   quorum, ordered output, count, charge, np.mean
+//
+// Every table lives in a bump-allocated arena of the workspace; a cluster that
+// does not fit goes on to the bin-range split path, an unsorted or NaN one to
+// the global kernel.  HBM traffic per peak: m/z three times, the intensity once,
+// 16 B of contribution written and read back, plus the (block x slot) tables.
+#pragma once
+#include "bin_mean.hip"
+
+namespace spx {
+
+constexpr int SG_SB = 64;      // spectra per block (one bit each in a u64 mask)
+constexpr int SG_BLOCK = 256;  // threads per workgroup
+constexpr int SG_TILE = 256;   // slots per fold / count workgroup
+enum : int32_t { kSegOk = 0, kSegBad = 1, kSegNoRoom = 2, kSegDone = 3 };
+
+struct SegMeta {
+  int64_t c, p0;
+  int32_t n, nb;       // spectra, blocks
+  int32_t D, state;    // occupied bins; kSeg*
+  int32_t task0, tile0;  // first block task, first slot tile
+  int64_t bm, pre;       // arena offsets: bitmap (n_words u64), prefix (n_words u32)
+  int64_t mask, boff;    // mask[b * D + slot] u64, boff[b * D + slot] u16
+  int64_t seg, vals;     // seg[slot] u32 (D + 1), contributions (m/z, intensity) f64 x 2
+  int64_t res, keep;     // res[slot] (m/z mean, intensity mean) f64 x 2, keep[slot] u32 (D + 1)
+};
+
+__device__ __forceinline__ int64_t seg_align(int64_t b) { return (b + 255) & ~int64_t(255); }
+
+// bump allocation from the arena; -1 when it is exhausted
+__device__ __forceinline__ int64_t seg_alloc(unsigned long long* bump, int64_t bytes, int64_t cap) {
+  const unsigned long long o = atomicAdd(bump, (unsigned long long)seg_align(bytes));
+  return (int64_t)o + seg_align(bytes) <= cap ? (int64_t)o : -1;
+}
+
+// setup: one workgroup per deferred cluster (grid-stride over the list)
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_setup_kernel(
+    CsrView v, BinMeanParams P, PeaksOut out, double* prec_out, int32_t* charge_out, int32_t* status,
+    const int32_t* list, const int32_t* n_list, SegMeta* meta, char* arena, unsigned long long* bump, int64_t cap,
+    int32_t* task_cl, int32_t* n_tasks) {
+  __shared__ int votes[2 * (SG_BLOCK / kWave)];
+  __shared__ int64_t s_bm;
+  __shared__ int32_t s_task0;
+  const int tid = threadIdx.x;
+  const int32_t nl = *n_list;
+  for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    const int64_t c = list[i];
+    const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+    const int n = (int)(s1 - s0);
+    const int32_t z0 = v.charge[s0];
+    int mixed = 0;
+    for (int64_t s = s0 + 1 + tid; s < s1; s += SG_BLOCK) mixed |= v.charge[s] != z0;
+    const bool mix = block_any<SG_BLOCK, false>(mixed, votes, 0);
+    SegMeta M = {};
+    M.c = c;
+    M.p0 = v.spec_off[s0];
+    M.n = n;
+    M.nb = (n + SG_SB - 1) / SG_SB;
+    if (mix) {  // binning.py:205-206: nothing emitted
+      if (tid == 0) {
+        out.count[c] = 0;
+        prec_out[c] = __longlong_as_double(0x7ff8000000000000ll);
+        charge_out[c] = 0;
+        status[c] = kMixedCharge;
+        M.state = kSegDone;
+        M.task0 = 0;
+        M.nb = 0;
+        meta[i] = M;
+      }
+      __syncthreads();
+      continue;
+    }
+    const int64_t P_c = v.spec_off[s1] - M.p0;
+    // the tables' limits: the LDS bitmap of a block, u16 block offsets, u32 segments
+    const bool fits = P.n_words <= BM_WMAX && n <= 65535 && P_c < (int64_t(1) << 31);
+    if (tid == 0) {
+      s_bm = fits ? seg_alloc(bump, (int64_t)P.n_words * 12, cap) : -1;
+      s_task0 = s_bm >= 0 ? atomicAdd(n_tasks, M.nb) : 0;
+    }
+    __syncthreads();
+    const int64_t bm = s_bm;
+    M.bm = bm;
+    M.pre = bm + (int64_t)P.n_words * 8;
+    M.task0 = s_task0;
+    if (bm < 0) {
+      M.state = kSegNoRoom;
+      M.nb = 0;
+    } else {
+      unsigned long long* B = reinterpret_cast<unsigned long long*>(arena + bm);
+      for (int w = tid; w < P.n_words; w += SG_BLOCK) B[w] = 0ull;
+      for (int k = tid; k < M.nb; k += SG_BLOCK) task_cl[M.task0 + k] = i;
+    }
+    if (tid == 0) meta[i] = M;
+    __syncthreads();
+  }
+}
+
+// The block's spectra, one wave per spectrum at a time, in GROUPS of 4 x 63
+// peaks (lane j of chunk q owns peak g0 + 63q + j, j < 63; lane 63 reads the next
+// peak only to hand lane 62 its key): bin, last-in-bin by the DPP neighbour key
+// (numpy fancy-index += keeps the last, binning.py:197-199), the sortedness / NaN
+// check.  The next group's loads are issued before the current one is processed.
+// f(k, key, last, spectrum-in-block) for every in-range peak.  Returns "bad".
+constexpr int SG_GQ = 4;                       // chunks per group
+constexpr int SG_GROUP = SG_GQ * (kWave - 1);  // peaks per group (252)
+
+template <class F>
+__device__ __forceinline__ int seg_walk_block(const CsrView& v, const BinMeanParams& P, const SegMeta& M, int b,
+                                              const int32_t* soff, F&& f) {
+  constexpr int NW = SG_BLOCK / kWave;
+  const int lane = lane_id(), wid = wave_id();
+  const int nsb = min(M.n - b * SG_SB, SG_SB);  // spectra in this block
+  const double* __restrict__ mz = v.mz + M.p0;
+  const bool owner = lane < kWave - 1;
+  // uniform cursor: spectrum sl (this wave's: wid, wid + NW, ...), group start g0
+  int sl = wid, g0 = 0;
+  auto skip = [&](int& s) { while (s < nsb && soff[s + 1] == soff[s]) s += NW; };
+  auto load = [&](int s, int g, double* m) __attribute__((always_inline)) {
+    const int a = s < nsb ? soff[s] : 0, e = s < nsb ? soff[s + 1] : 0;
+#pragma unroll
+    for (int q = 0; q < SG_GQ; ++q) {
+      const int k = a + g + q * (kWave - 1) + lane;
+      m[q] = k < e ? mz[k] : 0.0;
+    }
+  };
+  skip(sl);
+  double cur[SG_GQ], nxt[SG_GQ];
+  load(sl, g0, cur);
+  int bad = 0;
+  while (sl < nsb) {  // uniform
+    // the following group's cursor and loads first
+    int sn = sl, gn = g0 + SG_GROUP;
+    if (gn >= soff[sl + 1] - soff[sl]) {
+      sn = sl + NW;
+      gn = 0;
+      skip(sn);
+    }
+    load(sn, gn, nxt);
+    const int a = soff[sl], e = soff[sl + 1];
+#pragma unroll
+    for (int q = 0; q < SG_GQ; ++q) {
+      const int k = a + g0 + q * (kWave - 1) + lane;
+      const bool act = k < e;
+      const double m = cur[q];
+      const bool inr = act && in_range(m, P);
+      const int32_t key = inr ? bin_small(m, P) : ((act && m < P.minimum) ? -1 : 0x7fffffff);
+      const int32_t kn = wave_next(key, 0x7fffffff);
+      bad |= (int)(owner && act && ((m != m) || key > kn));
+      if (owner && inr) f(M.p0 + k, key, kn != key, sl);
+    }
+#pragma unroll
+    for (int q = 0; q < SG_GQ; ++q) cur[q] = nxt[q];
+    sl = sn;
+    g0 = gn;
+  }
+  return bad;
+}
+
+// the block's spectrum offsets (relative to the cluster's first peak) into LDS
+__device__ __forceinline__ void seg_block_offsets(const CsrView& v, const SegMeta& M, int b, int32_t* soff) {
+  const int64_t s0 = v.cluster_off[M.c] + (int64_t)b * SG_SB;
+  const int nsb = min(M.n - b * SG_SB, SG_SB);
+  for (int j = threadIdx.x; j <= nsb; j += SG_BLOCK) soff[j] = (int32_t)(v.spec_off[s0 + j] - M.p0);
+}
+
+// occupancy: one workgroup per (cluster, block) task
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_occupy_kernel(CsrView v, BinMeanParams P, SegMeta* meta,
+                                                                       char* arena, const int32_t* task_cl,
+                                                                       const int32_t* n_tasks) {
+  __shared__ unsigned long long bits[BM_WMAX];
+  __shared__ int32_t soff[SG_SB + 1];
+  __shared__ int votes[2 * (SG_BLOCK / kWave)];
+  const int tid = threadIdx.x;
+  const int32_t nt = *n_tasks;
+  for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int i = task_cl[t];
+    const SegMeta M = meta[i];
+    for (int w = tid; w < P.n_words; w += SG_BLOCK) bits[w] = 0ull;
+    seg_block_offsets(v, M, t - M.task0, soff);
+    lds_barrier();
+    const int bad = seg_walk_block(v, P, M, t - M.task0, soff, [&](int64_t, int32_t key, bool, int) {
+      atomicOr(&bits[key >> 6], 1ull << (key & 63));
+    });
+    if (block_any<SG_BLOCK, true>(bad, votes, 0) && tid == 0) atomicOr(&meta[i].state, kSegBad);
+    unsigned long long* B = reinterpret_cast<unsigned long long*>(arena + M.bm);
+    for (int w = tid; w < P.n_words; w += SG_BLOCK)
+      if (bits[w]) atomicOr(&B[w], bits[w]);
+    lds_barrier();
+  }
+}
+
+// prefix: one workgroup per cluster -- slots, then the D-sized tables
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_prefix_kernel(
+    CsrView v, BinMeanParams P, PeaksOut out, double* prec_out, int32_t* charge_out, int32_t* status,
+    const int32_t* n_list, SegMeta* meta, char* arena, unsigned long long* bump, int64_t cap, int32_t* tile_cl,
+    int32_t* n_tiles) {
+  __shared__ int tmp[SG_BLOCK / kWave + 1];
+  __shared__ SegMeta sM;
+  const int tid = threadIdx.x;
+  const int32_t nl = *n_list;
+  for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    SegMeta M = meta[i];
+    if (M.state != kSegOk) {
+      __syncthreads();
+      continue;
+    }
+    const unsigned long long* B = reinterpret_cast<const unsigned long long*>(arena + M.bm);
+    uint32_t* pre = reinterpret_cast<uint32_t*>(arena + M.pre);
+    const int D = bitmap_prefix<SG_BLOCK, uint32_t>(B, pre, P.n_words, tmp);
+    if (tid == 0) {
+      M.D = D;
+      const int64_t nbD = (int64_t)M.nb * D;
+      const int64_t P_c = v.spec_off[v.cluster_off[M.c + 1]] - M.p0;  // contributions <= peaks
+      const int64_t bytes = seg_align(nbD * 8) + seg_align(nbD * 2) + seg_align((int64_t)(D + 1) * 4) +
+                            seg_align(P_c * 16) + seg_align((int64_t)D * 16) + seg_align((int64_t)(D + 1) * 4);
+      const int64_t base = D > 0 ? seg_alloc(bump, bytes, cap) : 0;
+      if (D == 0) {
+        // no in-range peak: an empty consensus (count 0), charge and np.mean as usual
+        const int64_t s0 = v.cluster_off[M.c];
+        out.count[M.c] = 0;
+        charge_out[M.c] = v.charge[s0];
+        prec_out[M.c] = pw_sum([&](int64_t j) { return v.prec_mz[s0 + j]; }, M.n) / (double)M.n;
+        status[M.c] = kOk;
+        M.state = kSegDone;
+      } else if (base < 0) {
+        M.state = kSegNoRoom;
+      } else {
+        M.mask = base;
+        M.boff = M.mask + seg_align(nbD * 8);
+        M.seg = M.boff + seg_align(nbD * 2);
+        M.vals = M.seg + seg_align((int64_t)(D + 1) * 4);
+        M.res = M.vals + seg_align(P_c * 16);
+        M.keep = M.res + seg_align((int64_t)D * 16);
+        const int nt = (D + SG_TILE - 1) / SG_TILE;
+        M.tile0 = atomicAdd(n_tiles, nt);
+      }
+      sM = M;
+    }
+    __syncthreads();
+    M = sM;
+    if (M.state == kSegOk) {
+      const int nt = (M.D + SG_TILE - 1) / SG_TILE;
+      for (int k = tid; k < nt; k += SG_BLOCK) tile_cl[M.tile0 + k] = i;
+    }
+    if (tid == 0) meta[i] = M;
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ int seg_slot(const SegMeta& M, const char* arena, int32_t key) {
+  const unsigned long long* B = reinterpret_cast<const unsigned long long*>(arena + M.bm);
+  const uint32_t* pre = reinterpret_cast<const uint32_t*>(arena + M.pre);
+  return bitmap_rank(B, pre, (int64_t)key);
+}
+
+// mask: one workgroup per (cluster, block) task -- bit s of mask[b][slot] for
+// every contribution (spectrum s of block b is the last peak of that bin)
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_mask_kernel(CsrView v, BinMeanParams P,
+                                                                     const SegMeta* meta, char* arena,
+                                                                     const int32_t* task_cl,
+                                                                     const int32_t* n_tasks) {
+  __shared__ int32_t soff[SG_SB + 1];
+  const int tid = threadIdx.x;
+  const int32_t nt = *n_tasks;
+  for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int i = task_cl[t];
+    const SegMeta M = meta[i];
+    if (M.state != kSegOk) continue;  // uniform
+    const int b = t - M.task0;
+    unsigned long long* mask = reinterpret_cast<unsigned long long*>(arena + M.mask) + (int64_t)b * M.D;
+    for (int d = tid; d < M.D; d += SG_BLOCK) mask[d] = 0ull;
+    seg_block_offsets(v, M, b, soff);
+    __syncthreads();  // the row is zero before any bit is set (global memory)
+    seg_walk_block(v, P, M, b, soff, [&](int64_t, int32_t key, bool last, int s) {
+      if (last) atomicOr(&mask[seg_slot(M, arena, key)], 1ull << s);
+    });
+    __syncthreads();  // soff is reused by the next task
+  }
+}
+
+// count: one thread per slot -- contributions of earlier blocks and the total
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_count_kernel(const SegMeta* meta, char* arena,
+                                                                      const int32_t* tile_cl,
+                                                                      const int32_t* n_tiles) {
+  const int32_t nt = *n_tiles;
+  for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int i = tile_cl[t];
+    const SegMeta M = meta[i];
+    if (M.state != kSegOk) continue;
+    const int d = (t - M.tile0) * SG_TILE + threadIdx.x;
+    if (d >= M.D) continue;
+    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(arena + M.mask);
+    uint16_t* boff = reinterpret_cast<uint16_t*>(arena + M.boff);
+    uint32_t run = 0;
+    for (int b = 0; b < M.nb; ++b) {
+      boff[(int64_t)b * M.D + d] = (uint16_t)run;
+      run += (uint32_t)__popcll(mask[(int64_t)b * M.D + d]);
+    }
+    reinterpret_cast<uint32_t*>(arena + M.seg)[d] = run;
+  }
+}
+
+// scan: one workgroup per cluster -- seg[slot] = contributions of earlier slots
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_scan_kernel(const int32_t* n_list, const SegMeta* meta,
+                                                                     char* arena) {
+  __shared__ uint32_t tmp[SG_BLOCK / kWave + 1];
+  const int tid = threadIdx.x;
+  const int32_t nl = *n_list;
+  for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    const SegMeta M = meta[i];
+    if (M.state != kSegOk) continue;  // uniform
+    uint32_t* seg = reinterpret_cast<uint32_t*>(arena + M.seg);
+    const int per = (M.D + SG_BLOCK - 1) / SG_BLOCK, d0 = tid * per;
+    uint32_t local = 0;
+    for (int k = 0; k < per; ++k)
+      if (d0 + k < M.D) local += seg[d0 + k];
+    uint32_t total;
+    uint32_t base = block_exclusive_scan<SG_BLOCK, uint32_t>(local, tmp, total);
+    for (int k = 0; k < per; ++k) {
+      if (d0 + k < M.D) {
+        const uint32_t x = seg[d0 + k];
+        seg[d0 + k] = base;
+        base += x;
+      }
+    }
+    if (tid == 0) seg[M.D] = total;
+    __syncthreads();
+  }
+}
+
+// place: one workgroup per (cluster, block) task -- each contribution into its
+// bin's segment, in spectrum order
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_place_kernel(CsrView v, BinMeanParams P,
+                                                                      const SegMeta* meta, char* arena,
+                                                                      const int32_t* task_cl,
+                                                                      const int32_t* n_tasks) {
+  __shared__ int32_t soff[SG_SB + 1];
+  const int32_t nt = *n_tasks;
+  for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int i = task_cl[t];
+    const SegMeta M = meta[i];
+    if (M.state != kSegOk) continue;  // uniform
+    const int b = t - M.task0;
+    seg_block_offsets(v, M, b, soff);
+    __syncthreads();
+    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(arena + M.mask) + (int64_t)b * M.D;
+    const uint16_t* boff = reinterpret_cast<const uint16_t*>(arena + M.boff) + (int64_t)b * M.D;
+    const uint32_t* seg = reinterpret_cast<const uint32_t*>(arena + M.seg);
+    double2* vals = reinterpret_cast<double2*>(arena + M.vals);
+    seg_walk_block(v, P, M, b, soff, [&](int64_t k, int32_t key, bool last, int s) {
+      if (!last) return;
+      const int d = seg_slot(M, arena, key);
+      const uint32_t pos = seg[d] + boff[d] + (uint32_t)__popcll(mask[d] & ((1ull << s) - 1ull));
+      vals[pos] = make_double2(v.mz[k], v.inten[k]);
+    });
+    __syncthreads();  // soff is reused by the next task
+  }
+}
+
+// fold: one thread per slot over its segment, in spectrum order (binning.py:198-199),
+// then the quorum (:181-183) and the means (:209-222)
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_fold_kernel(BinMeanParams P, const SegMeta* meta,
+                                                                     char* arena, const int32_t* tile_cl,
+                                                                     const int32_t* n_tiles) {
+  const int32_t nt = *n_tiles;
+  for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int i = tile_cl[t];
+    const SegMeta M = meta[i];
+    if (M.state != kSegOk) continue;
+    const int d = (t - M.tile0) * SG_TILE + threadIdx.x;
+    if (d >= M.D) continue;
+    const uint32_t* seg = reinterpret_cast<const uint32_t*>(arena + M.seg);
+    const double2* vals = reinterpret_cast<const double2*>(arena + M.vals);
+    const uint32_t a = seg[d], e = seg[d + 1];
+    float si = 0.0f, sm = 0.0f;
+    for (uint32_t k = a; k < e; ++k) {
+      const double2 x = vals[k];
+      si = (float)((double)si + x.y);
+      sm = (float)((double)sm + x.x);
+    }
+    const uint32_t cnt = e - a;
+    const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)M.n * 0.25) + 1u : 1u;
+    const bool keep = cnt >= quorum && !isnan(si);  // cnt >= 1: mean NaN iff sum NaN
+    reinterpret_cast<uint32_t*>(arena + M.keep)[d] = keep ? 1u : 0u;
+    const double cn = (double)cnt;
+    reinterpret_cast<double2*>(arena + M.res)[d] =
+        make_double2(sm == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)sm / cn, (double)si / cn);
+  }
+}
+
+// emit: one workgroup per cluster -- kept slots in bin order, count, charge, np.mean
+__global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_emit_kernel(CsrView v, PeaksOut out, double* prec_out,
+                                                                     int32_t* charge_out, int32_t* status,
+                                                                     const int32_t* n_list, const SegMeta* meta,
+                                                                     char* arena, int32_t* split_list,
+                                                                     int32_t* n_split, int32_t* glist,
+                                                                     int32_t* n_glist) {
+  __shared__ uint32_t tmp[SG_BLOCK / kWave + 1];
+  const int tid = threadIdx.x;
+  const int32_t nl = *n_list;
+  for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    const SegMeta M = meta[i];
+    if (M.state != kSegOk) {  // uniform
+      if (tid == 0) {
+        if (M.state == kSegBad) glist[atomicAdd(n_glist, 1)] = (int32_t)M.c;  // unsorted / NaN
+        if (M.state == kSegNoRoom) split_list[atomicAdd(n_split, 1)] = (int32_t)M.c;  // arena full
+      }
+      continue;
+    }
+    const uint32_t* keep = reinterpret_cast<const uint32_t*>(arena + M.keep);
+    const double2* res = reinterpret_cast<const double2*>(arena + M.res);
+    const int per = (M.D + SG_BLOCK - 1) / SG_BLOCK, d0 = tid * per;
+    uint32_t local = 0;
+    for (int k = 0; k < per; ++k)
+      if (d0 + k < M.D) local += keep[d0 + k];
+    uint32_t total;
+    uint32_t o = block_exclusive_scan<SG_BLOCK, uint32_t>(local, tmp, total);
+    for (int k = 0; k < per; ++k) {
+      const int d = d0 + k;
+      if (d < M.D && keep[d]) {
+        const double2 r = res[d];
+        out.mz[M.p0 + o] = r.x;
+        out.inten[M.p0 + o] = r.y;
+        ++o;
+      }
+    }
+    if (tid == 0) {
+      const int64_t s0 = v.cluster_off[M.c];
+      out.count[M.c] = total;
+      charge_out[M.c] = v.charge[s0];
+      prec_out[M.c] = pw_sum([&](int64_t j) { return v.prec_mz[s0 + j]; }, M.n) / (double)M.n;  // np.mean (binning.py:224)
+      status[M.c] = kOk;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace spx

@@ -24,8 +24,9 @@
 //
 // HBM traffic: the m/z twice (phase 3 re-reads what phase 1 pulled toward the
 // caches), the intensities once.  A key inversion or NaN inside a spectrum
-// (unsorted input) sends the cluster on to the split path / global kernel, as
-// does a cluster with more than BW_DCAP distinct bins or BM_NMAX spectra.
+// (unsorted input) sends the cluster to the global kernel; one with more than
+// BW_DCAP distinct bins, BM_NMAX spectra or BW_IMAX work items to the segmented
+// fold (bin_mean_seg.hip).
 #pragma once
 #include "bin_mean.hip"
 
@@ -43,6 +44,7 @@ namespace spx {
 #ifndef SPX_BW_BLOCK
 #define SPX_BW_BLOCK 512
 #endif
+constexpr int32_t kUnsortedW = -2;  // (internal) a key inversion or NaN: straight to the global kernel
 constexpr int BW_DCAP = SPX_BW_DCAP;  // distinct occupied bins per cluster (10 B of LDS each)
 constexpr int BW_PF = SPX_BW_PF;      // items in flight per lane
 constexpr int BW_BLOCK = SPX_BW_BLOCK;  // threads per workgroup (8 waves: 2 workgroups per CU = 4 waves per SIMD)
@@ -200,7 +202,7 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
     const float2 a = L.acc[pslot];
     L.acc[pslot] = make_float2((float)((double)a.x + pit), (float)((double)a.y + pm));
   }
-  if (block_any<BW_BLOCK, true>(bad, L.votes, 1)) return kDeferred;  // unsorted / NaN: the general paths
+  if (block_any<BW_BLOCK, true>(bad, L.votes, 1)) return kUnsortedW;  // unsorted / NaN: the global kernel
 
   // 4: quorum filter and ordered output (binning.py:181-183, 209-222)
   const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
@@ -221,15 +223,21 @@ __global__ __launch_bounds__(BW_BLOCK, SPX_BW_MINW) void bin_mean_wide_kernel(Cs
                                                                               const int32_t* list,
                                                                               const int32_t* n_list,
                                                                               int32_t* deferred,
-                                                                              int32_t* n_deferred) {
+                                                                              int32_t* n_deferred, int32_t* glist,
+                                                                              int32_t* n_glist) {
   __shared__ BinWideSmem L;
   const int32_t nl = *n_list;
   for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
     const int64_t c = list[i];
     const int32_t st = bin_mean_wide_body(v, P, L, c, out, prec_out, charge_out);
     if (threadIdx.x == 0) {
-      status[c] = st;
-      if (st == kDeferred) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+      if (st == kUnsortedW) {
+        status[c] = kDeferred;
+        glist[atomicAdd(n_glist, 1)] = (int32_t)c;
+      } else {
+        status[c] = st;
+        if (st == kDeferred) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+      }
     }
     lds_barrier();  // the LDS is reused by the next cluster
   }

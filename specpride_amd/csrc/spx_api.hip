@@ -16,16 +16,13 @@
 #include "../../include/specpride.h"
 #include "best_score.hip"
 #include "bin_mean.hip"
+#include "bin_mean_seg.hip"
 #include "bin_mean_split.hip"
 #include "bin_mean_wide.hip"
 #include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
 #include "transfer.hip"
-
-#ifndef SPX_BM_WIDE
-#define SPX_BM_WIDE 1  // the register kernel's leftovers: bin_mean_wide_kernel (0: the older bin_mean_lds_kernel)
-#endif
 
 namespace {
 
@@ -138,14 +135,71 @@ int32_t split_range_cap(const spx_csr* csr) {
   return (int32_t)std::max<int64_t>(1, std::min<int64_t>(r, int64_t(1) << 20));
 }
 
+}  // extern "C"
+
+namespace {
+// Arena of the segmented fold (bin_mean_seg.hip): a cluster needs its bitmap and
+// prefix (12 B per bin word), (blocks x slots) tables and 16 B per contribution;
+// clusters that do not fit take the bin-range split path.  Bounded by the batch
+// (64 B per peak) and by a fixed cap.
+// SPX_SEG_ARENA (environment, tests only) caps it, so clusters overflow to the
+// split path on small batches.
+int64_t seg_arena_bytes(const spx_csr* csr, const spx_bin_params* params) {
+  constexpr int64_t kCap = int64_t(2) << 30;
+  const int64_t per_cluster = align256((size_t)bin_words(params) * 12) + 4096;
+  int64_t b = 64 * csr->n_peaks + per_cluster * std::min<int64_t>(csr->n_clusters, 4096) + (int64_t(1) << 20);
+  if (const char* e = std::getenv("SPX_SEG_ARENA")) {
+    const long long v = std::strtoll(e, nullptr, 10);
+    if (v >= 0) b = std::min<int64_t>(b, v);
+  }
+  return std::min(b, kCap);
+}
+
+struct BinMeanWs {
+  int32_t *counters, *def, *rest, *glist, *split_list, *task_cl, *tile_cl;
+  unsigned long long* bump;
+  spx::SplitCluster* scl;
+  spx::SplitRange* ranges;
+  spx::SegMeta* meta;
+  char *arena, *scratch;
+  int64_t arena_bytes, n_task_cap, n_tile_cap;
+  int32_t range_cap;
+};
+
+// The workspace layout (the size query and the launch use the same carving).
+BinMeanWs carve_bin_mean(Carver& w, const spx_csr* csr, const spx_bin_params* params) {
+  const size_t C = (size_t)std::max<int64_t>(csr->n_clusters, 1);
+  BinMeanWs W;
+  W.counters = w.take<int32_t>(8);
+  W.bump = w.take<unsigned long long>(1);
+  W.def = w.take<int32_t>(C);
+  W.rest = w.take<int32_t>(C);
+  W.glist = w.take<int32_t>(C);
+  W.split_list = w.take<int32_t>(C);
+  W.scl = w.take<spx::SplitCluster>(C);
+  W.range_cap = split_range_cap(csr);
+  W.ranges = w.take<spx::SplitRange>((size_t)W.range_cap);
+  W.meta = w.take<spx::SegMeta>(C);
+  W.n_task_cap = csr->n_spectra / spx::SG_SB + csr->n_clusters + 1;
+  W.task_cl = w.take<int32_t>((size_t)W.n_task_cap);
+  W.n_tile_cap = csr->n_peaks / spx::SG_TILE + csr->n_clusters + 1;
+  W.tile_cl = w.take<int32_t>((size_t)W.n_tile_cap);
+  W.arena_bytes = seg_arena_bytes(csr, params);
+  W.arena = w.take<char>((size_t)W.arena_bytes);
+  W.scratch = w.base + w.used;
+  return W;
+}
+}  // namespace
+
+extern "C" {
+
 size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info) {
   if (!csr || !params || !info) return 0;
   const int64_t C = csr->n_clusters;
-  const size_t Cm = (size_t)std::max<int64_t>(C, 1);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
-  return align256(sizeof(int32_t) * 5) + 3 * align256(sizeof(int32_t) * Cm) +
-         align256(sizeof(spx::SplitCluster) * Cm) + align256(sizeof(spx::SplitRange) * (size_t)split_range_cap(csr)) +
-         (size_t)bin_mean_fallback_grid(C, params, dcap) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
+  Carver w{nullptr, 0, 0};
+  carve_bin_mean(w, csr, params);
+  return w.used + (size_t)bin_mean_fallback_grid(C, params, dcap) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
 int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info, spx_peaks_out* out,
@@ -162,21 +216,19 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   if (C == 0) return SPX_SUCCESS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
-  // [0] deferred past the LDS kernel, [1] left to the LDS kernel, [2] planned split
-  // clusters, [3] split ranges, [4] the global kernel's list
-  int32_t* counters = w.take<int32_t>(5);
-  int32_t* n_def = counters;
-  int32_t* n_rest = counters + 1;
-  int32_t* n_scl = counters + 2;
-  int32_t* n_ranges = counters + 3;
-  int32_t* n_glist = counters + 4;
-  int32_t* def = w.take<int32_t>((size_t)C);
-  int32_t* rest = w.take<int32_t>((size_t)C);
-  int32_t* glist = w.take<int32_t>((size_t)C);
-  spx::SplitCluster* scl = w.take<spx::SplitCluster>((size_t)C);
-  const int32_t range_cap = split_range_cap(csr);
-  spx::SplitRange* ranges = w.take<spx::SplitRange>((size_t)range_cap);
-  char* scratch = w.base + w.used;
+  const BinMeanWs W = carve_bin_mean(w, csr, params);
+  // counters: [0] deferred past the wide kernel (segmented fold), [1] left to the
+  // wide kernel, [2] planned split clusters, [3] split ranges, [4] the global
+  // kernel's list, [5] segmented-fold block tasks, [6] its slot tiles, [7] the
+  // split path's list (clusters the segmented fold's arena could not hold)
+  int32_t* n_def = W.counters;
+  int32_t* n_rest = W.counters + 1;
+  int32_t* n_scl = W.counters + 2;
+  int32_t* n_ranges = W.counters + 3;
+  int32_t* n_glist = W.counters + 4;
+  int32_t* n_tasks = W.counters + 5;
+  int32_t* n_tiles = W.counters + 6;
+  int32_t* n_split = W.counters + 7;
 
   spx::BinMeanParams P;
   P.minimum = params->minimum;
@@ -189,32 +241,56 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const spx::CsrView V = view(csr);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
-  if (hipMemsetAsync(counters, 0, 5 * sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
+  // the 8 counters and the bump pointer share the first 256 B of the workspace
+  if (hipMemsetAsync(W.counters, 0, 256 + sizeof(unsigned long long), s) != hipSuccess)
+    return check_launch("spx_bin_mean memset");
+  // register path; its leftovers (longer spectra, more spectra, unsorted, > 1,536
+  // bins) all go to the wide kernel's list
   hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                     charge_out, status, rest, n_rest, def, n_def);
+                     charge_out, status, W.rest, n_rest, W.rest, n_rest);
   if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
-#if SPX_BM_WIDE
-  hipLaunchKernelGGL(spx::bin_mean_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),
-                     dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
+  const dim3 gcl((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048)));
+  hipLaunchKernelGGL(spx::bin_mean_wide_kernel, gcl, dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out, status,
+                     W.rest, n_rest, W.def, n_def, W.glist, n_glist);
   if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
-#else
-  hipLaunchKernelGGL(spx::bin_mean_lds_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048))),
-                     dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, rest, n_rest, def, n_def);
-  if (int rc = check_launch("bin_mean_lds_kernel")) return rc;
-#endif
-  const dim3 gsplit((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048)));
-  hipLaunchKernelGGL(spx::bin_mean_split_plan_kernel, gsplit, dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                     charge_out, status, def, n_def, scl, n_scl, ranges, n_ranges, range_cap, glist, n_glist);
+  // segmented fold of the clusters past the wide kernel
+  const dim3 gtask((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.n_task_cap, 8192)));
+  const dim3 gtile((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.n_tile_cap, 8192)));
+  const dim3 bsg(spx::SG_BLOCK);
+  hipLaunchKernelGGL(spx::bin_mean_seg_setup_kernel, gcl, bsg, 0, s, V, P, O, prec_out, charge_out, status, W.def,
+                     n_def, W.meta, W.arena, W.bump, W.arena_bytes, W.task_cl, n_tasks);
+  if (int rc = check_launch("bin_mean_seg_setup_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_seg_occupy_kernel, gtask, bsg, 0, s, V, P, W.meta, W.arena, W.task_cl, n_tasks);
+  if (int rc = check_launch("bin_mean_seg_occupy_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_seg_prefix_kernel, gcl, bsg, 0, s, V, P, O, prec_out, charge_out, status, n_def,
+                     W.meta, W.arena, W.bump, W.arena_bytes, W.tile_cl, n_tiles);
+  if (int rc = check_launch("bin_mean_seg_prefix_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_seg_mask_kernel, gtask, bsg, 0, s, V, P, W.meta, W.arena, W.task_cl, n_tasks);
+  if (int rc = check_launch("bin_mean_seg_mask_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_seg_count_kernel, gtile, bsg, 0, s, W.meta, W.arena, W.tile_cl, n_tiles);
+  if (int rc = check_launch("bin_mean_seg_count_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_seg_scan_kernel, gcl, bsg, 0, s, n_def, W.meta, W.arena);
+  if (int rc = check_launch("bin_mean_seg_scan_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_seg_place_kernel, gtask, bsg, 0, s, V, P, W.meta, W.arena, W.task_cl, n_tasks);
+  if (int rc = check_launch("bin_mean_seg_place_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_seg_fold_kernel, gtile, bsg, 0, s, P, W.meta, W.arena, W.tile_cl, n_tiles);
+  if (int rc = check_launch("bin_mean_seg_fold_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_seg_emit_kernel, gcl, bsg, 0, s, V, O, prec_out, charge_out, status, n_def, W.meta,
+                     W.arena, W.split_list, n_split, W.glist, n_glist);
+  if (int rc = check_launch("bin_mean_seg_emit_kernel")) return rc;
+  // bin-range split path for what the arena could not hold, then the global kernel
+  hipLaunchKernelGGL(spx::bin_mean_split_plan_kernel, gcl, dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                     charge_out, status, W.split_list, n_split, W.scl, n_scl, W.ranges, n_ranges, W.range_cap, W.glist,
+                     n_glist);
   if (int rc = check_launch("bin_mean_split_plan_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_split_fold_kernel, dim3(4096), dim3(spx::BM_BLOCK), 0, s, V, P, O, scl, ranges,
-                     n_ranges, range_cap);
+  hipLaunchKernelGGL(spx::bin_mean_split_fold_kernel, dim3(4096), dim3(spx::BM_BLOCK), 0, s, V, P, O, W.scl, W.ranges,
+                     n_ranges, W.range_cap);
   if (int rc = check_launch("bin_mean_split_fold_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_split_emit_kernel, gsplit, dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                     charge_out, status, scl, n_scl, ranges, glist, n_glist);
+  hipLaunchKernelGGL(spx::bin_mean_split_emit_kernel, gcl, dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                     charge_out, status, W.scl, n_scl, W.ranges, W.glist, n_glist);
   if (int rc = check_launch("bin_mean_split_emit_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)bin_mean_fallback_grid(C, params, dcap)),
-                     dim3(spx::BM_BLOCK), 0, s, V, P,
-                     O, prec_out, charge_out, status, glist, n_glist, scratch,
+                     dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, W.glist, n_glist, W.scratch,
                      spx::bin_mean_slice_bytes(P.n_words, dcap), (int)std::min<int64_t>(dcap, INT32_MAX));
   return check_launch("bin_mean_global_kernel");
 }

@@ -452,11 +452,11 @@ def test_medoid_many_runtime_deferrals(gpu):
 
 
 def test_bin_mean_split_path(gpu):
-    """Clusters past the register and LDS kernels (> 128 spectra, > 1,536 distinct
-    bins, 600-peak spectra) through the bin-range split path: one 3,000-spectrum
-    cluster, long-spectrum clusters, a giant unsorted one (flagged by the fold ->
-    the global kernel), a giant mixed-charge one and NaN m/z in a long one, mixed
-    with ordinary clusters; bit-exact against the C oracle, values included."""
+    """Clusters past the register and wide kernels (> 128 spectra, > 4,096 distinct
+    bins) through the segmented fold and -- with its arena capped -- the bin-range
+    split path: one 3,000-spectrum cluster, long-spectrum clusters, a giant unsorted
+    one (-> the global kernel), a giant mixed-charge one and NaN m/z in a long one,
+    mixed with ordinary clusters; bit-exact against the C oracle, values included."""
     big = make_clusters_np(1, seed=41, sizes=np.array([3000]))
     longsp = make_clusters_np(12, seed=42, n_template=600, max_size=30)
     plain = make_clusters_np(30, seed=43)
@@ -485,9 +485,17 @@ def test_bin_mean_split_path(gpu):
     # global kernel and their reserved records are dropped, never read unwritten
     import os
 
-    for cap in ("1", "3", "7"):
-        os.environ["SPX_SPLIT_RANGE_CAP"] = cap
+    # the segmented fold's arena (SPX_SEG_ARENA): none (every deferred cluster takes
+    # the bin-range split path), room for part of the clusters
+    for arena in ("0", "400000"):
+        os.environ["SPX_SEG_ARENA"] = arena
         try:
             assert_bin_mean_equal(_bin_mean(csr), want)
+            for cap in ("1", "3", "7"):
+                os.environ["SPX_SPLIT_RANGE_CAP"] = cap
+                try:
+                    assert_bin_mean_equal(_bin_mean(csr), want)
+                finally:
+                    del os.environ["SPX_SPLIT_RANGE_CAP"]
         finally:
-            del os.environ["SPX_SPLIT_RANGE_CAP"]
+            del os.environ["SPX_SEG_ARENA"]
