@@ -279,13 +279,57 @@ __device__ __forceinline__ int seg_slot(const SegMeta& M, const char* arena, int
   return bitmap_rank(B, pre, (int64_t)key);
 }
 
-// mask: one workgroup per (cluster, block) task -- bit s of mask[b][slot] for
-// every contribution (spectrum s of block b is the last peak of that bin)
+// ---- block-local slots: the block's own occupied bins, ranked in LDS, so the
+// mask and place passes work on LDS arrays instead of global atomics / lookups
+#ifndef SPX_SG_LCAP
+#define SPX_SG_LCAP 3072
+#endif
+constexpr int SG_LCAP = SPX_SG_LCAP;  // block-local occupied bins held in LDS (more: the global-atomic form)
+
+struct SegBlockSmem {
+  unsigned long long bits[BM_WMAX];
+  uint16_t lpre[BM_WMAX];
+  unsigned long long lmask[SG_LCAP];  // mask pass: bit s = spectrum s of the block contributes
+  uint32_t lbase[SG_LCAP];            // place pass: the slot's segment position of the block's first
+  int32_t soff[SG_SB + 1];
+  int tmp[SG_BLOCK / kWave + 1];
+};
+
+// walk 1 + prefix: the block's occupied bins and their local ranks; returns D_b
+__device__ __forceinline__ int seg_local_slots(const CsrView& v, const BinMeanParams& P, const SegMeta& M, int b,
+                                               SegBlockSmem& L) {
+  const int tid = threadIdx.x;
+  for (int w = tid; w < P.n_words; w += SG_BLOCK) L.bits[w] = 0ull;
+  seg_block_offsets(v, M, b, L.soff);
+  lds_barrier();
+  seg_walk_block(v, P, M, b, L.soff, [&](int64_t, int32_t key, bool last, int) {
+    if (last) atomicOr(&L.bits[key >> 6], 1ull << (key & 63));
+  });
+  lds_barrier();
+  return bitmap_prefix<SG_BLOCK, uint16_t, true>(L.bits, L.lpre, P.n_words, L.tmp);
+}
+
+// f(local slot, bin) for every occupied bin of the block (thread per bitmap word)
+template <class F>
+__device__ __forceinline__ void seg_for_local_slots(const BinMeanParams& P, const SegBlockSmem& L, F&& f) {
+  for (int w = threadIdx.x; w < P.n_words; w += SG_BLOCK) {
+    unsigned long long x = L.bits[w];
+    int ls = L.lpre[w];
+    while (x) {
+      const int bit = __ffsll((long long)x) - 1;
+      x &= x - 1ull;
+      f(ls++, w * 64 + bit);
+    }
+  }
+}
+
+// mask: one workgroup per (cluster, block) task -- mask[b][slot] bit s: spectrum
+// s of block b holds the last peak of that bin
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_mask_kernel(CsrView v, BinMeanParams P,
                                                                      const SegMeta* meta, char* arena,
                                                                      const int32_t* task_cl,
                                                                      const int32_t* n_tasks) {
-  __shared__ int32_t soff[SG_SB + 1];
+  __shared__ SegBlockSmem L;
   const int tid = threadIdx.x;
   const int32_t nt = *n_tasks;
   for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
@@ -295,19 +339,30 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_mask_kernel(CsrView v, 
     const int b = t - M.task0;
     unsigned long long* mask = reinterpret_cast<unsigned long long*>(arena + M.mask) + (int64_t)b * M.D;
     for (int d = tid; d < M.D; d += SG_BLOCK) mask[d] = 0ull;
-    seg_block_offsets(v, M, b, soff);
-    __syncthreads();  // the row is zero before any bit is set (global memory)
-    seg_walk_block(v, P, M, b, soff, [&](int64_t, int32_t key, bool last, int s) {
-      if (last) atomicOr(&mask[seg_slot(M, arena, key)], 1ull << s);
-    });
-    __syncthreads();  // soff is reused by the next task
+    const int Db = seg_local_slots(v, P, M, b, L);
+    if (Db <= SG_LCAP) {
+      for (int ls = tid; ls < Db; ls += SG_BLOCK) L.lmask[ls] = 0ull;
+      lds_barrier();
+      seg_walk_block(v, P, M, b, L.soff, [&](int64_t, int32_t key, bool last, int s) {
+        if (last) atomicOr(&L.lmask[bitmap_rank(L.bits, L.lpre, (int64_t)key)], 1ull << s);
+      });
+      __syncthreads();  // the LDS masks are complete and the row's zeros have landed
+      seg_for_local_slots(P, L, [&](int ls, int32_t key) { mask[seg_slot(M, arena, key)] = L.lmask[ls]; });
+    } else {  // a block with more distinct bins than LDS holds: global atomics
+      __syncthreads();
+      seg_walk_block(v, P, M, b, L.soff, [&](int64_t, int32_t key, bool last, int s) {
+        if (last) atomicOr(&mask[seg_slot(M, arena, key)], 1ull << s);
+      });
+    }
+    __syncthreads();  // the LDS is reused by the next task
   }
 }
 
-// count: one thread per slot -- contributions of earlier blocks and the total
+// count: one thread per slot -- contributions of earlier blocks (boff) and the total
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_count_kernel(const SegMeta* meta, char* arena,
                                                                       const int32_t* tile_cl,
                                                                       const int32_t* n_tiles) {
+  constexpr int U = 8;  // mask loads in flight per thread
   const int32_t nt = *n_tiles;
   for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     const int i = tile_cl[t];
@@ -315,38 +370,54 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_count_kernel(const SegM
     if (M.state != kSegOk) continue;
     const int d = (t - M.tile0) * SG_TILE + threadIdx.x;
     if (d >= M.D) continue;
-    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(arena + M.mask);
-    uint16_t* boff = reinterpret_cast<uint16_t*>(arena + M.boff);
+    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(arena + M.mask) + d;
+    uint16_t* boff = reinterpret_cast<uint16_t*>(arena + M.boff) + d;
     uint32_t run = 0;
-    for (int b = 0; b < M.nb; ++b) {
-      boff[(int64_t)b * M.D + d] = (uint16_t)run;
-      run += (uint32_t)__popcll(mask[(int64_t)b * M.D + d]);
+    for (int b0 = 0; b0 < M.nb; b0 += U) {
+      unsigned long long x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = b0 + u < M.nb ? mask[(int64_t)(b0 + u) * M.D] : 0ull;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (b0 + u < M.nb) boff[(int64_t)(b0 + u) * M.D] = (uint16_t)run;
+        run += (uint32_t)__popcll(x[u]);
+      }
     }
     reinterpret_cast<uint32_t*>(arena + M.seg)[d] = run;
   }
 }
 
 // scan: one workgroup per cluster -- seg[slot] = contributions of earlier slots
+// (thread t scans the contiguous run t*per .. (t+1)*per, its loads batched)
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_scan_kernel(const int32_t* n_list, const SegMeta* meta,
                                                                      char* arena) {
   __shared__ uint32_t tmp[SG_BLOCK / kWave + 1];
+  constexpr int U = 8;
   const int tid = threadIdx.x;
   const int32_t nl = *n_list;
   for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
     const SegMeta M = meta[i];
     if (M.state != kSegOk) continue;  // uniform
     uint32_t* seg = reinterpret_cast<uint32_t*>(arena + M.seg);
-    const int per = (M.D + SG_BLOCK - 1) / SG_BLOCK, d0 = tid * per;
+    const int per = (M.D + SG_BLOCK - 1) / SG_BLOCK, d0 = tid * per, d1 = min(M.D, d0 + per);
     uint32_t local = 0;
-    for (int k = 0; k < per; ++k)
-      if (d0 + k < M.D) local += seg[d0 + k];
+    for (int k0 = d0; k0 < d1; k0 += U) {
+      uint32_t x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = k0 + u < d1 ? seg[k0 + u] : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u) local += x[u];
+    }
     uint32_t total;
     uint32_t base = block_exclusive_scan<SG_BLOCK, uint32_t>(local, tmp, total);
-    for (int k = 0; k < per; ++k) {
-      if (d0 + k < M.D) {
-        const uint32_t x = seg[d0 + k];
-        seg[d0 + k] = base;
-        base += x;
+    for (int k0 = d0; k0 < d1; k0 += U) {
+      uint32_t x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = k0 + u < d1 ? seg[k0 + u] : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k0 + u < d1) seg[k0 + u] = base;
+        base += x[u];
       }
     }
     if (tid == 0) seg[M.D] = total;
@@ -355,36 +426,53 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_scan_kernel(const int32
 }
 
 // place: one workgroup per (cluster, block) task -- each contribution into its
-// bin's segment, in spectrum order
+// bin's segment at seg[slot] + boff[b][slot] + popcount(mask[b][slot] below s),
+// i.e. in spectrum order
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_place_kernel(CsrView v, BinMeanParams P,
                                                                       const SegMeta* meta, char* arena,
                                                                       const int32_t* task_cl,
                                                                       const int32_t* n_tasks) {
-  __shared__ int32_t soff[SG_SB + 1];
+  __shared__ SegBlockSmem L;
   const int32_t nt = *n_tasks;
   for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     const int i = task_cl[t];
     const SegMeta M = meta[i];
     if (M.state != kSegOk) continue;  // uniform
     const int b = t - M.task0;
-    seg_block_offsets(v, M, b, soff);
-    __syncthreads();
     const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(arena + M.mask) + (int64_t)b * M.D;
     const uint16_t* boff = reinterpret_cast<const uint16_t*>(arena + M.boff) + (int64_t)b * M.D;
     const uint32_t* seg = reinterpret_cast<const uint32_t*>(arena + M.seg);
     double2* vals = reinterpret_cast<double2*>(arena + M.vals);
-    seg_walk_block(v, P, M, b, soff, [&](int64_t k, int32_t key, bool last, int s) {
-      if (!last) return;
-      const int d = seg_slot(M, arena, key);
-      const uint32_t pos = seg[d] + boff[d] + (uint32_t)__popcll(mask[d] & ((1ull << s) - 1ull));
-      vals[pos] = make_double2(v.mz[k], v.inten[k]);
-    });
-    __syncthreads();  // soff is reused by the next task
+    const int Db = seg_local_slots(v, P, M, b, L);
+    if (Db <= SG_LCAP) {
+      seg_for_local_slots(P, L, [&](int ls, int32_t key) {
+        const int d = seg_slot(M, arena, key);
+        L.lbase[ls] = seg[d] + boff[d];
+        L.lmask[ls] = mask[d];
+      });
+      lds_barrier();
+      seg_walk_block(v, P, M, b, L.soff, [&](int64_t k, int32_t key, bool last, int s) {
+        if (!last) return;
+        const int ls = bitmap_rank(L.bits, L.lpre, (int64_t)key);
+        const uint32_t pos = L.lbase[ls] + (uint32_t)__popcll(L.lmask[ls] & ((1ull << s) - 1ull));
+        vals[pos] = make_double2(v.mz[k], v.inten[k]);
+      });
+    } else {
+      seg_walk_block(v, P, M, b, L.soff, [&](int64_t k, int32_t key, bool last, int s) {
+        if (!last) return;
+        const int d = seg_slot(M, arena, key);
+        const uint32_t pos = seg[d] + boff[d] + (uint32_t)__popcll(mask[d] & ((1ull << s) - 1ull));
+        vals[pos] = make_double2(v.mz[k], v.inten[k]);
+      });
+    }
+    __syncthreads();  // the LDS is reused by the next task
   }
 }
 
 // fold: one thread per slot over its segment, in spectrum order (binning.py:198-199),
-// then the quorum (:181-183) and the means (:209-222)
+// loads issued SG_FU ahead of the (serial) f32 accumulation; then the quorum
+// (:181-183) and the means (:209-222)
+constexpr int SG_FU = 8;
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_fold_kernel(BinMeanParams P, const SegMeta* meta,
                                                                      char* arena, const int32_t* tile_cl,
                                                                      const int32_t* n_tiles) {
@@ -399,10 +487,19 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_fold_kernel(BinMeanPara
     const double2* vals = reinterpret_cast<const double2*>(arena + M.vals);
     const uint32_t a = seg[d], e = seg[d + 1];
     float si = 0.0f, sm = 0.0f;
-    for (uint32_t k = a; k < e; ++k) {
-      const double2 x = vals[k];
-      si = (float)((double)si + x.y);
-      sm = (float)((double)sm + x.x);
+    double2 ring[SG_FU];
+#pragma unroll
+    for (int u = 0; u < SG_FU; ++u) ring[u] = vals[min(a + u, e - 1)];  // e > a: every slot has a contribution
+    for (uint32_t k0 = a; k0 < e; k0 += SG_FU) {
+#pragma unroll
+      for (int u = 0; u < SG_FU; ++u) {
+        const double2 x = ring[u];
+        ring[u] = vals[min(k0 + u + SG_FU, e - 1)];  // (clamped: the tail re-reads the last)
+        if (k0 + u < e) {
+          si = (float)((double)si + x.y);
+          sm = (float)((double)sm + x.x);
+        }
+      }
     }
     const uint32_t cnt = e - a;
     const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)M.n * 0.25) + 1u : 1u;
@@ -414,6 +511,53 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_fold_kernel(BinMeanPara
   }
 }
 
+// numpy's pairwise mean of x[0..n) by a whole workgroup: the leaves (<= 128
+// elements, numpy's recursion) summed in parallel, one thread per leaf, then the
+// tree over the leaf sums by thread 0 in numpy's order.  `lo`, `len` and `sum`
+// hold SG_MAXLEAF entries in LDS; more leaves than that: thread 0 alone.
+constexpr int SG_MAXLEAF = SG_BLOCK;
+__device__ double seg_pw_mean(const double* x, int64_t n, int64_t* lo, int64_t* len, double* sum, int* nleaf) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    // the leaves left to right: split [l, l+m) at h = m/2 - (m/2)%8 while m > 128
+    int k = 0;
+    int64_t st_l[40], st_m[40];
+    int sp = 0;
+    st_l[0] = 0;
+    st_m[0] = n;
+    sp = 1;
+    while (sp > 0 && k <= SG_MAXLEAF) {
+      --sp;
+      const int64_t l = st_l[sp], m = st_m[sp];
+      if (m <= 128) {
+        if (k < SG_MAXLEAF) { lo[k] = l; len[k] = m; }
+        ++k;
+      } else {
+        int64_t h = m / 2;
+        h -= h % 8;
+        st_l[sp] = l + h; st_m[sp] = m - h; ++sp;  // right half after the left
+        st_l[sp] = l; st_m[sp] = h; ++sp;
+      }
+    }
+    *nleaf = k;
+  }
+  __syncthreads();
+  const int nl = *nleaf;
+  if (nl > SG_MAXLEAF) {  // thread 0, serially
+    double r = 0.0;
+    if (tid == 0) r = pw_sum([&](int64_t j) { return x[j]; }, n) / (double)n;
+    return r;
+  }
+  if (tid < nl) sum[tid] = pw_leaf([&](int64_t j) { return x[j]; }, lo[tid], len[tid]);
+  __syncthreads();
+  double r = 0.0;
+  if (tid == 0) {
+    int next = 0;
+    r = pw_tree([&](int64_t, int64_t) { return sum[next++]; }, n) / (double)n;
+  }
+  return r;
+}
+
 // emit: one workgroup per cluster -- kept slots in bin order, count, charge, np.mean
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_emit_kernel(CsrView v, PeaksOut out, double* prec_out,
                                                                      int32_t* charge_out, int32_t* status,
@@ -422,6 +566,10 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_emit_kernel(CsrView v, 
                                                                      int32_t* n_split, int32_t* glist,
                                                                      int32_t* n_glist) {
   __shared__ uint32_t tmp[SG_BLOCK / kWave + 1];
+  __shared__ int64_t leaf_lo[SG_MAXLEAF], leaf_len[SG_MAXLEAF];
+  __shared__ double leaf_sum[SG_MAXLEAF];
+  __shared__ int nleaf;
+  constexpr int U = 8;
   const int tid = threadIdx.x;
   const int32_t nl = *n_list;
   for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
@@ -435,26 +583,31 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_emit_kernel(CsrView v, 
     }
     const uint32_t* keep = reinterpret_cast<const uint32_t*>(arena + M.keep);
     const double2* res = reinterpret_cast<const double2*>(arena + M.res);
-    const int per = (M.D + SG_BLOCK - 1) / SG_BLOCK, d0 = tid * per;
+    const int per = (M.D + SG_BLOCK - 1) / SG_BLOCK, d0 = tid * per, d1 = min(M.D, d0 + per);
     uint32_t local = 0;
-    for (int k = 0; k < per; ++k)
-      if (d0 + k < M.D) local += keep[d0 + k];
+    for (int k0 = d0; k0 < d1; k0 += U) {
+      uint32_t x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[u] = k0 + u < d1 ? keep[k0 + u] : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u) local += x[u];
+    }
     uint32_t total;
     uint32_t o = block_exclusive_scan<SG_BLOCK, uint32_t>(local, tmp, total);
-    for (int k = 0; k < per; ++k) {
-      const int d = d0 + k;
-      if (d < M.D && keep[d]) {
+    for (int d = d0; d < d1; ++d) {
+      if (keep[d]) {
         const double2 r = res[d];
         out.mz[M.p0 + o] = r.x;
         out.inten[M.p0 + o] = r.y;
         ++o;
       }
     }
+    const int64_t s0 = v.cluster_off[M.c];
+    const double pm = seg_pw_mean(v.prec_mz + s0, M.n, leaf_lo, leaf_len, leaf_sum, &nleaf);  // np.mean (binning.py:224)
     if (tid == 0) {
-      const int64_t s0 = v.cluster_off[M.c];
       out.count[M.c] = total;
       charge_out[M.c] = v.charge[s0];
-      prec_out[M.c] = pw_sum([&](int64_t j) { return v.prec_mz[s0 + j]; }, M.n) / (double)M.n;  // np.mean (binning.py:224)
+      prec_out[M.c] = pm;
       status[M.c] = kOk;
     }
     __syncthreads();

@@ -149,14 +149,23 @@ __device__ __forceinline__ void md_defer(int64_t c, int64_t s0, int n, int32_t* 
 //       ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) by shuffles, sequential tail,
 //       total = (row + col)/n
 //   P6  lowest index of the minimum (:103-110), one wave
-// Deferred to the large path: n > 64, > MR_UMAX*256 peaks, a bin outside
+// Deferred (to the wide kernel, then the large path): n > 64, > MR_UMAX*256 peaks, a bin outside
 // [0, 65,536), > 64 * MD_KWMAX distinct bins.
 constexpr int MR_UMAX = 48;                  // peaks per thread (12,288 per cluster)
 constexpr int MR_PMAX = MR_UMAX * MD_BLOCK;
 constexpr int MR_WMAX = 512;                 // union-bitmap words: bins < 32,768 (m/z < 3,276.8 at 0.1)
 constexpr int MR_TRI = MD_NMAX * (MD_NMAX + 1) / 2;  // packed upper triangle of the distance matrix
 
+// The wide variant (medoid_wide_kernel): what the register kernel defers for its
+// peak or bin caps alone (n <= 64 still) -- 512 threads, 64 peaks per thread
+// (32,768 per cluster), 95 row words (<= 6,080 occupied bins): 59 KB of LDS, two
+// workgroups per CU.  600-peak spectra reach it from n ~ 20 on.
+constexpr int MW_BLOCK = 512;
+constexpr int MW_UMAX = 64;
+constexpr int MW_PMAX = MW_UMAX * MW_BLOCK;
+constexpr int MW_KWMAX = 95;
 
+template <int BLOCK, int UMAX, int KWMAX>
 struct MedoidRegSmem {
   union {
     struct {
@@ -166,30 +175,33 @@ struct MedoidRegSmem {
       // record put them on 16 of 32 and 8 of 32 banks)
       unsigned long long bits[MR_WMAX];
       uint32_t pre[MR_WMAX];
-      unsigned long long rows[MD_NMAX * MD_KWMAX];
-      unsigned long long sbits[MR_PMAX / 64];    // bit r: peak r starts spectrum >= 1
-      uint8_t spre[MR_PMAX / 64];                // spectra started before word w
+      unsigned long long rows[MD_NMAX * KWMAX];
+      unsigned long long sbits[UMAX * BLOCK / 64];  // bit r: peak r starts spectrum >= 1
+      uint8_t spre[UMAX * BLOCK / 64];              // spectra started before word w
     } a;                                         // P0..P4a
     double d[MR_TRI];                            // P4b..P5: d(i, j), j >= i, row-major packed
   } u;
   int32_t soff[MD_NMAX + 1];
   double totals[MD_NMAX];
-  int tmp[MD_BLOCK / kWave + 1];
+  int tmp[BLOCK / kWave + 1];
   long long red[4];
-  int votes[2 * (MD_BLOCK / kWave)];
+  int votes[2 * (BLOCK / kWave)];
 };
 
-__global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
-                                                              double* totals_out, int32_t* deferred,
-                                                              int32_t* n_deferred, MedoidMeta* meta) {
-  __shared__ MedoidRegSmem L;
+// The small-cluster body for one cluster c: BLOCK threads, <= UMAX peaks per
+// thread, <= 64 * KWMAX occupied bins.  defer() hands a cluster past those caps on.
+template <int BLOCK, int UMAX, int KWMAX, class Defer>
+__device__ __forceinline__ void medoid_small_body(const CsrView& v, const MedoidParams& P, int64_t* rep,
+                                                  double* totals_out, MedoidRegSmem<BLOCK, UMAX, KWMAX>& L,
+                                                  int64_t c, const Defer& defer) {
+  constexpr int PMAX = UMAX * BLOCK;
+  constexpr int NWV = BLOCK / kWave;
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
-  const int64_t c = blockIdx.x;
   SPX_STAMP(0);
   const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
   const int n = (int)(s1 - s0);
   if (s1 - s0 > MD_NMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
+    if (tid == 0) defer(c, s0, n);
     return;
   }
   if (n <= 1) {
@@ -201,8 +213,8 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
   }
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
   const int np = (int)(p1 - p0);
-  if (p1 - p0 > MR_PMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
+  if (p1 - p0 > PMAX) {
+    if (tid == 0) defer(c, s0, n);
     return;
   }
   const double* __restrict__ mzc = v.mz + p0;
@@ -211,15 +223,15 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
   // ceil(mz/tol) in [0, 65,536) (m/z < 6,553.6 at tol 0.1): the xcorr is a set
   // intersection, so neither a range pass nor sorted spectra are needed.
   const int nsw = (np + 63) / 64;
-  for (int w = tid; w < nsw; w += MD_BLOCK) L.u.a.sbits[w] = 0ull;
+  for (int w = tid; w < nsw; w += BLOCK) L.u.a.sbits[w] = 0ull;
   if (tid <= n) L.soff[tid] = (int32_t)(v.spec_off[s0 + tid] - p0);
-  for (int w = tid; w < MR_WMAX; w += MD_BLOCK) L.u.a.bits[w] = 0ull;
+  for (int w = tid; w < MR_WMAX; w += BLOCK) L.u.a.bits[w] = 0ull;
   __syncthreads();
   if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
     const bool empty_spec = tid < n && L.soff[tid + 1] == L.soff[tid];
     if (tid == 0) L.red[1] = __ballot(empty_spec) != 0ull;
   }
-  for (int j = 1 + tid; j < n; j += MD_BLOCK) {
+  for (int j = 1 + tid; j < n; j += BLOCK) {
     const int r = L.soff[j];
     if (r < np) atomicOr(&L.u.a.sbits[r >> 6], 1ull << (r & 63));
   }
@@ -242,10 +254,10 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
   // The batch count is a compile-time constant per size class, so every load
   // is unconditional: no ring register is ever a merge of a load and another
   // value, and the compiler waits with counted vmcnt.
-  uint32_t bins[MR_UMAX / 2];
+  uint32_t bins[UMAX / 2];
   int outside = 0;
   constexpr uint32_t kBins = (uint32_t)MR_WMAX * 64u;
-  constexpr int NB = MR_UMAX / 8;
+  constexpr int NB = UMAX / 8;
   auto pass1 = [&](auto nbt_c) __attribute__((always_inline)) {
     constexpr int NBT = decltype(nbt_c)::value;
     double mb[2][8];
@@ -254,7 +266,7 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
       if (bt < NBT) {  // issue batch bt
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const int r = (bt * 8 + q) * MD_BLOCK + tid;
+          const int r = (bt * 8 + q) * BLOCK + tid;
           mb[bt & 1][q] = mzc[r < np ? r : 0];
         }
       }
@@ -263,7 +275,7 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int u = pb * 8 + q;
-          const int r = u * MD_BLOCK + tid;
+          const int r = u * BLOCK + tid;
           uint32_t b = 0u;
           if (r < np) {
             const int64_t bb = md_bin(mb[pb & 1][q], P);
@@ -281,18 +293,20 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
       }
     }
   };
-  switch ((np + 8 * MD_BLOCK - 1) / (8 * MD_BLOCK)) {  // uniform size class
+  switch ((np + 8 * BLOCK - 1) / (8 * BLOCK)) {  // uniform size class
     case 0: break;
     case 1: pass1(std::integral_constant<int, 1>{}); break;
     case 2: pass1(std::integral_constant<int, 2>{}); break;
     case 3: pass1(std::integral_constant<int, 3>{}); break;
     case 4: pass1(std::integral_constant<int, 4>{}); break;
     case 5: pass1(std::integral_constant<int, 5>{}); break;
+    case 6: pass1(std::integral_constant<int, (NB < 6 ? NB : 6)>{}); break;
+    case 7: pass1(std::integral_constant<int, (NB < 7 ? NB : 7)>{}); break;
     default: pass1(std::integral_constant<int, NB>{}); break;
   }
-  static_assert(NB == 6, "size classes above cover MR_UMAX = 48");
-  if (block_any<MD_BLOCK, true>(outside, L.votes, 0)) {  // m/z out of the LDS bitmap's range: general path
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
+  static_assert(NB >= 5 && NB <= 8, "size classes above cover 40..64 peaks per thread");
+  if (block_any<BLOCK, true>(outside, L.votes, 0)) {  // m/z out of the LDS bitmap's range: general path
+    if (tid == 0) defer(c, s0, n);
     return;
   }
   SPX_STAMP(2);
@@ -301,7 +315,7 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
   {
     // all MR_WMAX records (P0 cleared them), RPT
     // contiguous per thread, read unconditionally: the reads pipeline
-    constexpr int RPT = MR_WMAX / MD_BLOCK;
+    constexpr int RPT = MR_WMAX / BLOCK;
     const int w0 = tid * RPT;
     unsigned long long b[RPT];
 #pragma unroll
@@ -309,7 +323,7 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
     int local = 0;
 #pragma unroll
     for (int k = 0; k < RPT; ++k) local += __popcll(b[k]);
-    int base = block_exclusive_scan<MD_BLOCK, int, true>(local, L.tmp, K);
+    int base = block_exclusive_scan<BLOCK, int, true>(local, L.tmp, K);
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       L.u.a.pre[w0 + k] = (uint32_t)base;
@@ -319,26 +333,26 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
   // row stride KW is odd: lanes reading rows j, j+1, ... at one word hit
   // different LDS banks (an even stride of u64s would fold them together)
   const int KW = ((K + 63) / 64) | 1;
-  if (KW > MD_KWMAX) {
-    if (tid == 0) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
+  if (KW > KWMAX) {
+    if (tid == 0) defer(c, s0, n);
     return;
   }
   SPX_STAMP(3);
   // P3: bit-packed rows from the register bins
-  for (int w = tid; w < n * KW; w += MD_BLOCK) L.u.a.rows[w] = 0ull;
-  // start-bit word 4u + wid and its prefix for slice u, lane u holds them
+  for (int w = tid; w < n * KW; w += BLOCK) L.u.a.rows[w] = 0ull;
+  // start-bit word NWV*u + wid and its prefix for slice u, lane u holds them
   unsigned long long my_sw = 0ull;
   int my_sp = 0;
   {
-    const int w = 4 * lane + wid;
-    if (lane < MR_UMAX && w < nsw) { my_sw = L.u.a.sbits[w]; my_sp = L.u.a.spre[w]; }
+    const int w = NWV * lane + wid;
+    if (lane < UMAX && w < nsw) { my_sw = L.u.a.sbits[w]; my_sp = L.u.a.spre[w]; }
   }
   __syncthreads();
   const unsigned long long upto = (2ull << lane) - 1ull;  // bits 0..lane
 #pragma unroll
-  for (int u = 0; u < MR_UMAX; ++u) {
-    if (u * MD_BLOCK < np) {  // uniform
-      const int r = u * MD_BLOCK + tid;
+  for (int u = 0; u < UMAX; ++u) {
+    if (u * BLOCK < np) {  // uniform
+      const int r = u * BLOCK + tid;
       const uint32_t swlo = __builtin_amdgcn_readlane((uint32_t)my_sw, u);
       const uint32_t swhi = __builtin_amdgcn_readlane((uint32_t)(my_sw >> 32), u);
       const int spw = __builtin_amdgcn_readlane(my_sp, u);
@@ -360,14 +374,14 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
   // P4: every pair i <= j of the row-major upper triangle (row i starts at
   // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
   // registers until the rows are dead
-  constexpr int PPT = (MD_NMAX * (MD_NMAX + 1) / 2 + MD_BLOCK - 1) / MD_BLOCK;  // pairs per thread (9)
+  constexpr int PPT = (MD_NMAX * (MD_NMAX + 1) / 2 + BLOCK - 1) / BLOCK;  // pairs per thread (9)
   const int NP = n * (n + 1) / 2;
   auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
   uint32_t pc[PPT];
   int pij[PPT];
 #pragma unroll
   for (int q = 0; q < PPT; ++q) {
-    const int p = tid + q * MD_BLOCK;
+    const int p = tid + q * BLOCK;
     pc[q] = 0u;
     pij[q] = -1;
     if (p < NP) {
@@ -401,7 +415,7 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
   const int k = lane & 7;
   const bool colside = (lane & 8) != 0;
   const int lim = n - (n % 8);
-  for (int i0 = 0; i0 < n; i0 += MD_BLOCK / 16) {  // uniform
+  for (int i0 = 0; i0 < n; i0 += BLOCK / 16) {  // uniform
     const int i = i0 + tid / 16;
     const bool valid = i < n;
     const int ii = valid ? i : 0;
@@ -442,6 +456,37 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrVi
     if (tid == 0) rep[c] = s0 + idx;
   }
   SPX_STAMP(7);
+}
+
+// Register kernel: one 256-thread workgroup per cluster.  Clusters past its caps
+// go to the wide kernel's list.
+__global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
+                                                              double* totals_out, int32_t* wide, int32_t* n_wide) {
+  __shared__ MedoidRegSmem<MD_BLOCK, MR_UMAX, MD_KWMAX> L;
+  medoid_small_body<MD_BLOCK, MR_UMAX, MD_KWMAX>(v, P, rep, totals_out, L, (int64_t)blockIdx.x,
+                                                [&](int64_t c, int64_t, int) {
+    // every leftover via the wide kernel, which passes n > 64 straight on (one
+    // list target here keeps the kernel's register budget)
+    rep[c] = -4;
+    wide[atomicAdd(n_wide, 1)] = (int32_t)c;
+  });
+}
+
+// Wide kernel: the register kernel's leftovers, grid-stride; what it cannot hold
+// (n > 64 first of all) goes on to the large path.
+__global__ __launch_bounds__(MW_BLOCK, 4) void medoid_wide_kernel(CsrView v, MedoidParams P, int64_t* rep,
+                                                                  double* totals_out, const int32_t* wide,
+                                                                  const int32_t* n_wide, int32_t* deferred,
+                                                                  int32_t* n_deferred, MedoidMeta* meta) {
+  __shared__ MedoidRegSmem<MW_BLOCK, MW_UMAX, MW_KWMAX> L;
+  const int32_t nw = *n_wide;
+  for (int32_t i = blockIdx.x; i < nw; i += gridDim.x) {
+    medoid_small_body<MW_BLOCK, MW_UMAX, MW_KWMAX>(v, P, rep, totals_out, L, (int64_t)wide[i],
+                                                  [&](int64_t c, int64_t s0, int n) {
+      md_defer(c, s0, n, deferred, n_deferred, meta, rep);
+    });
+    __syncthreads();  // the LDS is reused by the next cluster
+  }
 }
 
 // ------------------------------------------------------------ large path

@@ -86,66 +86,59 @@ inline void strip(const char*& b, const char*& e) {
   while (e > b && is_py_space((unsigned char)e[-1])) --e;
 }
 
-// plain decimal float grammar; returns false on anything else
+// Plain decimal float grammar [+-]digits[.digits][e[+-]digits] in ONE pass that
+// also accumulates the significand; returns false on anything else.  Clinger's
+// exact fast path: an integer significand w <= 2^53 scaled by an exactly
+// representable 10^k (|k| <= 22) is ONE correctly rounded IEEE multiply or divide
+// of exact operands -- the correctly rounded value of the decimal, i.e. what
+// strtod and Python's float() return.  m/z and intensity lines ("1234.56789
+// 17.25") take it; anything longer (> 19 significant digits, large exponents)
+// falls to strtod.
 bool parse_float(const char* b, const char* e, double& out) {
+  static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                    1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
   const char* p = b;
-  if (p < e && (*p == '+' || *p == '-')) ++p;
-  const char* d0 = p;
-  while (p < e && *p >= '0' && *p <= '9') ++p;
-  bool digits = p > d0;
+  bool neg = false;
+  if (p < e && (*p == '+' || *p == '-')) { neg = *p == '-'; ++p; }
+  uint64_t w = 0;
+  int nd = 0, frac = 0;
+  bool digits = false, fast = true;
+  for (; p < e && (unsigned)(*p - '0') <= 9u; ++p) {  // integer part
+    digits = true;
+    const unsigned d = (unsigned)(*p - '0');
+    if (w == 0 && d == 0) continue;  // leading zeros: no significant digit
+    if (++nd > 19) fast = false;
+    else w = w * 10 + d;
+  }
   if (p < e && *p == '.') {
     ++p;
-    const char* f0 = p;
-    while (p < e && *p >= '0' && *p <= '9') ++p;
-    digits |= p > f0;
+    for (; p < e && (unsigned)(*p - '0') <= 9u; ++p) {
+      digits = true;
+      const unsigned d = (unsigned)(*p - '0');
+      ++frac;
+      if (w == 0 && d == 0) continue;
+      if (++nd > 19) fast = false;
+      else w = w * 10 + d;
+    }
   }
   if (!digits) return false;
+  int ex = 0;
   if (p < e && (*p == 'e' || *p == 'E')) {
     ++p;
-    if (p < e && (*p == '+' || *p == '-')) ++p;
+    bool eneg = false;
+    if (p < e && (*p == '+' || *p == '-')) { eneg = *p == '-'; ++p; }
     const char* x0 = p;
-    while (p < e && *p >= '0' && *p <= '9') ++p;
+    for (; p < e && (unsigned)(*p - '0') <= 9u; ++p)
+      if (ex < 100000) ex = ex * 10 + (*p - '0');
     if (p == x0) return false;
+    if (eneg) ex = -ex;
   }
   if (p != e) return false;
-  // Clinger's exact fast path: an integer significand w <= 2^53 scaled by an
-  // exactly representable 10^k (|k| <= 22) is ONE correctly rounded IEEE
-  // multiply or divide of exact operands -- the correctly rounded value of the
-  // decimal, i.e. what strtod and Python's float() return.  m/z and intensity
-  // lines ("1234.56789 17.25") take this path; anything longer falls to strtod.
-  {
-    static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
-                                      1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-    const char* q = b;
-    const bool neg = *q == '-';
-    if (*q == '+' || *q == '-') ++q;
-    uint64_t w = 0;
-    int nd = 0, frac = 0;
-    bool in_frac = false, ok = true;
-    for (; q < e && *q != 'e' && *q != 'E'; ++q) {
-      if (*q == '.') { in_frac = true; continue; }
-      if (w == 0 && *q == '0') { frac += in_frac; continue; }  // leading zeros: no significant digit
-      if (++nd > 19) { ok = false; break; }
-      w = w * 10 + (uint64_t)(*q - '0');
-      frac += in_frac;
-    }
-    int ex = 0;
-    if (ok && q < e) {  // exponent (grammar checked above)
-      ++q;
-      const bool eneg = *q == '-';
-      if (*q == '+' || *q == '-') ++q;
-      for (; q < e && ok; ++q) {
-        ex = ex * 10 + (*q - '0');
-        if (ex > 400) ok = false;
-      }
-      if (eneg) ex = -ex;
-    }
-    const int k = ex - frac;
-    if (ok && w <= (uint64_t(1) << 53) && k >= -22 && k <= 22) {
-      const double v = k < 0 ? (double)w / kPow10[-k] : (double)w * kPow10[k];
-      out = neg ? -v : v;
-      return true;
-    }
+  const int k = ex - frac;
+  if (fast && w <= (uint64_t(1) << 53) && k >= -22 && k <= 22) {
+    const double v = k < 0 ? (double)w / kPow10[-k] : (double)w * kPow10[k];
+    out = neg ? -v : v;
+    return true;
   }
   char buf[128];
   const size_t n = (size_t)(e - b);
@@ -158,6 +151,31 @@ bool parse_float(const char* b, const char* e, double& out) {
     out = std::strtod(buf, nullptr);
   }
   return true;
+}
+
+// One line of [p, e): [ls, le) without its terminator (\n, \r\n or \r: Python's
+// universal newlines), p advanced past it; false if the line holds a non-ASCII
+// byte (one pass over the bytes).
+inline bool next_line(const char*& p, const char* e, const char*& ls, const char*& le) {
+  ls = p;
+  const char* q = p;
+  unsigned char hi = 0;
+  for (; q < e; ++q) {
+    const unsigned char c = (unsigned char)*q;
+    if (c == '\n' || c == '\r') break;
+    hi |= c;
+  }
+  le = q;
+  if (q < e) {
+    if (*q == '\r') {
+      ++q;
+      if (q < e && *q == '\n') ++q;
+    } else {
+      ++q;
+    }
+  }
+  p = q;
+  return hi < 0x80;
 }
 
 bool parse_charge(const char* b, const char* e, int64_t& out) {
@@ -190,22 +208,26 @@ void parse_range(const char* b, const char* e, Chunk& C) {
   const char* p = b;
   auto fail = [&](const char* why) { if (C.error.empty()) C.error = std::string("fallback: ") + why; };
   while (p < e && C.error.empty()) {
-    const char* ls = p;
-    const char* le = p;
-    while (le < e && *le != '\n' && *le != '\r') ++le;
-    p = le;  // universal newlines, like Python text mode: \n, \r\n or \r
-    if (p < e) {
-      if (*p == '\r') {
-        ++p;
-        if (p < e && *p == '\n') ++p;
-      } else {
-        ++p;
-      }
-    }
-    for (const char* q = ls; q < le; ++q)
-      if ((unsigned char)*q >= 0x80) { fail("non-ASCII text"); break; }
-    if (!C.error.empty()) break;
+    const char *ls, *le;  // universal newlines, like Python text mode: \n, \r\n or \r
+    if (!next_line(p, e, ls, le)) { fail("non-ASCII text"); break; }
     const size_t n = (size_t)(le - ls);
+    // peak lines first (most lines; none of the keywords below starts with a digit)
+    if (n >= 1 && *ls >= '0' && *ls <= '9') {
+      if (!have || stored) { fail("peak outside a spectrum"); break; }
+      const char *vb = ls, *ve = le;
+      strip(vb, ve);
+      const char* sp = (const char*)std::memchr(vb, ' ', (size_t)(ve - vb));
+      if (!sp) { fail("peak line without ' '"); break; }
+      const char* t1 = sp + 1;
+      const char* sp2 = (const char*)std::memchr(t1, ' ', (size_t)(ve - t1));
+      const char* t1e = sp2 ? sp2 : ve;
+      double a, v;
+      if (!parse_float(vb, sp, a) || !parse_float(t1, t1e, v)) { fail("peak value"); break; }
+      C.mz.push_back(a);
+      C.it.push_back(v);
+      ++cur_np;
+      continue;
+    }
     if (n >= 6 && std::memcmp(ls, "TITLE=", 6) == 0) {
       const char *tb = ls + 6, *te = le;
       strip(tb, te);
@@ -232,22 +254,6 @@ void parse_range(const char* b, const char* e, Chunk& C) {
       if (!have || stored) { fail("CHARGE outside a spectrum"); break; }
       if (!parse_charge(ls + 7, le, cur_z)) { fail("CHARGE value"); break; }
       cur_f |= 2;
-      continue;
-    }
-    if (n >= 1 && *ls >= '0' && *ls <= '9') {
-      if (!have || stored) { fail("peak outside a spectrum"); break; }
-      const char *vb = ls, *ve = le;
-      strip(vb, ve);
-      const char* sp = (const char*)std::memchr(vb, ' ', (size_t)(ve - vb));
-      if (!sp) { fail("peak line without ' '"); break; }
-      const char* t1 = sp + 1;
-      const char* sp2 = (const char*)std::memchr(t1, ' ', (size_t)(ve - t1));
-      const char* t1e = sp2 ? sp2 : ve;
-      double a, v;
-      if (!parse_float(vb, sp, a) || !parse_float(t1, t1e, v)) { fail("peak value"); break; }
-      C.mz.push_back(a);
-      C.it.push_back(v);
-      ++cur_np;
       continue;
     }
     const char *sb = ls, *se = le;
@@ -307,17 +313,8 @@ void parse_range_general(const char* b, const char* e, GenChunk& C) {
   const char* p = b;
   auto fail = [&](const char* why) { if (C.error.empty()) C.error = std::string("fallback: ") + why; };
   while (p < e && C.error.empty()) {
-    const char* ls = p;
-    const char* le = p;
-    while (le < e && *le != '\n' && *le != '\r') ++le;
-    p = le;
-    if (p < e) {
-      if (*p == '\r') { ++p; if (p < e && *p == '\n') ++p; }
-      else ++p;
-    }
-    for (const char* q = ls; q < le; ++q)
-      if ((unsigned char)*q >= 0x80) { fail("non-ASCII text"); break; }
-    if (!C.error.empty()) break;
+    const char *ls, *le;
+    if (!next_line(p, e, ls, le)) { fail("non-ASCII text"); break; }
     const char *sb = ls, *se = le;
     strip(sb, se);
     const size_t n = (size_t)(se - sb);

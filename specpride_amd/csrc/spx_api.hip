@@ -368,7 +368,8 @@ size_t medoid_cluster_bytes(int64_t n, int64_t p) {
                   spx::md_align(n * 8));
 }
 
-bool medoid_large_by_size(int64_t n, int64_t p) { return n > spx::MD_NMAX || p > spx::MR_PMAX; }
+// past the small-cluster kernels by size alone (the register kernel, then the wide one)
+bool medoid_large_by_size(int64_t n, int64_t p) { return n > spx::MD_NMAX || p > spx::MW_PMAX; }
 }  // namespace
 
 extern "C" {
@@ -377,7 +378,8 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
                                  int64_t n_extra) {
   if (C < 0 || (C > 0 && (!hco || !hso)) || n_extra < 0 || (n_extra > 0 && !extra)) return 0;
   const size_t Cm = (size_t)std::max<int64_t>(C, 1);
-  size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(sizeof(int32_t) * Cm) +
+  size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(sizeof(int32_t)) +
+                 align256(sizeof(int32_t) * Cm) + align256(sizeof(int32_t) * Cm) +
                  align256(sizeof(spx::MedoidMeta) * Cm) + 4 * align256(sizeof(int64_t) * (Cm + 1));
   size_t arena = 0, margin = 0;
   for (int64_t c = 0; c < C; ++c) {
@@ -415,7 +417,9 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   if (!workspace) return fail(SPX_ENOSPACE, "spx_medoid: no workspace");
   int32_t* n_def = w.take<int32_t>(1);
   unsigned long long* bump = w.take<unsigned long long>(1);
+  int32_t* n_wide = w.take<int32_t>(1);
   int32_t* def = w.take<int32_t>((size_t)C);
+  int32_t* wide = w.take<int32_t>((size_t)C);
   spx::MedoidMeta* meta = w.take<spx::MedoidMeta>((size_t)C);
   int64_t* tile_base = w.take<int64_t>((size_t)C + 1);
   int64_t* unit_base = w.take<int64_t>((size_t)C + 1);
@@ -431,9 +435,13 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   // and an empty deferred list (the common case) costs a small launch
   const dim3 grid2(spx::MD_GRIDX, std::min<unsigned>(g, 32u)), blk(spx::MD_BLOCK);
 
-  if (hipMemsetAsync(n_def, 0, 512, s) != hipSuccess) return check_launch("spx_medoid memset");
-  hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, def, n_def, meta);
+  // n_def, bump and n_wide: the first 768 B
+  if (hipMemsetAsync(n_def, 0, 768, s) != hipSuccess) return check_launch("spx_medoid memset");
+  hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, wide, n_wide);
   if (int rc = check_launch("medoid_reg_kernel")) return rc;
+  hipLaunchKernelGGL(spx::medoid_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024))),
+                     dim3(spx::MW_BLOCK), 0, s, V, P, rep, totals, wide, n_wide, def, n_def, meta);
+  if (int rc = check_launch("medoid_wide_kernel")) return rc;
   if (!params->large_path) return SPX_SUCCESS;  // deferred clusters keep rep = SPX_REP_DEFERRED
   hipLaunchKernelGGL(spx::medoid_range_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena, bump, arena_bytes);
   if (int rc = check_launch("medoid_range_kernel")) return rc;

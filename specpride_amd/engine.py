@@ -97,16 +97,19 @@ class DeviceBatch:
 
     @classmethod
     def from_host(cls, csr: SpectraCSR, device="cuda") -> "DeviceBatch":
-        # the m/z span over FINITE values only: a NaN/inf peak makes its cluster
-        # SPX_NON_FINITE, it must not blow up the workspace sizing of the others
-        fin = csr.mz[np.isfinite(csr.mz)] if csr.n_peaks else csr.mz
-        span = float(fin.max() - fin.min()) if len(fin) else 0.0
         items = [("cluster_off", csr.cluster_off), ("spec_off", csr.spec_off), ("mz", csr.mz),
                  ("inten", csr.inten), ("prec_mz", csr.prec_mz), ("charge", csr.charge), ("rt", csr.rt)]
         off, total = _layout(items)
         if total > PACKED_MAX_BYTES:
+            # large batches: the span is reduced in HBM after the copy (a host
+            # pass over the m/z array costs more than its transfer)
             tensors = _staged_to_device(items, off, total, device)
+            span = _device_span(tensors["mz"])
         else:
+            # the m/z span over FINITE values only: a NaN/inf peak makes its cluster
+            # SPX_NON_FINITE, it must not blow up the workspace sizing of the others
+            fin = csr.mz[np.isfinite(csr.mz)] if csr.n_peaks else csr.mz
+            span = float(fin.max() - fin.min()) if len(fin) else 0.0
             tensors = _packed_to_device(items, off, total, device)
         tensors.update(n_clusters=csr.n_clusters, n_spectra=csr.n_spectra, n_peaks=csr.n_peaks)
         return cls(tensors, csr.cluster_off, csr.spec_off, span, cluster_ids=csr.cluster_ids, titles=csr.titles)
@@ -116,15 +119,8 @@ class DeviceBatch:
         """Wrap tensors already in HBM (e.g. synthetic.make_clusters_torch)."""
         import torch
 
-        mz = tensors["mz"]
-        span = 0.0
-        if mz.numel():
-            fin = torch.isfinite(mz)
-            inf = torch.tensor(float("inf"), dtype=mz.dtype, device=mz.device)
-            hi = torch.where(fin, mz, -inf).max()
-            lo = torch.where(fin, mz, inf).min()
-            span = float((hi - lo).clamp(min=0.0).item()) if bool(fin.any().item()) else 0.0
-        return cls(tensors, tensors["cluster_off"].cpu().numpy(), tensors["spec_off"].cpu().numpy(), span)
+        return cls(tensors, tensors["cluster_off"].cpu().numpy(), tensors["spec_off"].cpu().numpy(),
+                   _device_span(tensors["mz"]))
 
     def workspace(self, key: str, nbytes: int):
         import torch
@@ -138,6 +134,19 @@ class DeviceBatch:
     @property
     def device(self):
         return self.t["mz"].device
+
+
+def _device_span(mz) -> float:
+    """max - min over the finite values of a device m/z tensor (0.0 if none)."""
+    import torch
+
+    if not mz.numel():
+        return 0.0
+    fin = torch.isfinite(mz)
+    inf = torch.tensor(float("inf"), dtype=mz.dtype, device=mz.device)
+    hi = torch.where(fin, mz, -inf).max()
+    lo = torch.where(fin, mz, inf).min()
+    return float((hi - lo).clamp(min=0.0).item()) if bool(fin.any().item()) else 0.0
 
 
 def _packed_to_device(items, off, total, device):
