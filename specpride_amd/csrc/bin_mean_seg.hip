@@ -130,28 +130,32 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_setup_kernel(
 constexpr int SG_GQ = 4;                       // chunks per group
 constexpr int SG_GROUP = SG_GQ * (kWave - 1);  // peaks per group (252)
 
-template <class F>
-__device__ __forceinline__ int seg_walk_block(const CsrView& v, const BinMeanParams& P, const SegMeta& M, int b,
-                                              const int32_t* soff, F&& f) {
+// walk_block: the same walk for any block of nsb spectra whose offsets (relative
+// to the cluster's first peak p0) are in LDS; kInten also streams the
+// intensities alongside.  f(k, key, last, spectrum-in-block, m/z, intensity).
+template <bool kInten, class F>
+__device__ __forceinline__ int walk_block(const CsrView& v, const BinMeanParams& P, int64_t p0, int nsb,
+                                          const int32_t* soff, F&& f) {
   constexpr int NW = SG_BLOCK / kWave;
   const int lane = lane_id(), wid = wave_id();
-  const int nsb = min(M.n - b * SG_SB, SG_SB);  // spectra in this block
-  const double* __restrict__ mz = v.mz + M.p0;
+  const double* __restrict__ mz = v.mz + p0;
+  const double* __restrict__ it = v.inten + p0;
   const bool owner = lane < kWave - 1;
   // uniform cursor: spectrum sl (this wave's: wid, wid + NW, ...), group start g0
   int sl = wid, g0 = 0;
   auto skip = [&](int& s) { while (s < nsb && soff[s + 1] == soff[s]) s += NW; };
-  auto load = [&](int s, int g, double* m) __attribute__((always_inline)) {
+  auto load = [&](int s, int g, double* m, double* x) __attribute__((always_inline)) {
     const int a = s < nsb ? soff[s] : 0, e = s < nsb ? soff[s + 1] : 0;
 #pragma unroll
     for (int q = 0; q < SG_GQ; ++q) {
       const int k = a + g + q * (kWave - 1) + lane;
       m[q] = k < e ? mz[k] : 0.0;
+      if constexpr (kInten) x[q] = k < e ? it[k] : 0.0;
     }
   };
   skip(sl);
-  double cur[SG_GQ], nxt[SG_GQ];
-  load(sl, g0, cur);
+  double cur[SG_GQ], nxt[SG_GQ], curi[SG_GQ], nxti[SG_GQ];
+  load(sl, g0, cur, curi);
   int bad = 0;
   while (sl < nsb) {  // uniform
     // the following group's cursor and loads first
@@ -161,7 +165,7 @@ __device__ __forceinline__ int seg_walk_block(const CsrView& v, const BinMeanPar
       gn = 0;
       skip(sn);
     }
-    load(sn, gn, nxt);
+    load(sn, gn, nxt, nxti);
     const int a = soff[sl], e = soff[sl + 1];
 #pragma unroll
     for (int q = 0; q < SG_GQ; ++q) {
@@ -172,14 +176,26 @@ __device__ __forceinline__ int seg_walk_block(const CsrView& v, const BinMeanPar
       const int32_t key = inr ? bin_small(m, P) : ((act && m < P.minimum) ? -1 : 0x7fffffff);
       const int32_t kn = wave_next(key, 0x7fffffff);
       bad |= (int)(owner && act && ((m != m) || key > kn));
-      if (owner && inr) f(M.p0 + k, key, kn != key, sl);
+      if (owner && inr) f(p0 + k, key, kn != key, sl, m, kInten ? curi[q] : 0.0);
     }
 #pragma unroll
-    for (int q = 0; q < SG_GQ; ++q) cur[q] = nxt[q];
+    for (int q = 0; q < SG_GQ; ++q) {
+      cur[q] = nxt[q];
+      if constexpr (kInten) curi[q] = nxti[q];
+    }
     sl = sn;
     g0 = gn;
   }
   return bad;
+}
+
+template <class F>
+__device__ __forceinline__ int seg_walk_block(const CsrView& v, const BinMeanParams& P, const SegMeta& M, int b,
+                                              const int32_t* soff, F&& f) {
+  const int nsb = min(M.n - b * SG_SB, SG_SB);  // spectra in this block
+  return walk_block<false>(v, P, M.p0, nsb, soff, [&](int64_t k, int32_t key, bool last, int s, double, double) {
+    f(k, key, last, s);
+  });
 }
 
 // the block's spectrum offsets (relative to the cluster's first peak) into LDS

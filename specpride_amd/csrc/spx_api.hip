@@ -17,6 +17,7 @@
 #include "best_score.hip"
 #include "bin_mean.hip"
 #include "bin_mean_seg.hip"
+#include "bin_mean_q.hip"
 #include "bin_mean_split.hip"
 #include "bin_mean_wide.hip"
 #include "binned_cosine.hip"
@@ -155,22 +156,31 @@ int64_t seg_arena_bytes(const spx_csr* csr, const spx_bin_params* params) {
   return std::min(b, kCap);
 }
 
+// SPX_KEPT_FOLD=0 (environment, tests only) sends every cluster the wide kernel
+// defers past the kept-bin fold, to the segmented fold
+int kept_fold_enabled() {
+  const char* e = std::getenv("SPX_KEPT_FOLD");
+  return !(e && e[0] == '0');
+}
+
 struct BinMeanWs {
   int32_t *counters, *def, *rest, *glist, *split_list, *task_cl, *tile_cl;
+  int32_t *seg_in, *q_task_cl, *q_tile_cl, *q_unit_cl;
   unsigned long long* bump;
   spx::SplitCluster* scl;
   spx::SplitRange* ranges;
   spx::SegMeta* meta;
+  spx::QMeta* qmeta;
   char *arena, *scratch;
   int64_t arena_bytes, n_task_cap, n_tile_cap;
-  int32_t range_cap;
+  int32_t range_cap, q_task_cap, q_tile_cap, q_unit_cap;
 };
 
 // The workspace layout (the size query and the launch use the same carving).
 BinMeanWs carve_bin_mean(Carver& w, const spx_csr* csr, const spx_bin_params* params) {
   const size_t C = (size_t)std::max<int64_t>(csr->n_clusters, 1);
   BinMeanWs W;
-  W.counters = w.take<int32_t>(8);
+  W.counters = w.take<int32_t>(16);
   W.bump = w.take<unsigned long long>(1);
   W.def = w.take<int32_t>(C);
   W.rest = w.take<int32_t>(C);
@@ -180,6 +190,19 @@ BinMeanWs carve_bin_mean(Carver& w, const spx_csr* csr, const spx_bin_params* pa
   W.range_cap = split_range_cap(csr);
   W.ranges = w.take<spx::SplitRange>((size_t)W.range_cap);
   W.meta = w.take<spx::SegMeta>(C);
+  // the kept-bin fold: clusters the wide kernel defers have > 128 spectra or
+  // > 4,096 peaks; tasks are blocks of >= 1 spectrum, units kept bins (each
+  // holding >= 33 contributions: the quorum of n > 128, or one of 4,096+ peaks'
+  // Q_KCAP-capped share)
+  W.seg_in = w.take<int32_t>(C);
+  W.qmeta = w.take<spx::QMeta>(C);
+  const int64_t q_bound = std::min<int64_t>(csr->n_clusters, csr->n_spectra / 129 + csr->n_peaks / 4097 + 2);
+  W.q_task_cap = (int32_t)std::min<int64_t>(csr->n_spectra + 1, INT32_MAX);
+  W.q_task_cl = w.take<int32_t>((size_t)W.q_task_cap);
+  W.q_tile_cap = (int32_t)std::min<int64_t>(q_bound * (spx::BM_WMAX / spx::Q_TILEW) + 1, INT32_MAX);
+  W.q_tile_cl = w.take<int32_t>((size_t)W.q_tile_cap);
+  W.q_unit_cap = (int32_t)std::min<int64_t>(csr->n_peaks / 32 + q_bound + 1, INT32_MAX);
+  W.q_unit_cl = w.take<int32_t>((size_t)W.q_unit_cap);
   W.n_task_cap = csr->n_spectra / spx::SG_SB + csr->n_clusters + 1;
   W.task_cl = w.take<int32_t>((size_t)W.n_task_cap);
   W.n_tile_cap = csr->n_peaks / spx::SG_TILE + csr->n_clusters + 1;
@@ -217,7 +240,7 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
   const BinMeanWs W = carve_bin_mean(w, csr, params);
-  // counters: [0] deferred past the wide kernel (segmented fold), [1] left to the
+  // counters: [0] deferred past the wide kernel (kept-bin fold), [1] left to the
   // wide kernel, [2] planned split clusters, [3] split ranges, [4] the global
   // kernel's list, [5] segmented-fold block tasks, [6] its slot tiles, [7] the
   // split path's list (clusters the segmented fold's arena could not hold)
@@ -229,6 +252,10 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   int32_t* n_tasks = W.counters + 5;
   int32_t* n_tiles = W.counters + 6;
   int32_t* n_split = W.counters + 7;
+  int32_t* n_seg_in = W.counters + 8;  // [8] the segmented fold's list (what the kept-bin fold passes on)
+  int32_t* n_qtasks = W.counters + 9;  // [9..11] kept-bin fold block tasks, count tiles, fold units
+  int32_t* n_qtiles = W.counters + 10;
+  int32_t* n_qunits = W.counters + 11;
 
   spx::BinMeanParams P;
   P.minimum = params->minimum;
@@ -253,29 +280,53 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   hipLaunchKernelGGL(spx::bin_mean_wide_kernel, gcl, dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out, status,
                      W.rest, n_rest, W.def, n_def, W.glist, n_glist);
   if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
-  // segmented fold of the clusters past the wide kernel
+  const dim3 bsg(spx::SG_BLOCK);
+  // kept-bin fold of the clusters past the wide kernel (the quorum applies)
+  const dim3 gqt((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.q_task_cap, 8192)));
+  hipLaunchKernelGGL(spx::bin_mean_q_setup_kernel, gcl, bsg, 0, s, V, P, O, prec_out, charge_out, status, W.def,
+                     n_def, W.qmeta, W.arena, W.bump, W.arena_bytes, W.q_task_cl, n_qtasks, W.q_task_cap, W.q_tile_cl,
+                     n_qtiles, W.q_tile_cap, kept_fold_enabled());
+  if (int rc = check_launch("bin_mean_q_setup_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_q_tally_kernel, gqt, bsg, 0, s, V, P, W.qmeta, W.arena, W.q_task_cl, n_qtasks,
+                     W.q_task_cap);
+  if (int rc = check_launch("bin_mean_q_tally_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_q_count_kernel, dim3((unsigned)std::max(1, std::min(W.q_tile_cap, 8192))), bsg, 0,
+                     s, W.qmeta, W.arena, W.q_tile_cl, n_qtiles, W.q_tile_cap);
+  if (int rc = check_launch("bin_mean_q_count_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_q_plan_kernel, gcl, bsg, 0, s, n_def, W.qmeta, W.arena, W.bump, W.arena_bytes,
+                     W.q_unit_cl, n_qunits, W.q_unit_cap);
+  if (int rc = check_launch("bin_mean_q_plan_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_q_place_kernel, gqt, bsg, 0, s, V, P, W.qmeta, W.arena, W.q_task_cl, n_qtasks,
+                     W.q_task_cap);
+  if (int rc = check_launch("bin_mean_q_place_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_q_fold_kernel, dim3((unsigned)std::max(1, std::min(W.q_unit_cap / 4 + 1, 4096))),
+                     bsg, 0, s, W.qmeta, W.arena, W.q_unit_cl, n_qunits, W.q_unit_cap);
+  if (int rc = check_launch("bin_mean_q_fold_kernel")) return rc;
+  hipLaunchKernelGGL(spx::bin_mean_q_emit_kernel, gcl, bsg, 0, s, V, O, prec_out, charge_out, status, n_def, W.qmeta,
+                     W.arena, W.seg_in, n_seg_in, W.glist, n_glist);
+  if (int rc = check_launch("bin_mean_q_emit_kernel")) return rc;
+  // segmented fold of what the kept-bin fold passes on (no quorum, no room)
   const dim3 gtask((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.n_task_cap, 8192)));
   const dim3 gtile((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.n_tile_cap, 8192)));
-  const dim3 bsg(spx::SG_BLOCK);
-  hipLaunchKernelGGL(spx::bin_mean_seg_setup_kernel, gcl, bsg, 0, s, V, P, O, prec_out, charge_out, status, W.def,
-                     n_def, W.meta, W.arena, W.bump, W.arena_bytes, W.task_cl, n_tasks);
+  hipLaunchKernelGGL(spx::bin_mean_seg_setup_kernel, gcl, bsg, 0, s, V, P, O, prec_out, charge_out, status, W.seg_in,
+                     n_seg_in, W.meta, W.arena, W.bump, W.arena_bytes, W.task_cl, n_tasks);
   if (int rc = check_launch("bin_mean_seg_setup_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_seg_occupy_kernel, gtask, bsg, 0, s, V, P, W.meta, W.arena, W.task_cl, n_tasks);
   if (int rc = check_launch("bin_mean_seg_occupy_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_seg_prefix_kernel, gcl, bsg, 0, s, V, P, O, prec_out, charge_out, status, n_def,
+  hipLaunchKernelGGL(spx::bin_mean_seg_prefix_kernel, gcl, bsg, 0, s, V, P, O, prec_out, charge_out, status, n_seg_in,
                      W.meta, W.arena, W.bump, W.arena_bytes, W.tile_cl, n_tiles);
   if (int rc = check_launch("bin_mean_seg_prefix_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_seg_mask_kernel, gtask, bsg, 0, s, V, P, W.meta, W.arena, W.task_cl, n_tasks);
   if (int rc = check_launch("bin_mean_seg_mask_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_seg_count_kernel, gtile, bsg, 0, s, W.meta, W.arena, W.tile_cl, n_tiles);
   if (int rc = check_launch("bin_mean_seg_count_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_seg_scan_kernel, gcl, bsg, 0, s, n_def, W.meta, W.arena);
+  hipLaunchKernelGGL(spx::bin_mean_seg_scan_kernel, gcl, bsg, 0, s, n_seg_in, W.meta, W.arena);
   if (int rc = check_launch("bin_mean_seg_scan_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_seg_place_kernel, gtask, bsg, 0, s, V, P, W.meta, W.arena, W.task_cl, n_tasks);
   if (int rc = check_launch("bin_mean_seg_place_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_seg_fold_kernel, gtile, bsg, 0, s, P, W.meta, W.arena, W.tile_cl, n_tiles);
   if (int rc = check_launch("bin_mean_seg_fold_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_seg_emit_kernel, gcl, bsg, 0, s, V, O, prec_out, charge_out, status, n_def, W.meta,
+  hipLaunchKernelGGL(spx::bin_mean_seg_emit_kernel, gcl, bsg, 0, s, V, O, prec_out, charge_out, status, n_seg_in, W.meta,
                      W.arena, W.split_list, n_split, W.glist, n_glist);
   if (int rc = check_launch("bin_mean_seg_emit_kernel")) return rc;
   // bin-range split path for what the arena could not hold, then the global kernel

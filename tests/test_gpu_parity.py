@@ -485,8 +485,17 @@ def test_bin_mean_split_path(gpu):
     # global kernel and their reserved records are dropped, never read unwritten
     import os
 
-    # the segmented fold's arena (SPX_SEG_ARENA): none (every deferred cluster takes
-    # the bin-range split path), room for part of the clusters
+    # no quorum: nothing for the kept-bin fold, the segmented fold takes every
+    # deferred cluster
+    assert_bin_mean_equal(_bin_mean(csr, apply_peak_quorum=False), c_oracle.bin_mean(csr, apply_peak_quorum=False))
+    # the segmented fold with the quorum (SPX_KEPT_FOLD=0 turns the kept-bin fold off)
+    os.environ["SPX_KEPT_FOLD"] = "0"
+    try:
+        assert_bin_mean_equal(_bin_mean(csr), want)
+    finally:
+        del os.environ["SPX_KEPT_FOLD"]
+    # the arena (SPX_SEG_ARENA): none (every deferred cluster takes the bin-range
+    # split path), room for part of the clusters
     for arena in ("0", "400000"):
         os.environ["SPX_SEG_ARENA"] = arena
         try:
@@ -499,3 +508,40 @@ def test_bin_mean_split_path(gpu):
                     del os.environ["SPX_SPLIT_RANGE_CAP"]
         finally:
             del os.environ["SPX_SEG_ARENA"]
+
+
+def test_bin_mean_kept_fold(gpu):
+    """The kept-bin fold (bin_mean_q.hip) on the clusters the wide kernel defers:
+    n = 129 .. 2,500 (blocks of 64 spectra, the last one partial), 700-peak spectra
+    (blocks of < 64 spectra), more than Q_KCAP = 2,048 kept bins (-> the segmented
+    fold), a NaN intensity in a kept bin (that bin dropped), every spectrum empty,
+    nothing in range, peaks on the window's ends, a mixed-charge one, an unsorted
+    one (-> the global kernel); bit-exact against the C oracle, with and without
+    the quorum."""
+    rng = np.random.default_rng(17)
+    parts = [make_clusters_np(1, seed=60 + k, sizes=np.array([n])) for k, n in enumerate((129, 192, 257, 700, 2500))]
+    parts.append(make_clusters_np(2, seed=70, sizes=np.array([140, 200]), n_template=700))
+
+    def spec(mz, it=None):
+        mz = np.asarray(mz, np.float64)
+        return {"m/z array": mz, "intensity array": rng.lognormal(4, 1, len(mz)) if it is None else it,
+                "precursor mz": 500.0, "precursor charge": 2}
+
+    wide = np.sort(rng.uniform(100, 2000, 2300))
+    nan_it = rng.lognormal(4, 1, 50)
+    nan_it[10] = np.nan
+    base = np.sort(rng.uniform(300, 900, 50))
+    ends = np.array([100.0, 100.01, 1999.99, 1999.999])
+    special = SpectraCSR.from_clusters([
+        [spec(wide) for _ in range(130)],                                  # K = 2,300 > Q_KCAP
+        [spec(base, nan_it if k == 3 else None) for k in range(150)],      # NaN intensity in a kept bin
+        [spec(np.zeros(0)) for _ in range(131)],                           # every spectrum empty
+        [spec(np.array([50.0, 99.0, 2000.0, 3000.0])) for _ in range(135)],  # nothing in range
+        [spec(ends) for _ in range(133)],                                  # the window's ends
+    ])
+    mixed = make_clusters_np(1, seed=71, sizes=np.array([300]))
+    mixed.charge[5] = mixed.charge[0] + 1
+    uns = _shuffled(make_clusters_np(1, seed=72, sizes=np.array([180])), seed=9)
+    csr = _concat(make_clusters_np(20, seed=73), *parts, special, mixed, uns, make_clusters_np(20, seed=74))
+    for q in (True, False):
+        assert_bin_mean_equal(_bin_mean(csr, apply_peak_quorum=q), c_oracle.bin_mean(csr, apply_peak_quorum=q))
