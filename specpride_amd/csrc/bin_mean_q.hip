@@ -45,16 +45,25 @@ namespace spx {
 constexpr int Q_LCAP = SPX_Q_LCAP;  // block-local occupied bins (u8 counts packed four to an LDS word)
 constexpr int Q_KCAP = 2048;        // kept bins per cluster (place's LDS presence masks)
 constexpr int Q_TILEW = 16;         // bitmap words (1,024 bins) per count workgroup
+constexpr int QF_LONG = 1024;       // clusters of at least this many spectra fold first (the longest chains)
 enum : int32_t { kQOk = 0, kQBad = 1, kQNoFit = 2, kQDone = 3 };
 
 struct QMeta {
   int64_t c, p0;
   int32_t n, nb, sb, state;      // spectra, blocks, spectra per block, kQ*
   int32_t lo_w, nw, task0, tile0;  // window words [lo_w, lo_w + nw); first block task, first count tile
-  int32_t unit0, K, pad0, pad1;  // first fold unit (wave), kept bins
+  int32_t unit0, K, G, pad;      // first fold unit, kept bins, 64-bin groups of them (the fold units)
   int64_t rows, kbits, kpre;     // arena offsets: rows[b][bin] u8, kept bitmap (nw u64), its prefix (nw u32)
-  int64_t vals, pbits, res;      // V[k][s] (m/z, intensity), P[k][b] u64, res[k] (m/z mean, intensity mean)
+  int64_t vals, pres, res;       // V[s][k] (m/z, intensity; rows of 64 G), presence P[g][s] u64, res[k]
+  double prec;                   // np.mean of the precursors (binning.py:224)
 };
+
+// OR over the wave, every lane gets it
+__device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long x) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) x |= __shfl_xor(x, o, kWave);
+  return x;
+}
 
 __device__ __forceinline__ unsigned long long uniform_u64(unsigned long long x) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
@@ -79,6 +88,7 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_setup_kernel(
   __shared__ int votes[2 * (SG_BLOCK / kWave)];
   __shared__ int red[3];
   __shared__ QMeta sM;
+  __shared__ PwSmem pws;
   const int tid = threadIdx.x;
   const int32_t nl = *n_list;
   for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
@@ -87,7 +97,13 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_setup_kernel(
     const int n = (int)(s1 - s0);
     const int32_t z0 = v.charge[s0];
     int mixed = 0;
-    for (int64_t s = s0 + 1 + tid; s < s1; s += SG_BLOCK) mixed |= v.charge[s] != z0;
+    for (int64_t r0 = s0 + 1 + tid; r0 < s1; r0 += 8 * SG_BLOCK) {
+      int32_t z[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) z[u] = v.charge[min(r0 + u * SG_BLOCK, s1 - 1)];  // (clamped: a repeat)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) mixed |= z[u] != z0;
+    }
     if (tid == 0) { red[0] = 0; red[1] = 0x7fffffff; red[2] = -1; }
     const bool mix = block_any<SG_BLOCK, false>(mixed, votes, 0);
     QMeta M = {};
@@ -106,21 +122,39 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_setup_kernel(
       __syncthreads();
       continue;
     }
-    // longest spectrum and the bin window (first / last peak of each spectrum)
+    // longest spectrum and the bin window (first / last peak of each spectrum),
+    // QS_U spectra per thread per round with their loads issued together
+    constexpr int QS_U = 4;
     int maxlen = 0, lok = 0x7fffffff, hik = -1;
-    for (int64_t s = s0 + tid; s < s1; s += SG_BLOCK) {
-      const int64_t a = v.spec_off[s], e = v.spec_off[s + 1];
-      if (e > a) {
-        maxlen = max(maxlen, (int)min<int64_t>(e - a, 0x7fffffff));
-        lok = min(lok, q_window_key(v.mz[a], P));
-        hik = max(hik, q_window_key(v.mz[e - 1], P));
+    for (int64_t r0 = s0 + tid; r0 < s1; r0 += QS_U * SG_BLOCK) {
+      int64_t a[QS_U], e[QS_U];
+#pragma unroll
+      for (int u = 0; u < QS_U; ++u) {
+        const int64_t sp = min(r0 + u * SG_BLOCK, s1 - 1);
+        a[u] = v.spec_off[sp];
+        e[u] = v.spec_off[sp + 1];
+      }
+      double mf[QS_U], ml[QS_U];
+#pragma unroll
+      for (int u = 0; u < QS_U; ++u) {
+        mf[u] = e[u] > a[u] ? v.mz[a[u]] : 0.0;
+        ml[u] = e[u] > a[u] ? v.mz[e[u] - 1] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < QS_U; ++u) {
+        if (r0 + u * SG_BLOCK < s1 && e[u] > a[u]) {
+          maxlen = max(maxlen, (int)min<int64_t>(e[u] - a[u], 0x7fffffff));
+          lok = min(lok, q_window_key(mf[u], P));
+          hik = max(hik, q_window_key(ml[u], P));
+        }
       }
     }
     atomicMax(&red[0], maxlen);
     atomicMin(&red[1], lok);
     atomicMax(&red[2], hik);
-    __syncthreads();
+    const double pm = seg_pw_mean(v.prec_mz + s0, n, pws);  // (barriers inside)
     if (tid == 0) {
+      M.prec = pm;
       const int64_t P_c = v.spec_off[s1] - M.p0;
       maxlen = red[0];
       lok = red[1];
@@ -131,7 +165,7 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_setup_kernel(
       M.lo_w = lok >> 6;
       M.nw = (hik >> 6) - M.lo_w + 1;
       const bool fits = enabled && P.apply_quorum && P.n_words <= BM_WMAX && n <= 65535 && maxlen <= Q_LCAP &&
-                        P_c < (int64_t(1) << 31);
+                        P_c < (int64_t(1) << 28);
       const int64_t W = (int64_t)M.nw * 64;
       const int64_t bytes = seg_align((int64_t)M.nb * W) + seg_align((int64_t)M.nw * 8) + seg_align((int64_t)M.nw * 4);
       const int64_t base = fits ? seg_alloc(bump, bytes, cap) : -1;
@@ -238,32 +272,58 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_tally_kernel(CsrView v, B
   }
 }
 
-// count: one workgroup per (cluster, Q_TILEW words) tile; wave per bitmap word,
-// lane per bin: the column sum over the blocks' rows against the quorum
+// bit i of a 16-bit value -> bit 4 i
+__device__ __forceinline__ unsigned long long spread4(uint32_t x) {
+  unsigned long long y = x & 0xFFFFu;
+  y = (y | (y << 24)) & 0x000000FF000000FFull;
+  y = (y | (y << 12)) & 0x000F000F000F000Full;
+  y = (y | (y << 6)) & 0x0303030303030303ull;
+  y = (y | (y << 3)) & 0x1111111111111111ull;
+  return y;
+}
+
+// count: one workgroup per (cluster, Q_TILEW words) tile; a wave per 4 bitmap
+// words, 4 bins per lane (u32 row loads): the column sums over the blocks' rows
+// against the quorum, kept words assembled from the four ballots
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_count_kernel(const QMeta* meta, char* arena,
                                                                     const int32_t* tile_cl, const int32_t* n_tiles,
                                                                     int32_t tile_cap) {
   constexpr int U = 8;  // row loads in flight per lane
+  static_assert(Q_TILEW == 4 * (SG_BLOCK / kWave), "a wave per 4 words");
   const int lane = lane_id(), wid = wave_id();
   const int32_t nt = min(*n_tiles, tile_cap);
   for (int32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     const int i = tile_cl[t];
     const QMeta M = meta[i];
     if (M.state != kQOk) continue;
-    const int64_t W = (int64_t)M.nw * 64;
+    const int w0 = (t - M.tile0) * Q_TILEW + 4 * wid;  // this wave's first word
+    if (w0 >= M.nw) continue;                          // uniform per wave
+    const int64_t W4 = (int64_t)M.nw * 16;              // row length in u32
     const uint32_t quorum = (uint32_t)((double)M.n * 0.25) + 1u;  // binning.py:181-183
-    for (int w = (t - M.tile0) * Q_TILEW + wid; w < min(M.nw, (t - M.tile0 + 1) * Q_TILEW); w += SG_BLOCK / kWave) {
-      const uint8_t* col = reinterpret_cast<const uint8_t*>(arena + M.rows) + w * 64 + lane;
-      uint32_t tot = 0;
-      for (int b0 = 0; b0 < M.nb; b0 += U) {
-        uint32_t x[U];
+    const int q4 = w0 * 16 + lane;                      // this lane's u32 (bins 4 q4 .. 4 q4 + 3)
+    const bool inw = q4 < W4;
+    const uint32_t* col = reinterpret_cast<const uint32_t*>(arena + M.rows) + (inw ? q4 : 0);
+    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    for (int b0 = 0; b0 < M.nb; b0 += U) {
+      uint32_t x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = b0 + u < M.nb ? col[(int64_t)(b0 + u) * W] : 0u;
+      for (int u = 0; u < U; ++u) x[u] = col[(int64_t)min(b0 + u, M.nb - 1) * W4];
 #pragma unroll
-        for (int u = 0; u < U; ++u) tot += x[u];
+      for (int u = 0; u < U; ++u) {
+        const uint32_t y = b0 + u < M.nb ? x[u] : 0u;
+        t0 += y & 0xFFu;
+        t1 += (y >> 8) & 0xFFu;
+        t2 += (y >> 16) & 0xFFu;
+        t3 += y >> 24;
       }
-      const unsigned long long kept = __ballot(tot >= quorum);
-      if (lane == 0) reinterpret_cast<unsigned long long*>(arena + M.kbits)[w] = kept;
+    }
+    const unsigned long long k0 = __ballot(inw && t0 >= quorum), k1 = __ballot(inw && t1 >= quorum);
+    const unsigned long long k2 = __ballot(inw && t2 >= quorum), k3 = __ballot(inw && t3 >= quorum);
+    if (lane < 4 && w0 + lane < M.nw) {  // word w0 + lane: lanes 16 lane .. 16 lane + 15
+      const int sh = 16 * lane;
+      reinterpret_cast<unsigned long long*>(arena + M.kbits)[w0 + lane] =
+          spread4((uint32_t)(k0 >> sh)) | (spread4((uint32_t)(k1 >> sh)) << 1) |
+          (spread4((uint32_t)(k2 >> sh)) << 2) | (spread4((uint32_t)(k3 >> sh)) << 3);
     }
   }
 }
@@ -285,19 +345,23 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_plan_kernel(const int32_t
     const int K = bitmap_prefix<SG_BLOCK, uint32_t>(kb, kp, M.nw, tmp);
     if (tid == 0) {
       M.K = K;
+      M.G = (K + 63) / 64;
       if (K > Q_KCAP) {
         M.state = kQNoFit;
       } else if (K > 0) {
-        const int64_t bytes = seg_align((int64_t)K * M.n * 16) + seg_align((int64_t)K * M.nb * 8) +
+        const int64_t Kp = (int64_t)M.G * 64;
+        const int64_t bytes = seg_align((int64_t)M.n * Kp * 16) + seg_align((int64_t)M.G * M.n * 8) +
                               seg_align((int64_t)K * 16);
         const int64_t base = seg_alloc(bump, bytes, cap);
-        M.unit0 = base >= 0 ? atomicAdd(n_units, K) : 0;
-        if (base < 0 || M.unit0 + K > unit_cap) {
+        // long chains first (the front half of unit_cl), the rest from the back
+        const bool lng = M.n >= QF_LONG;
+        M.unit0 = base >= 0 ? atomicAdd(&n_units[lng ? 0 : 1], M.G) : 0;
+        if (base < 0 || M.unit0 + M.G > (lng ? unit_cap / 2 : unit_cap - unit_cap / 2)) {
           M.state = kQNoFit;
         } else {
           M.vals = base;
-          M.pbits = M.vals + seg_align((int64_t)K * M.n * 16);
-          M.res = M.pbits + seg_align((int64_t)K * M.nb * 8);
+          M.pres = M.vals + seg_align((int64_t)M.n * Kp * 16);
+          M.res = M.pres + seg_align((int64_t)M.G * M.n * 8);
         }
       }
       sM = M;
@@ -305,7 +369,7 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_plan_kernel(const int32_t
     __syncthreads();
     M = sM;
     if (M.state == kQOk)
-      for (int k = tid; k < M.K; k += SG_BLOCK) unit_cl[M.unit0 + k] = i;
+      for (int g = tid; g < M.G; g += SG_BLOCK) unit_cl[M.n >= QF_LONG ? M.unit0 + g : unit_cap - 1 - (M.unit0 + g)] = i;
     if (tid == 0) meta[i] = M;
     __syncthreads();
   }
@@ -314,11 +378,12 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_plan_kernel(const int32_t
 struct QPlaceSmem {
   unsigned long long kb[BM_WMAX];
   uint16_t kp[BM_WMAX];
-  unsigned long long lmask[Q_KCAP];  // bit s: spectrum s of the block has kept bin k
+  unsigned long long lp[SG_SB * (Q_KCAP / 64)];  // presence of spectrum s in group g: lp[s * G + g]
   int32_t soff[SG_SB + 1];
 };
 
-// place: one workgroup per (cluster, block) task -- V[k][s] and P[k][b]
+// place: one workgroup per (cluster, block) task -- V[s][k] (a spectrum's kept
+// peaks are consecutive k: contiguous stores) and P[g][s]
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_place_kernel(CsrView v, BinMeanParams P, const QMeta* meta,
                                                                     char* arena, const int32_t* task_cl,
                                                                     const int32_t* n_tasks, int32_t task_cap) {
@@ -331,90 +396,203 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_place_kernel(CsrView v, B
     if (M.state != kQOk || M.K == 0) continue;  // uniform
     const int b = t - M.task0;
     const int32_t base = M.lo_w * 64, W = M.nw * 64;
+    const int64_t Kp = (int64_t)M.G * 64;
     const unsigned long long* kb = reinterpret_cast<const unsigned long long*>(arena + M.kbits);
     const uint32_t* kp = reinterpret_cast<const uint32_t*>(arena + M.kpre);
     for (int w = tid; w < M.nw; w += SG_BLOCK) {
       L.kb[w] = kb[w];
       L.kp[w] = (uint16_t)kp[w];  // K <= Q_KCAP
     }
-    for (int k = tid; k < M.K; k += SG_BLOCK) L.lmask[k] = 0ull;
     const int nsb = q_block_offsets(v, M, b, L.soff);
+    for (int e = tid; e < nsb * M.G; e += SG_BLOCK) L.lp[e] = 0ull;
     __syncthreads();
     double2* V = reinterpret_cast<double2*>(arena + M.vals);
     const int sb0 = b * M.sb;
-    walk_block<true>(v, P, M.p0, nsb, L.soff, [&](int64_t, int32_t key, bool last, int s, double m, double it) {
-      const uint32_t r = (uint32_t)(key - base);
-      if (!last || r >= (uint32_t)W) return;
-      const unsigned long long word = L.kb[r >> 6];
-      if (!((word >> (r & 63)) & 1ull)) return;  // a bin under the quorum
-      const int k = (int)L.kp[r >> 6] + __popcll(word & ((1ull << (r & 63)) - 1ull));
-      V[(int64_t)k * M.n + sb0 + s] = make_double2(m, it);
-      atomicOr(&L.lmask[k], 1ull << s);
-    });
+    // a chunk's kept peaks are ascending kept ranks of one spectrum, mostly in one
+    // 64-bin group: their presence bits are ORed across the wave per group and
+    // merged by one lane (only this wave writes spectrum s's words) -- 63 LDS
+    // atomics on one word would serialise
+    int my_g = -1;
+    unsigned long long my_bit = 0ull;
+    walk_block<true>(
+        v, P, M.p0, nsb, L.soff,
+        [&](int64_t, int32_t key, bool last, int s, double m, double it) {
+          const uint32_t r = (uint32_t)(key - base);
+          if (!last || r >= (uint32_t)W) return;
+          const unsigned long long word = L.kb[r >> 6];
+          if (!((word >> (r & 63)) & 1ull)) return;  // a bin under the quorum
+          const int k = (int)L.kp[r >> 6] + __popcll(word & ((1ull << (r & 63)) - 1ull));
+          V[(int64_t)(sb0 + s) * Kp + k] = make_double2(m, it);
+          my_g = k >> 6;
+          my_bit = 1ull << (k & 63);
+        },
+        [&](int s) {
+          unsigned long long pending = __ballot(my_g >= 0);
+          while (pending) {  // uniform
+            const int l0 = __builtin_ctzll(pending);
+            const int g = __builtin_amdgcn_readlane(my_g, l0);
+            const bool sel = my_g == g;
+            const unsigned long long w = wave_or_u64(sel ? my_bit : 0ull);
+            if (lane_id() == l0) L.lp[s * M.G + g] |= w;
+            pending &= ~__ballot(sel);
+          }
+          my_g = -1;
+        });
     lds_barrier();
-    unsigned long long* Pb = reinterpret_cast<unsigned long long*>(arena + M.pbits);
-    for (int k = tid; k < M.K; k += SG_BLOCK) Pb[(int64_t)k * M.nb + b] = L.lmask[k];
+    unsigned long long* Pg = reinterpret_cast<unsigned long long*>(arena + M.pres);
+    for (int e = tid; e < nsb * M.G; e += SG_BLOCK) {
+      const int g = e / nsb, s = e - g * nsb;  // consecutive threads: consecutive spectra of one group
+      Pg[(int64_t)g * M.n + sb0 + s] = L.lp[s * M.G + g];
+    }
     __syncthreads();  // the LDS is reused by the next task
   }
 }
 
-// fold: one wave per kept bin (grid-stride over the units) -- block by block, the
-// lanes load the block's sb entries of V[k] at once (the next block's while this
-// one is folded) and the present ones are folded in spectrum order by broadcast
-__global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_fold_kernel(const QMeta* meta, char* arena,
-                                                                   const int32_t* unit_cl, const int32_t* n_units,
-                                                                   int32_t unit_cap) {
-  constexpr int NW = SG_BLOCK / kWave;
-  const int lane = lane_id();
-  const int32_t nu = min(*n_units, unit_cap);
-  for (int32_t u = blockIdx.x * NW + wave_id(); u < nu; u += gridDim.x * NW) {  // uniform per wave
-    const int i = unit_cl[u];
+// fold: one workgroup per 64-bin group of a cluster's kept bins (grid-stride over
+// the units).  Lane j of wave 0 owns kept bin 64 g + j and runs its
+// f32(f64(acc) + v) chain over the spectra in order (binning.py:198-199);
+// waves 1..4 stream the rows V[s][64 g .. 64 g + 63] (1 KB each) and the presence
+// words into an LDS ring with LDS-DMA loads, QF_NS - 1 stages of QF_TS spectra
+// ahead, so the chain -- as long as the cluster -- never waits on HBM latency.
+#ifndef SPX_QF_TS
+#define SPX_QF_TS 16
+#endif
+#ifndef SPX_QF_NS
+#define SPX_QF_NS 8
+#endif
+#ifndef SPX_QF_DIAG
+#define SPX_QF_DIAG 0  // A/B diagnostics only: 1 = no fold arithmetic, 2 = no loads (wrong results)
+#endif
+constexpr int QF_TS = SPX_QF_TS;             // spectra per stage
+constexpr int QF_NS = SPX_QF_NS;             // ring stages (QF_NS x QF_TS KB of rows)
+constexpr int QF_LOADERS = 4;                // loader waves
+constexpr int QF_RPW = QF_TS / QF_LOADERS;   // rows per loader wave per stage
+constexpr int QF_BLOCK = (QF_LOADERS + 1) * kWave;
+static_assert(QF_TS % QF_LOADERS == 0 && 2 * QF_TS <= kWave, "rows split evenly; presence: 2 x u32 per spectrum");
+
+struct QFoldSmem {
+  double2 v[QF_NS][QF_TS][kWave];
+  uint32_t p[QF_NS][kWave];  // presence words of the stage's spectra (lanes 0..2 QF_TS - 1)
+};
+
+__device__ __forceinline__ void q_glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+__device__ __forceinline__ void q_glds4(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left open)
+template <int N>
+__device__ __forceinline__ void q_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | 0x0F70);
+}
+// at most `stages` stages of G loads each still in flight (past what vmcnt can
+// count: wait for all)
+template <int G, int K = 0>
+__device__ __forceinline__ void q_wait_stages(int stages) {
+  if constexpr (K * G < 64 && K <= 16) {
+    if (stages == K) q_wait_vm<K * G>();
+    else q_wait_stages<G, K + 1>(stages);
+  } else {
+    q_wait_vm<0>();
+  }
+}
+
+__global__ __launch_bounds__(QF_BLOCK, 1) void bin_mean_q_fold_kernel(const QMeta* meta, char* arena,
+                                                                      const int32_t* unit_cl, const int32_t* n_units,
+                                                                      int32_t unit_cap) {
+  __shared__ QFoldSmem L;
+  const int lane = lane_id(), wid = wave_id();
+  // the long-chain units first (front of unit_cl), then the others (from the back)
+  const int32_t n_long = min(n_units[0], unit_cap / 2);
+  const int32_t nu = n_long + min(n_units[1], unit_cap - unit_cap / 2);
+  for (int32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+    const int32_t j = u < n_long ? u : u - n_long;
+    const int i = unit_cl[u < n_long ? u : unit_cap - 1 - j];
     const QMeta M = meta[i];
-    const int k = u - M.unit0;
-    const double2* Vk = reinterpret_cast<const double2*>(arena + M.vals) + (int64_t)k * M.n;
-    const unsigned long long* Pk = reinterpret_cast<const unsigned long long*>(arena + M.pbits) + (int64_t)k * M.nb;
-    const int last_s = M.n - 1;
-    double2 x = Vk[min(lane, last_s)];
-    unsigned long long mask = Pk[0];
+    const int g = j - M.unit0;
+    const int n = M.n;
+    const int64_t Kp = (int64_t)M.G * 64;
+    const int nst = (n + QF_TS - 1) / QF_TS;
+    const double2* Vg = reinterpret_cast<const double2*>(arena + M.vals) + (int64_t)g * 64 + lane;
+    const uint32_t* Pg = reinterpret_cast<const uint32_t*>(arena + M.pres) + (int64_t)g * n * 2;
+    // loader wave w (1..4) issues rows w-1, w-1+4, ... of a stage; wave 1 also the
+    // presence words (2 x u32 per spectrum: lanes 0..31; 32..63 repeat them)
+    auto issue = [&](int st) __attribute__((always_inline)) {
+      const int slot = st % QF_NS;
+      const int sbase = st * QF_TS;
+#pragma unroll
+      for (int r = 0; r < QF_RPW; ++r) {
+        const int row = (wid - 1) + r * QF_LOADERS;
+        const int sp = min(sbase + row, n - 1);  // rows past the cluster: never folded
+        q_glds16(Vg + (int64_t)sp * Kp, &L.v[slot][row][0]);
+      }
+      if (wid == 1) {
+        const int sp = min(sbase + ((lane & 31) >> 1), n - 1);
+        q_glds4(Pg + (int64_t)sp * 2 + (lane & 1), &L.p[slot][0]);
+      }
+    };
+    if (wid > 0 && SPX_QF_DIAG != 2)
+      for (int st = 0; st < min(QF_NS - 1, nst); ++st) issue(st);
     float si = 0.0f, sm = 0.0f;
     uint32_t cnt = 0;
-    for (int b = 0; b < M.nb; ++b) {
-      const int bn = min(b + 1, M.nb - 1);
-      const double2 xn = Vk[min(bn * M.sb + lane, last_s)];  // (entries of absent spectra are never used)
-      const unsigned long long mn = Pk[bn];
-      unsigned long long m = uniform_u64(mask);
-      cnt += (uint32_t)__popcll(m);
-      while (m) {
-        const int j = __builtin_ctzll(m);
-        m &= m - 1ull;
-        const double xi = readlane_f64(x.y, j), xm = readlane_f64(x.x, j);
-        si = (float)((double)si + xi);
-        sm = (float)((double)sm + xm);
+    for (int t = 0; t < nst; ++t) {  // uniform
+      if (wid > 0) {  // stage t landed: stages t+1 .. t+NS-2 may stay in flight
+        const int ahead = min(QF_NS - 2, nst - 1 - t);
+        if (wid == 1) q_wait_stages<QF_RPW + 1>(ahead);
+        else q_wait_stages<QF_RPW>(ahead);
       }
-      x = xn;
-      mask = mn;
+      __builtin_amdgcn_s_barrier();
+      if (wid > 0) {
+        if (t + QF_NS - 1 < nst && SPX_QF_DIAG != 2) issue(t + QF_NS - 1);  // into the slot folded in iteration t - 1
+      } else if (SPX_QF_DIAG != 1) {
+        const int slot = t % QF_NS;
+        const int steps = min(QF_TS, n - t * QF_TS);  // uniform
+        // the stage's words and entries read first (stale ones past `steps` are
+        // never used), then the chain with selects: no branch between LDS reads
+        uint32_t pl[QF_TS], ph[QF_TS];
+        double2 x[QF_TS];
+#pragma unroll
+        for (int j = 0; j < QF_TS; ++j) {
+          pl[j] = L.p[slot][2 * j];
+          ph[j] = L.p[slot][2 * j + 1];
+          x[j] = L.v[slot][j][lane];
+        }
+#pragma unroll
+        for (int j = 0; j < QF_TS; ++j) {
+          const uint32_t w = lane < 32 ? pl[j] : ph[j];
+          const bool pr = j < steps && ((w >> (lane & 31)) & 1u);
+          const float ni = (float)((double)si + x[j].y);
+          const float nm = (float)((double)sm + x[j].x);
+          si = pr ? ni : si;
+          sm = pr ? nm : sm;
+          cnt += pr ? 1u : 0u;
+        }
+      }
     }
-    if (lane == 0) {
+    if (wid == 0 && g * 64 + lane < M.K) {
       const double cn = (double)cnt;  // >= the quorum
-      reinterpret_cast<double2*>(arena + M.res)[k] =
+      reinterpret_cast<double2*>(arena + M.res)[g * 64 + lane] =
           make_double2(sm == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)sm / cn, (double)si / cn);
     }
+    __syncthreads();  // the ring is reused by the next unit (every load has landed: vmcnt(0) above)
   }
 }
 
 // emit: one workgroup per cluster -- kept bins whose intensity mean is not NaN,
-// in bin order (binning.py:209-222); count, charge, np.mean (:224).  Clusters
-// that did not fit go to the segmented fold's list, unsorted / NaN ones to the
-// global kernel's.
+// in bin order (binning.py:209-222); count, charge, np.mean (:224, from setup).
+// Clusters that did not fit go to the segmented fold's list, unsorted / NaN ones
+// to the global kernel's.
 __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_emit_kernel(CsrView v, PeaksOut out, double* prec_out,
                                                                    int32_t* charge_out, int32_t* status,
                                                                    const int32_t* n_list, const QMeta* meta,
                                                                    char* arena, int32_t* seg_list, int32_t* n_seg,
                                                                    int32_t* glist, int32_t* n_glist) {
   __shared__ uint32_t tmp[SG_BLOCK / kWave + 1];
-  __shared__ int64_t leaf_lo[SG_MAXLEAF], leaf_len[SG_MAXLEAF];
-  __shared__ double leaf_sum[SG_MAXLEAF];
-  __shared__ int nleaf;
   constexpr int PER = Q_KCAP / SG_BLOCK;
   const int tid = threadIdx.x;
   const int32_t nl = *n_list;
@@ -446,15 +624,12 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_emit_kernel(CsrView v, Pe
         ++o;
       }
     }
-    const int64_t s0 = v.cluster_off[M.c];
-    const double pm = seg_pw_mean(v.prec_mz + s0, M.n, leaf_lo, leaf_len, leaf_sum, &nleaf);  // np.mean (binning.py:224)
     if (tid == 0) {
       out.count[M.c] = total;
-      charge_out[M.c] = v.charge[s0];
-      prec_out[M.c] = pm;
+      charge_out[M.c] = v.charge[v.cluster_off[M.c]];
+      prec_out[M.c] = M.prec;
       status[M.c] = kOk;
     }
-    __syncthreads();
   }
 }
 

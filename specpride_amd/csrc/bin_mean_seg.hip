@@ -98,7 +98,7 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_setup_kernel(
     }
     const int64_t P_c = v.spec_off[s1] - M.p0;
     // the tables' limits: the LDS bitmap of a block, u16 block offsets, u32 segments
-    const bool fits = P.n_words <= BM_WMAX && n <= 65535 && P_c < (int64_t(1) << 31);
+    const bool fits = P.n_words <= BM_WMAX && n <= 65535 && P_c < (int64_t(1) << 28);
     if (tid == 0) {
       s_bm = fits ? seg_alloc(bump, (int64_t)P.n_words * 12, cap) : -1;
       s_task0 = s_bm >= 0 ? atomicAdd(n_tasks, M.nb) : 0;
@@ -133,58 +133,100 @@ constexpr int SG_GROUP = SG_GQ * (kWave - 1);  // peaks per group (252)
 // walk_block: the same walk for any block of nsb spectra whose offsets (relative
 // to the cluster's first peak p0) are in LDS; kInten also streams the
 // intensities alongside.  f(k, key, last, spectrum-in-block, m/z, intensity).
-template <bool kInten, class F>
+// SG_WR groups are in flight per wave: a ring of register groups, unrolled so
+// every slot is a fixed register set, each refilled with the group SG_WR ahead.
+#ifndef SPX_WALK_R
+#define SPX_WALK_R 1
+#endif
+constexpr int SG_WR = SPX_WALK_R + 1;  // ring slots (groups in flight + the one processed)
+
+struct NoChunkHook {
+  __device__ void operator()(int) const {}
+};
+
+// chunk(sl): after each 63-peak chunk of spectrum sl, every lane of the wave (uniform)
+template <bool kInten, class F, class C = NoChunkHook>
 __device__ __forceinline__ int walk_block(const CsrView& v, const BinMeanParams& P, int64_t p0, int nsb,
-                                          const int32_t* soff, F&& f) {
+                                          const int32_t* soff, F&& f, C&& chunk = C{}) {
   constexpr int NW = SG_BLOCK / kWave;
   const int lane = lane_id(), wid = wave_id();
-  const double* __restrict__ mz = v.mz + p0;
-  const double* __restrict__ it = v.inten + p0;
+  // buffer loads over the block's peaks: a position past its spectrum reads the
+  // descriptor's end and returns 0 -- no guarded load, so no register is a merge
+  // of a load and a constant and the ring stays in flight (counted vmcnt)
+  const int npb = soff[nsb];  // < 2^28 (the setups' limit)
+  const __amdgpu_buffer_rsrc_t rmz = bf_rsrc(v.mz + p0, npb);
+  const __amdgpu_buffer_rsrc_t rit = bf_rsrc(v.inten + p0, npb);
   const bool owner = lane < kWave - 1;
-  // uniform cursor: spectrum sl (this wave's: wid, wid + NW, ...), group start g0
-  int sl = wid, g0 = 0;
   auto skip = [&](int& s) { while (s < nsb && soff[s + 1] == soff[s]) s += NW; };
+  // the group after (sl, g0): the next 252 peaks of the spectrum or the wave's
+  // next non-empty spectrum; past the end it stays there
+  auto advance = [&](int& sl, int& g0) __attribute__((always_inline)) {
+    if (sl >= nsb) return;
+    g0 += SG_GROUP;
+    if (g0 >= soff[sl + 1] - soff[sl]) {
+      sl += NW;
+      g0 = 0;
+      skip(sl);
+    }
+  };
   auto load = [&](int s, int g, double* m, double* x) __attribute__((always_inline)) {
     const int a = s < nsb ? soff[s] : 0, e = s < nsb ? soff[s + 1] : 0;
 #pragma unroll
     for (int q = 0; q < SG_GQ; ++q) {
       const int k = a + g + q * (kWave - 1) + lane;
-      m[q] = k < e ? mz[k] : 0.0;
-      if constexpr (kInten) x[q] = k < e ? it[k] : 0.0;
+      const int bo = (k < e ? k : npb) * 8;
+      m[q] = bf_load(rmz, bo, 0);
+      if constexpr (kInten) x[q] = bf_load(rit, bo, 0);
     }
   };
-  skip(sl);
-  double cur[SG_GQ], nxt[SG_GQ], curi[SG_GQ], nxti[SG_GQ];
-  load(sl, g0, cur, curi);
+  int csl[SG_WR], cg[SG_WR];
+  double cm[SG_WR][SG_GQ], cx[SG_WR][SG_GQ];
+  csl[0] = wid;
+  cg[0] = 0;
+  skip(csl[0]);
+#pragma unroll
+  for (int r = 1; r < SG_WR; ++r) {
+    csl[r] = csl[r - 1];
+    cg[r] = cg[r - 1];
+    advance(csl[r], cg[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < SG_WR; ++r) load(csl[r], cg[r], cm[r], cx[r]);
   int bad = 0;
-  while (sl < nsb) {  // uniform
-    // the following group's cursor and loads first
-    int sn = sl, gn = g0 + SG_GROUP;
-    if (gn >= soff[sl + 1] - soff[sl]) {
-      sn = sl + NW;
-      gn = 0;
-      skip(sn);
-    }
-    load(sn, gn, nxt, nxti);
-    const int a = soff[sl], e = soff[sl + 1];
+  while (csl[0] < nsb) {  // uniform
 #pragma unroll
-    for (int q = 0; q < SG_GQ; ++q) {
-      const int k = a + g0 + q * (kWave - 1) + lane;
-      const bool act = k < e;
-      const double m = cur[q];
-      const bool inr = act && in_range(m, P);
-      const int32_t key = inr ? bin_small(m, P) : ((act && m < P.minimum) ? -1 : 0x7fffffff);
-      const int32_t kn = wave_next(key, 0x7fffffff);
-      bad |= (int)(owner && act && ((m != m) || key > kn));
-      if (owner && inr) f(p0 + k, key, kn != key, sl, m, kInten ? curi[q] : 0.0);
-    }
+    for (int r = 0; r < SG_WR; ++r) {
+      if (csl[r] < nsb) {  // uniform; cursors ascend, so past one end all are
+        const int sl = csl[r];
+        const int a = soff[sl], e = soff[sl + 1];
+        const int g0 = cg[r];
+        double m_[SG_GQ], x_[SG_GQ];
 #pragma unroll
-    for (int q = 0; q < SG_GQ; ++q) {
-      cur[q] = nxt[q];
-      if constexpr (kInten) curi[q] = nxti[q];
+        for (int q = 0; q < SG_GQ; ++q) {
+          m_[q] = cm[r][q];
+          if constexpr (kInten) x_[q] = cx[r][q];
+        }
+        // refill this slot with the group SG_WR ahead (after the newest cursor)
+        const int prev = (r + SG_WR - 1) % SG_WR;
+        int nsl = csl[prev], ng = cg[prev];
+        advance(nsl, ng);
+        load(nsl, ng, cm[r], cx[r]);
+        csl[r] = nsl;
+        cg[r] = ng;
+#pragma unroll
+        for (int q = 0; q < SG_GQ; ++q) {
+          const int k = a + g0 + q * (kWave - 1) + lane;
+          const bool act = k < e;
+          const double m = m_[q];
+          const bool inr = act && in_range(m, P);
+          const int32_t key = inr ? bin_small(m, P) : ((act && m < P.minimum) ? -1 : 0x7fffffff);
+          const int32_t kn = wave_next(key, 0x7fffffff);
+          bad |= (int)(owner && act && ((m != m) || key > kn));
+          if (owner && inr) f(p0 + k, key, kn != key, sl, m, kInten ? x_[q] : 0.0);
+          chunk(sl);
+        }
+      }
     }
-    sl = sn;
-    g0 = gn;
   }
   return bad;
 }
@@ -528,48 +570,109 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_fold_kernel(BinMeanPara
 }
 
 // numpy's pairwise mean of x[0..n) by a whole workgroup: the leaves (<= 128
-// elements, numpy's recursion) summed in parallel, one thread per leaf, then the
-// tree over the leaf sums by thread 0 in numpy's order.  `lo`, `len` and `sum`
-// hold SG_MAXLEAF entries in LDS; more leaves than that: thread 0 alone.
+// elements, numpy's recursion) found by descending from the root (thread 0, no
+// stack), summed 8 lanes per leaf, then combined in numpy's order by a post-order
+// stack machine over the leaves' root paths (thread 0, the stack in LDS).  More
+// than SG_MAXLEAF leaves: thread 0 alone (pw_sum).
 constexpr int SG_MAXLEAF = SG_BLOCK;
-__device__ double seg_pw_mean(const double* x, int64_t n, int64_t* lo, int64_t* len, double* sum, int* nleaf) {
+struct PwSmem {
+  int64_t lo[SG_MAXLEAF];
+  int32_t len[SG_MAXLEAF];
+  uint32_t path[SG_MAXLEAF];  // left (0) / right (1) turns from the root, the last turn in bit 0
+  int32_t depth[SG_MAXLEAF];
+  double sum[SG_MAXLEAF];
+  double stk[40];
+  int nleaf;
+};
+
+__device__ double seg_pw_mean(const double* x, int64_t n, PwSmem& S) {
   const int tid = threadIdx.x;
   if (tid == 0) {
-    // the leaves left to right: split [l, l+m) at h = m/2 - (m/2)%8 while m > 128
     int k = 0;
-    int64_t st_l[40], st_m[40];
-    int sp = 0;
-    st_l[0] = 0;
-    st_m[0] = n;
-    sp = 1;
-    while (sp > 0 && k <= SG_MAXLEAF) {
-      --sp;
-      const int64_t l = st_l[sp], m = st_m[sp];
-      if (m <= 128) {
-        if (k < SG_MAXLEAF) { lo[k] = l; len[k] = m; }
-        ++k;
-      } else {
+    int64_t p = 0;
+    while (p < n && k <= SG_MAXLEAF) {
+      int64_t l = 0, m = n;
+      uint32_t path = 0;
+      int d = 0;
+      while (m > 128) {  // split [l, l+m) at h = m/2 - (m/2)%8 (pw_tree)
         int64_t h = m / 2;
         h -= h % 8;
-        st_l[sp] = l + h; st_m[sp] = m - h; ++sp;  // right half after the left
-        st_l[sp] = l; st_m[sp] = h; ++sp;
+        if (p < l + h) {
+          m = h;
+          path <<= 1;
+        } else {
+          l += h;
+          m -= h;
+          path = (path << 1) | 1u;
+        }
+        ++d;
       }
+      if (k < SG_MAXLEAF) {
+        S.lo[k] = l;
+        S.len[k] = (int32_t)m;
+        S.path[k] = path;
+        S.depth[k] = d;
+      }
+      ++k;
+      p = l + m;
     }
-    *nleaf = k;
+    S.nleaf = k;
   }
   __syncthreads();
-  const int nl = *nleaf;
+  const int nl = S.nleaf;
   if (nl > SG_MAXLEAF) {  // thread 0, serially
     double r = 0.0;
     if (tid == 0) r = pw_sum([&](int64_t j) { return x[j]; }, n) / (double)n;
     return r;
   }
-  if (tid < nl) sum[tid] = pw_leaf([&](int64_t j) { return x[j]; }, lo[tid], len[tid]);
+  // the leaf sums, 8 lanes per leaf: lane i holds numpy's i-th strided partial
+  // sum (its <= 16 loads issued at once), combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
+  // by xor shuffles, then the sequential tail (pw_leaf)
+  for (int base = 0; base < nl; base += SG_BLOCK / 8) {  // uniform
+    const int l = base + tid / 8, i = tid & 7;
+    const bool act = l < nl;
+    const int64_t l0 = act ? S.lo[l] : 0;
+    const int64_t m = act ? S.len[l] : 0;
+    const int64_t lim = m - (m % 8);
+    double r = 0.0;
+    if (m >= 8) {
+      double xs[16];
+#pragma unroll
+      for (int t = 0; t < 16; ++t) xs[t] = x[l0 + min<int64_t>(i + 8 * t, m - 1)];  // (clamped: m <= 128)
+      r = xs[0];
+#pragma unroll
+      for (int t = 1; t < 16; ++t)
+        if (8 * t < lim) r += xs[t];
+    }
+    r += xor_f64<1>(r);
+    r += xor_f64<2>(r);
+    r += xor_f64<4>(r);
+    if (act && i == 0) {
+      if (m < 8) {
+        r = 0.0;
+        for (int64_t j = 0; j < m; ++j) r += x[l0 + j];
+      } else {
+        for (int64_t j = lim; j < m; ++j) r += x[l0 + j];
+      }
+      S.sum[l] = r;
+    }
+  }
   __syncthreads();
   double r = 0.0;
   if (tid == 0) {
-    int next = 0;
-    r = pw_tree([&](int64_t, int64_t) { return sum[next++]; }, n) / (double)n;
+    // post-order: a leaf (or a finished subtree) that is a right child joins its
+    // left sibling on the stack: left + right, as pw_tree adds them
+    int sp = 0;
+    for (int k = 0; k < nl; ++k) {
+      double v = S.sum[k];
+      uint32_t path = S.path[k];
+      for (int d = S.depth[k]; d > 0 && (path & 1u); --d) {
+        v = S.stk[--sp] + v;
+        path >>= 1;
+      }
+      S.stk[sp++] = v;
+    }
+    r = (0.0 + S.stk[0]) / (double)n;
   }
   return r;
 }
@@ -582,9 +685,7 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_emit_kernel(CsrView v, 
                                                                      int32_t* n_split, int32_t* glist,
                                                                      int32_t* n_glist) {
   __shared__ uint32_t tmp[SG_BLOCK / kWave + 1];
-  __shared__ int64_t leaf_lo[SG_MAXLEAF], leaf_len[SG_MAXLEAF];
-  __shared__ double leaf_sum[SG_MAXLEAF];
-  __shared__ int nleaf;
+  __shared__ PwSmem pws;
   constexpr int U = 8;
   const int tid = threadIdx.x;
   const int32_t nl = *n_list;
@@ -619,7 +720,7 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_seg_emit_kernel(CsrView v, 
       }
     }
     const int64_t s0 = v.cluster_off[M.c];
-    const double pm = seg_pw_mean(v.prec_mz + s0, M.n, leaf_lo, leaf_len, leaf_sum, &nleaf);  // np.mean (binning.py:224)
+    const double pm = seg_pw_mean(v.prec_mz + s0, M.n, pws);  // np.mean (binning.py:224)
     if (tid == 0) {
       out.count[M.c] = total;
       charge_out[M.c] = v.charge[s0];

@@ -255,7 +255,7 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   int32_t* n_seg_in = W.counters + 8;  // [8] the segmented fold's list (what the kept-bin fold passes on)
   int32_t* n_qtasks = W.counters + 9;  // [9..11] kept-bin fold block tasks, count tiles, fold units
   int32_t* n_qtiles = W.counters + 10;
-  int32_t* n_qunits = W.counters + 11;
+  int32_t* n_qunits = W.counters + 11;  // [11], [12]: long-chain / other fold units
 
   spx::BinMeanParams P;
   P.minimum = params->minimum;
@@ -299,8 +299,8 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   hipLaunchKernelGGL(spx::bin_mean_q_place_kernel, gqt, bsg, 0, s, V, P, W.qmeta, W.arena, W.q_task_cl, n_qtasks,
                      W.q_task_cap);
   if (int rc = check_launch("bin_mean_q_place_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_q_fold_kernel, dim3((unsigned)std::max(1, std::min(W.q_unit_cap / 4 + 1, 4096))),
-                     bsg, 0, s, W.qmeta, W.arena, W.q_unit_cl, n_qunits, W.q_unit_cap);
+  hipLaunchKernelGGL(spx::bin_mean_q_fold_kernel, dim3((unsigned)std::max(1, std::min(W.q_unit_cap, 2048))),
+                     dim3(spx::QF_BLOCK), 0, s, W.qmeta, W.arena, W.q_unit_cl, n_qunits, W.q_unit_cap);
   if (int rc = check_launch("bin_mean_q_fold_kernel")) return rc;
   hipLaunchKernelGGL(spx::bin_mean_q_emit_kernel, gcl, bsg, 0, s, V, O, prec_out, charge_out, status, n_def, W.qmeta,
                      W.arena, W.seg_in, n_seg_in, W.glist, n_glist);
