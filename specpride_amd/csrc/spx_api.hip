@@ -18,6 +18,7 @@
 #include "bin_mean.hip"
 #include "bin_mean_seg.hip"
 #include "bin_mean_q.hip"
+
 #include "bin_mean_split.hip"
 #include "bin_mean_wide.hip"
 #include "binned_cosine.hip"

@@ -1,11 +1,13 @@
 """Run one bin-mean shape of bench.bin_mean_shapes a few times (profiling driver):
 python tools/run_shape.py skewed_config3|long_spectra_600 [reps]."""
+import os
 import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
 
-from specpride_amd import engine
-from specpride_amd.synthetic import make_clusters_torch
+from specpride_amd import engine  # noqa: E402
+from specpride_amd.synthetic import make_clusters_torch  # noqa: E402
 
 SHAPES = {"skewed_config3": dict(n_clusters=20000, seed=4, skewed=True, forced_large=4, large_size=5000),
           "long_spectra_600": dict(n_clusters=20000, seed=6, n_template=600)}
