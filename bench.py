@@ -122,6 +122,17 @@ def load_pmc_traffic(kernel: str, batch):
     return v if not peaks or peaks == batch.n_peaks else v * batch.n_peaks / peaks
 
 
+def load_shape_traffic(key: str):
+    """HBM bytes per call of an off-shape run (all the entry point's kernels), from
+    the committed PMC passes of tools/gpu/shapes_pmc.sh over the same synthetic
+    batch (profiles/pmc_traffic_shapes.json, keys bm_<shape> / md_<shape>)."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_traffic_shapes.json")) as fh:
+            return json.load(fh).get(key)
+    except (OSError, ValueError):
+        return None
+
+
 def roofline(name, kernel, nbytes, ms, traffic=None):
     gbs = nbytes / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "kernel": kernel, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -389,7 +400,8 @@ def medoid_shapes(args, out):
         "clusters": batch.n_clusters, "spectra": batch.n_spectra, "peaks": batch.n_peaks,
         "large_path_by_size": int(large.sum()), "ms": round(ms, 3),
         "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1), "all_resolved": ok,
-        "roofline": roofline("spx_medoid", "all medoid kernels", medoid_bytes(batch), ms)}}
+        "roofline": roofline("spx_medoid", "all medoid kernels", medoid_bytes(batch), ms,
+                             load_shape_traffic("md_long_spectra_600"))}}
     del md, batch, t
     torch.cuda.empty_cache()
 
@@ -419,7 +431,8 @@ def bin_mean_shapes(args, out):
                      "max_n": int(sizes.max()), "max_spectrum_peaks": int(np.diff(so).max()),
                      "ms": round(ms, 3), "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1),
                      "all_ok": bool(np.all(st == 0)),
-                     "roofline": roofline("spx_bin_mean", "all bin-mean kernels", consensus_bytes(batch, kept), ms)}
+                     "roofline": roofline("spx_bin_mean", "all bin-mean kernels", consensus_bytes(batch, kept), ms,
+                                          load_shape_traffic(f"bm_{name}"))}
         del bm, batch, t
         torch.cuda.empty_cache()
     out["bin_mean_shapes"] = res

@@ -726,25 +726,20 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 }
 
 // Register-code kernel: one workgroup per cluster.  Clusters this path does not
-// take (kNotHere) go to `rest` for bin_mean_lds_kernel; kDeferred ones (unsorted,
-// NaN, too many distinct bins) straight to the global kernel's list.
+// take (kNotHere) and kDeferred ones (unsorted, NaN, too many distinct bins) go
+// to the striped `rest` list of the wide kernel (which hands the unsorted ones on
+// to the global kernel).
 __global__ __launch_bounds__(BM_BLOCK, SPX_BR_MINW) void bin_mean_reg_kernel(CsrView v, BinMeanParams P, PeaksOut out,
                                                                              double* prec_out, int32_t* charge_out,
-                                                                             int32_t* status, int32_t* rest,
-                                                                             int32_t* n_rest, int32_t* deferred,
-                                                                             int32_t* n_deferred) {
+                                                                             int32_t* status, StripedList rest) {
   __shared__ BinRegSmem L;
   const int64_t c = blockIdx.x;
   SPX_STAMP(0);
   const int32_t st = bin_mean_reg_path(v, P, L, c, out, prec_out, charge_out);
   SPX_STAMP(5);
   if (threadIdx.x == 0) {
-    if (st == kNotHere) {
-      rest[atomicAdd(n_rest, 1)] = (int32_t)c;
-    } else {
-      status[c] = st;
-      if (st == kDeferred) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
-    }
+    if (st != kNotHere) status[c] = st;
+    if (st == kNotHere || st == kDeferred) striped_push(rest, (int32_t)c);
   }
 }
 

@@ -220,15 +220,15 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
 __global__ __launch_bounds__(BW_BLOCK, SPX_BW_MINW) void bin_mean_wide_kernel(CsrView v, BinMeanParams P,
                                                                               PeaksOut out, double* prec_out,
                                                                               int32_t* charge_out, int32_t* status,
-                                                                              const int32_t* list,
-                                                                              const int32_t* n_list,
+                                                                              StripedList list,
                                                                               int32_t* deferred,
                                                                               int32_t* n_deferred, int32_t* glist,
                                                                               int32_t* n_glist) {
   __shared__ BinWideSmem L;
-  const int32_t nl = *n_list;
+  __shared__ int32_t lbase[kListStripes + 1];
+  const int32_t nl = striped_prefix(list, lbase);
   for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
-    const int64_t c = list[i];
+    const int64_t c = striped_at(list, lbase, i);
     const int32_t st = bin_mean_wide_body(v, P, L, c, out, prec_out, charge_out);
     if (threadIdx.x == 0) {
       if (st == kUnsortedW) {

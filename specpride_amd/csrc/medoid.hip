@@ -461,27 +461,28 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
 // Register kernel: one 256-thread workgroup per cluster.  Clusters past its caps
 // go to the wide kernel's list.
 __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
-                                                              double* totals_out, int32_t* wide, int32_t* n_wide) {
+                                                              double* totals_out, StripedList wide) {
   __shared__ MedoidRegSmem<MD_BLOCK, MR_UMAX, MD_KWMAX> L;
   medoid_small_body<MD_BLOCK, MR_UMAX, MD_KWMAX>(v, P, rep, totals_out, L, (int64_t)blockIdx.x,
                                                 [&](int64_t c, int64_t, int) {
     // every leftover via the wide kernel, which passes n > 64 straight on (one
     // list target here keeps the kernel's register budget)
     rep[c] = -4;
-    wide[atomicAdd(n_wide, 1)] = (int32_t)c;
+    striped_push(wide, (int32_t)c);
   });
 }
 
 // Wide kernel: the register kernel's leftovers, grid-stride; what it cannot hold
 // (n > 64 first of all) goes on to the large path.
 __global__ __launch_bounds__(MW_BLOCK, 4) void medoid_wide_kernel(CsrView v, MedoidParams P, int64_t* rep,
-                                                                  double* totals_out, const int32_t* wide,
-                                                                  const int32_t* n_wide, int32_t* deferred,
-                                                                  int32_t* n_deferred, MedoidMeta* meta) {
+                                                                  double* totals_out, StripedList wide,
+                                                                  int32_t* deferred, int32_t* n_deferred,
+                                                                  MedoidMeta* meta) {
   __shared__ MedoidRegSmem<MW_BLOCK, MW_UMAX, MW_KWMAX> L;
-  const int32_t nw = *n_wide;
+  __shared__ int32_t lbase[kListStripes + 1];
+  const int32_t nw = striped_prefix(wide, lbase);
   for (int32_t i = blockIdx.x; i < nw; i += gridDim.x) {
-    medoid_small_body<MW_BLOCK, MW_UMAX, MW_KWMAX>(v, P, rep, totals_out, L, (int64_t)wide[i],
+    medoid_small_body<MW_BLOCK, MW_UMAX, MW_KWMAX>(v, P, rep, totals_out, L, (int64_t)striped_at(wide, lbase, i),
                                                   [&](int64_t c, int64_t s0, int n) {
       md_defer(c, s0, n, deferred, n_deferred, meta, rep);
     });

@@ -165,7 +165,8 @@ int kept_fold_enabled() {
 }
 
 struct BinMeanWs {
-  int32_t *counters, *def, *rest, *glist, *split_list, *task_cl, *tile_cl;
+  int32_t *counters, *def, *glist, *split_list, *task_cl, *tile_cl;
+  spx::StripedList rest;  // the register kernel's leftovers (striped appends)
   int32_t *seg_in, *q_task_cl, *q_tile_cl, *q_unit_cl;
   unsigned long long* bump;
   spx::SplitCluster* scl;
@@ -183,8 +184,11 @@ BinMeanWs carve_bin_mean(Carver& w, const spx_csr* csr, const spx_bin_params* pa
   BinMeanWs W;
   W.counters = w.take<int32_t>(16);
   W.bump = w.take<unsigned long long>(1);
+  // right after the counters and the bump pointer: one memset clears all three
+  W.rest.counts = w.take<int32_t>((size_t)spx::kListStripes * spx::kListLine);
+  W.rest.cap = spx::striped_cap((int64_t)C);
+  W.rest.items = w.take<int32_t>((size_t)W.rest.cap * spx::kListStripes);
   W.def = w.take<int32_t>(C);
-  W.rest = w.take<int32_t>(C);
   W.glist = w.take<int32_t>(C);
   W.split_list = w.take<int32_t>(C);
   W.scl = w.take<spx::SplitCluster>(C);
@@ -241,12 +245,10 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
   const BinMeanWs W = carve_bin_mean(w, csr, params);
-  // counters: [0] deferred past the wide kernel (kept-bin fold), [1] left to the
-  // wide kernel, [2] planned split clusters, [3] split ranges, [4] the global
+  // counters: [0] deferred past the wide kernel (kept-bin fold), [1] (unused), [2] planned split clusters, [3] split ranges, [4] the global
   // kernel's list, [5] segmented-fold block tasks, [6] its slot tiles, [7] the
   // split path's list (clusters the segmented fold's arena could not hold)
   int32_t* n_def = W.counters;
-  int32_t* n_rest = W.counters + 1;
   int32_t* n_scl = W.counters + 2;
   int32_t* n_ranges = W.counters + 3;
   int32_t* n_glist = W.counters + 4;
@@ -269,17 +271,18 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const spx::CsrView V = view(csr);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
-  // the 8 counters and the bump pointer share the first 256 B of the workspace
-  if (hipMemsetAsync(W.counters, 0, 256 + sizeof(unsigned long long), s) != hipSuccess)
+  // the counters (first 256 B), the bump pointer (next 256 B) and the striped
+  // list's counters after them
+  if (hipMemsetAsync(W.counters, 0, 512 + spx::kListCountBytes, s) != hipSuccess)
     return check_launch("spx_bin_mean memset");
   // register path; its leftovers (longer spectra, more spectra, unsorted, > 1,536
   // bins) all go to the wide kernel's list
   hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                     charge_out, status, W.rest, n_rest, W.rest, n_rest);
+                     charge_out, status, W.rest);
   if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
   const dim3 gcl((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048)));
   hipLaunchKernelGGL(spx::bin_mean_wide_kernel, gcl, dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out, status,
-                     W.rest, n_rest, W.def, n_def, W.glist, n_glist);
+                     W.rest, W.def, n_def, W.glist, n_glist);
   if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
   const dim3 bsg(spx::SG_BLOCK);
   // kept-bin fold of the clusters past the wide kernel (the quorum applies)
@@ -430,8 +433,9 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
                                  int64_t n_extra) {
   if (C < 0 || (C > 0 && (!hco || !hso)) || n_extra < 0 || (n_extra > 0 && !extra)) return 0;
   const size_t Cm = (size_t)std::max<int64_t>(C, 1);
-  size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(sizeof(int32_t)) +
-                 align256(sizeof(int32_t) * Cm) + align256(sizeof(int32_t) * Cm) +
+  size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(spx::kListCountBytes) +
+                 align256(sizeof(int32_t) * Cm) +
+                 align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
                  align256(sizeof(spx::MedoidMeta) * Cm) + 4 * align256(sizeof(int64_t) * (Cm + 1));
   size_t arena = 0, margin = 0;
   for (int64_t c = 0; c < C; ++c) {
@@ -469,9 +473,11 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   if (!workspace) return fail(SPX_ENOSPACE, "spx_medoid: no workspace");
   int32_t* n_def = w.take<int32_t>(1);
   unsigned long long* bump = w.take<unsigned long long>(1);
-  int32_t* n_wide = w.take<int32_t>(1);
+  spx::StripedList wide;  // the register kernel's leftovers for the wide kernel (striped appends)
+  wide.counts = w.take<int32_t>((size_t)spx::kListStripes * spx::kListLine);
+  wide.cap = spx::striped_cap(C);
   int32_t* def = w.take<int32_t>((size_t)C);
-  int32_t* wide = w.take<int32_t>((size_t)C);
+  wide.items = w.take<int32_t>((size_t)wide.cap * spx::kListStripes);
   spx::MedoidMeta* meta = w.take<spx::MedoidMeta>((size_t)C);
   int64_t* tile_base = w.take<int64_t>((size_t)C + 1);
   int64_t* unit_base = w.take<int64_t>((size_t)C + 1);
@@ -487,12 +493,12 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   // and an empty deferred list (the common case) costs a small launch
   const dim3 grid2(spx::MD_GRIDX, std::min<unsigned>(g, 32u)), blk(spx::MD_BLOCK);
 
-  // n_def, bump and n_wide: the first 768 B
-  if (hipMemsetAsync(n_def, 0, 768, s) != hipSuccess) return check_launch("spx_medoid memset");
-  hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, wide, n_wide);
+  // n_def, bump and the striped list's counters: the first 512 B + kListCountBytes
+  if (hipMemsetAsync(n_def, 0, 512 + spx::kListCountBytes, s) != hipSuccess) return check_launch("spx_medoid memset");
+  hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, wide);
   if (int rc = check_launch("medoid_reg_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024))),
-                     dim3(spx::MW_BLOCK), 0, s, V, P, rep, totals, wide, n_wide, def, n_def, meta);
+                     dim3(spx::MW_BLOCK), 0, s, V, P, rep, totals, wide, def, n_def, meta);
   if (int rc = check_launch("medoid_wide_kernel")) return rc;
   if (!params->large_path) return SPX_SUCCESS;  // deferred clusters keep rep = SPX_REP_DEFERRED
   hipLaunchKernelGGL(spx::medoid_range_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena, bump, arena_bytes);
