@@ -105,6 +105,19 @@ size_t spx_bin_mean_workspace_size(const spx_csr *csr, const spx_bin_params *par
 int spx_bin_mean(const spx_csr *csr, const spx_bin_params *params, const spx_batch_info *info,
                  spx_peaks_out *out, double *prec_out, int32_t *charge_out, int32_t *status,
                  void *workspace, size_t workspace_bytes, void *stream);
+/* spx_bin_mean in two halves, for a caller that reads the statuses anyway (the
+ * per-cluster shim, binning.py:291-297, which copies every result back):
+ *   stage 1: the register and wide kernels (and the global kernel for unsorted
+ *            spectra) -- every cluster of <= 128 spectra and <= 4,096 distinct bins;
+ *            the others keep status SPX_UNRESOLVED;
+ *   stage 2: the chain for those (kept-bin fold, segmented fold, split path), on
+ *            the SAME workspace, untouched since stage 1;
+ *   stage 0: both (= spx_bin_mean).
+ * Stage 1 alone is a memset and 3 kernels instead of 21 kernels: a one-cluster
+ * call costs about 100 us less when no cluster needs stage 2. */
+int spx_bin_mean_stage(const spx_csr *csr, const spx_bin_params *params, const spx_batch_info *info,
+                       spx_peaks_out *out, double *prec_out, int32_t *charge_out, int32_t *status,
+                       void *workspace, size_t workspace_bytes, void *stream, int stage);
 
 /* ---- gap-average: average_spectrum(spectra, title, pepmass, rtinseconds, charge,
  *      mz_accuracy=0.01, dyn_range=1000, min_fraction=0.5) + precursor helpers ---- */

@@ -64,7 +64,7 @@ class SpxCosineParams(ctypes.Structure):
 
 
 # every symbol include/specpride.h declares (checked by tests/test_host.py)
-EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_gap_average_workspace_size", "spx_gap_average",
+EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_bin_mean_stage", "spx_gap_average_workspace_size", "spx_gap_average",
             "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
             "spx_compact_peaks", "spx_copy_h2d", "spx_copy_d2h",
             "spx_abi_version", "spx_last_error"]
@@ -127,6 +127,7 @@ def lib():
     L.spx_bin_mean_workspace_size.restype = _sz
     L.spx_bin_mean_workspace_size.argtypes = [_p, _p, _p]
     L.spx_bin_mean.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]
+    L.spx_bin_mean_stage.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _p, _i32]
     L.spx_gap_average_workspace_size.restype = _sz
     L.spx_gap_average_workspace_size.argtypes = [_p, _p, _p]
     L.spx_gap_average.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]

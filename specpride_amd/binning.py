@@ -147,8 +147,11 @@ class RepresentativeSpectrumCreator:
         """The device pass over a packed batch: the dense host result of
         :meth:`engine.PeaksResult.to_host`, after raising the reference's error for
         the first failing cluster (AssertionError on mixed charges, binning.py:205-206)."""
-        res = engine.bin_mean(engine.DeviceBatch.from_host(csr, self.device), minimum, maximum, binsize,
-                              apply_peak_quorum).to_host()
+        batch = engine.DeviceBatch.from_host(csr, self.device)
+        # a batch small enough for the one-copy readback (the per-cluster calls) runs
+        # the large-cluster chain only if a cluster needs it (spx_bin_mean_stage)
+        res = engine.bin_mean(batch, minimum, maximum, binsize, apply_peak_quorum,
+                              staged=engine.packed_readback(batch)).to_host()
         bad = np.flatnonzero(res["status"] != engine.STATUS_OK)
         if len(bad):
             if res["status"][bad[0]] == engine.STATUS_MIXED_CHARGE:

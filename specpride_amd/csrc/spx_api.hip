@@ -230,9 +230,10 @@ size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* par
   return w.used + (size_t)bin_mean_fallback_grid(C, params, dcap) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
-int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info, spx_peaks_out* out,
-                 double* prec_out, int32_t* charge_out, int32_t* status, void* workspace, size_t workspace_bytes,
-                 void* stream) {
+int spx_bin_mean_stage(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
+                       spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* workspace,
+                       size_t workspace_bytes, void* stream, int stage) {
+  if (stage < 0 || stage > 2) return fail(SPX_EINVAL, "spx_bin_mean_stage: stage must be 0, 1 or 2");
   if (!csr_ok(csr) || !params || !info || !out || !out->count || !prec_out || !charge_out || !status)
     return fail(SPX_EINVAL, "spx_bin_mean: null argument");
   if (!(params->binsize > 0) || !(params->maximum > params->minimum))
@@ -271,19 +272,31 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   const spx::CsrView V = view(csr);
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
-  // the counters (first 256 B), the bump pointer (next 256 B) and the striped
-  // list's counters after them
-  if (hipMemsetAsync(W.counters, 0, 512 + spx::kListCountBytes, s) != hipSuccess)
-    return check_launch("spx_bin_mean memset");
-  // register path; its leftovers (longer spectra, more spectra, unsorted, > 1,536
-  // bins) all go to the wide kernel's list
-  hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                     charge_out, status, W.rest);
-  if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
   const dim3 gcl((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048)));
-  hipLaunchKernelGGL(spx::bin_mean_wide_kernel, gcl, dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out, status,
-                     W.rest, W.def, n_def, W.glist, n_glist);
-  if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
+  auto global_pass = [&]() {
+    hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)bin_mean_fallback_grid(C, params, dcap)),
+                       dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, W.glist, n_glist, W.scratch,
+                       spx::bin_mean_slice_bytes(P.n_words, dcap), (int)std::min<int64_t>(dcap, INT32_MAX));
+    return check_launch("bin_mean_global_kernel");
+  };
+  // stage 0/1: the counters (first 256 B), the bump pointer (next 256 B) and the
+  // striped list's counters after them, then the register path, whose leftovers
+  // (longer spectra, more spectra, unsorted, > 1,536 bins) all go to the wide kernel
+  if (stage != 2) {
+    if (hipMemsetAsync(W.counters, 0, 512 + spx::kListCountBytes, s) != hipSuccess)
+      return check_launch("spx_bin_mean memset");
+    hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                       charge_out, status, W.rest);
+    if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
+    hipLaunchKernelGGL(spx::bin_mean_wide_kernel, gcl, dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out,
+                       status, W.rest, W.def, n_def, W.glist, n_glist);
+    if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
+  }
+  if (stage == 1) return global_pass();  // clusters past the wide kernel keep status SPX_UNRESOLVED
+  if (stage == 2) {
+    // the global kernel's list was consumed by stage 1: the chain's own start at 0
+    if (hipMemsetAsync(n_glist, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
+  }
   const dim3 bsg(spx::SG_BLOCK);
   // kept-bin fold of the clusters past the wide kernel (the quorum applies)
   const dim3 gqt((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.q_task_cap, 8192)));
@@ -344,10 +357,14 @@ int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_bat
   hipLaunchKernelGGL(spx::bin_mean_split_emit_kernel, gcl, dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                      charge_out, status, W.scl, n_scl, W.ranges, W.glist, n_glist);
   if (int rc = check_launch("bin_mean_split_emit_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)bin_mean_fallback_grid(C, params, dcap)),
-                     dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, W.glist, n_glist, W.scratch,
-                     spx::bin_mean_slice_bytes(P.n_words, dcap), (int)std::min<int64_t>(dcap, INT32_MAX));
-  return check_launch("bin_mean_global_kernel");
+  return global_pass();
+}
+
+int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info, spx_peaks_out* out,
+                 double* prec_out, int32_t* charge_out, int32_t* status, void* workspace, size_t workspace_bytes,
+                 void* stream) {
+  return spx_bin_mean_stage(csr, params, info, out, prec_out, charge_out, status, workspace, workspace_bytes, stream,
+                            0);
 }
 
 // -------------------------------------------------------------- gap-average

@@ -233,6 +233,11 @@ def _packed_to_host(tensors):
     return res
 
 
+def packed_readback(batch) -> bool:
+    """Results of this batch come back in one packed D2H (PeaksResult.to_host)."""
+    return 16 * batch.n_peaks + 32 * batch.n_clusters <= PACKED_MAX_BYTES
+
+
 @dataclass
 class PeaksResult:
     """Per-cluster peak lists in the capacity layout (cluster c at its input
@@ -246,6 +251,9 @@ class PeaksResult:
     charge: object
     rt: object = None
     stream: object = None  # the torch stream the producing kernel was enqueued on
+    # bin_mean(staged=True): enqueues spx_bin_mean_stage(2); to_host() runs it when a
+    # cluster came back SPX_UNRESOLVED from stage 1
+    pending: object = None
 
     def compact(self, stream=None, total: Optional[int] = None):
         """Dense device arrays: (out_off [C+1], mz, inten).  Enqueued on ``stream``
@@ -269,10 +277,18 @@ class PeaksResult:
         return out_off, dmz[:n], dint[:n]
 
     def to_host(self) -> dict:
+        d = self._to_host()
+        if self.pending is not None:
+            finish, self.pending = self.pending, None
+            if np.any(d["status"] == STATUS_UNRESOLVED):
+                finish()
+                d = self._to_host()
+        return d
+
+    def _to_host(self) -> dict:
         import torch
 
-        C, P = self.batch.n_clusters, self.batch.n_peaks
-        if 16 * P + 32 * C <= PACKED_MAX_BYTES:
+        if packed_readback(self.batch):
             return self._to_host_small()
         out_off, mz, inten = self.compact()
         if self.stream is not None:
@@ -319,8 +335,14 @@ def _alloc_peaks(batch: DeviceBatch):
 
 
 def bin_mean(batch: DeviceBatch, minimum=100.0, maximum=2000.0, binsize=0.02, apply_peak_quorum=True,
-             out: Optional[PeaksResult] = None, stream=None) -> PeaksResult:
-    """combine_bin_mean (binning.py:170-231) for every cluster of the batch."""
+             out: Optional[PeaksResult] = None, stream=None, staged: bool = False) -> PeaksResult:
+    """combine_bin_mean (binning.py:170-231) for every cluster of the batch.
+
+    ``staged``: enqueue only stage 1 of ``spx_bin_mean_stage`` (the register and wide
+    kernels); :meth:`PeaksResult.to_host` runs stage 2 (the large-cluster chain) if a
+    cluster needs it.  For callers that copy the result back anyway (the per-cluster
+    shims): 17 fewer empty launches per call.  Device-side consumers of the result
+    must not use it."""
     L = _lib.lib()
     prm = _lib.SpxBinParams(float(minimum), float(maximum), float(binsize), int(apply_peak_quorum is True))
     need = L.spx_bin_mean_workspace_size(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info))
@@ -330,9 +352,14 @@ def bin_mean(batch: DeviceBatch, minimum=100.0, maximum=2000.0, binsize=0.02, ap
         out = PeaksResult(batch, mz, it, cnt, st, prec, ch)
     out.stream = stream
     po = _lib.SpxPeaksOut(_ptr(out.mz), _ptr(out.inten), _ptr(out.count))
-    _lib.check(L.spx_bin_mean(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info), ctypes.byref(po),
-                              _ptr(out.prec), _ptr(out.charge), _ptr(out.status), _ptr(ws), ws.numel(),
-                              _stream_handle(stream)), "spx_bin_mean")
+
+    def launch(stage):
+        _lib.check(L.spx_bin_mean_stage(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info),
+                                        ctypes.byref(po), _ptr(out.prec), _ptr(out.charge), _ptr(out.status),
+                                        _ptr(ws), ws.numel(), _stream_handle(stream), stage), "spx_bin_mean")
+
+    launch(1 if staged else 0)
+    out.pending = (lambda: launch(2)) if staged else None
     return out
 
 

@@ -357,6 +357,38 @@ def test_bin_mean_skewed_and_unsorted(gpu):
     assert_bin_mean_equal(_bin_mean(sub), c_oracle.bin_mean(sub))
 
 
+def test_bin_mean_staged(gpu):
+    """spx_bin_mean_stage: stage 1 alone (every cluster within the wide kernel's
+    caps) and stage 1 + 2 on demand (skewed sizes, shuffled spectra: to_host runs
+    stage 2 when a cluster came back SPX_UNRESOLVED) equal the one-call chain and
+    the oracle bit for bit; the per-cluster shim takes the staged path."""
+    from specpride_amd.binning import RepresentativeSpectrumCreator
+
+    small = make_clusters_np(40, seed=93)
+    big = make_clusters_np(400, seed=91, skewed=True)
+    big = big.select([c for c in range(big.n_clusters) if big.cluster_off[c + 1] - big.cluster_off[c] <= 300])
+    for csr in (small, big, _shuffled(big.select(range(120)))):
+        ref = c_oracle.bin_mean(csr)
+        batch = engine.DeviceBatch.from_host(csr)
+        res = engine.bin_mean(batch, staged=True)
+        assert res.pending is not None
+        assert_bin_mean_equal(res.to_host(), ref)
+        assert res.pending is None
+        assert_bin_mean_equal(engine.bin_mean(batch).to_host(), ref)
+    sizes = np.diff(big.cluster_off)
+    assert sizes.max() > 128  # stage 2 really ran for this batch
+    c = int(np.argmax(sizes))
+    one = big.select([c])
+    clusters = [[{"m/z array": one.mz[one.spec_off[s]:one.spec_off[s + 1]],
+                  "intensity array": one.inten[one.spec_off[s]:one.spec_off[s + 1]],
+                  "precursor mz": float(one.prec_mz[s]), "precursor charge": int(one.charge[s])}
+                 for s in range(one.n_spectra)]]
+    got = RepresentativeSpectrumCreator().combine_bin_mean(clusters[0])
+    ref = c_oracle.bin_mean(one)
+    np.testing.assert_array_equal(got["mzs"], ref["out_mz"])
+    np.testing.assert_array_equal(got["intensities"], ref["out_int"])
+
+
 def test_bin_mean_range_boundaries(gpu):
     """Short spectra (1-3 peaks), spectra entirely below / above parts of the range,
     repeated identical spectra (every bin hit by every spectrum), spectra of 255
