@@ -10,7 +10,8 @@
 //   extra fields ignored); a stripped "END IONS" stores the spectrum.
 // Numbers use the plain decimal grammar [+-]digits[.digits][e[+-]digits]; the
 // values equal Python float(): both are correctly rounded (Clinger's exact fast
-// path for short decimals, strtod otherwise).  Any
+// path for short decimals, an x87 extended-precision step for up to 19 digits,
+// strtod otherwise).  Any
 // line outside that subset (underscores in numbers, inf/nan, tabs between
 // fields, non-ASCII text, PEPMASS before the first TITLE, a repeated END IONS,
 // a TITLE without ';') makes the parse report "fallback: ..." and the caller
@@ -36,6 +37,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -92,18 +94,56 @@ inline void strip(const char*& b, const char*& e) {
 // representable 10^k (|k| <= 22) is ONE correctly rounded IEEE multiply or divide
 // of exact operands -- the correctly rounded value of the decimal, i.e. what
 // strtod and Python's float() return.  m/z and intensity lines ("1234.56789
-// 17.25") take it; anything longer (> 19 significant digits, large exponents)
-// falls to strtod.
-bool parse_float(const char* b, const char* e, double& out) {
+// 17.25") take it; 16-19 digit ones take the extended-precision step below;
+// anything longer (> 19 significant digits, large exponents) falls to strtod.
+// The value of the decimal w * 10^k (w: its significant digits, `fast` false when
+// there were more than 19), correctly rounded; [b, e) is the token for strtod.
+inline double decimal_value(bool neg, uint64_t w, bool fast, int k, const char* b, const char* e) {
   static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                     1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-  const char* p = b;
-  bool neg = false;
-  if (p < e && (*p == '+' || *p == '-')) { neg = *p == '-'; ++p; }
-  uint64_t w = 0;
-  int nd = 0, frac = 0;
-  bool digits = false, fast = true;
-  for (; p < e && (unsigned)(*p - '0') <= 9u; ++p) {  // integer part
+  if (fast && w <= (uint64_t(1) << 53) && k >= -22 && k <= 22) {
+    const double v = k < 0 ? (double)w / kPow10[-k] : (double)w * kPow10[k];
+    return neg ? -v : v;
+  }
+  // Significands of 54..64 bits (the repr of an arbitrary double has 16-17 digits):
+  // one x87 extended-precision divide or multiply of exact operands (w < 2^64 and
+  // 10^|k| <= 10^27 are exact in a 64-bit significand) gives the decimal correctly
+  // rounded to 64 bits.  Rounding that to 53 bits is the correct rounding of the
+  // decimal itself unless a double's rounding midpoint lies within one extended
+  // unit of it -- low 11 significand bits 0x3FF..0x401 -- which strtod decides.
+  if (fast && k >= -27 && k <= 27) {
+    static const long double kPow10L[28] = {1e0L,  1e1L,  1e2L,  1e3L,  1e4L,  1e5L,  1e6L,  1e7L,  1e8L,  1e9L,
+                                            1e10L, 1e11L, 1e12L, 1e13L, 1e14L, 1e15L, 1e16L, 1e17L, 1e18L, 1e19L,
+                                            1e20L, 1e21L, 1e22L, 1e23L, 1e24L, 1e25L, 1e26L, 1e27L};
+    static_assert(sizeof(long double) >= 10 && std::numeric_limits<long double>::digits == 64,
+                  "x87 extended precision");
+    const long double L = k < 0 ? (long double)w / kPow10L[-k] : (long double)w * kPow10L[k];
+    uint64_t sig;
+    std::memcpy(&sig, &L, sizeof(sig));  // the 64-bit significand (explicit integer bit)
+    const unsigned lo = (unsigned)(sig & 0x7FFu);
+    if (lo < 0x3FFu || lo > 0x401u) {
+      const double v = (double)L;
+      return neg ? -v : v;
+    }
+  }
+  char buf[128];
+  const size_t n = (size_t)(e - b);
+  if (n >= sizeof(buf)) {
+    std::string s(b, e);
+    return std::strtod(s.c_str(), nullptr);
+  }
+  std::memcpy(buf, b, n);
+  buf[n] = 0;
+  return std::strtod(buf, nullptr);
+}
+
+// digits [. digits] from p (no sign, no exponent): the significand, its digit
+// count and fraction length, as parse_float accumulates them; p stops at the
+// first byte of neither.  Returns whether any digit was seen.
+inline bool scan_unsigned(const char*& p, const char* e, uint64_t& w, bool& fast, int& frac) {
+  bool digits = false;
+  int nd = 0;
+  for (; p < e && (unsigned)(*p - '0') <= 9u; ++p) {
     digits = true;
     const unsigned d = (unsigned)(*p - '0');
     if (w == 0 && d == 0) continue;  // leading zeros: no significant digit
@@ -121,7 +161,17 @@ bool parse_float(const char* b, const char* e, double& out) {
       else w = w * 10 + d;
     }
   }
-  if (!digits) return false;
+  return digits;
+}
+
+bool parse_float(const char* b, const char* e, double& out) {
+  const char* p = b;
+  bool neg = false;
+  if (p < e && (*p == '+' || *p == '-')) { neg = *p == '-'; ++p; }
+  uint64_t w = 0;
+  int frac = 0;
+  bool fast = true;
+  if (!scan_unsigned(p, e, w, fast, frac)) return false;
   int ex = 0;
   if (p < e && (*p == 'e' || *p == 'E')) {
     ++p;
@@ -134,22 +184,41 @@ bool parse_float(const char* b, const char* e, double& out) {
     if (eneg) ex = -ex;
   }
   if (p != e) return false;
-  const int k = ex - frac;
-  if (fast && w <= (uint64_t(1) << 53) && k >= -22 && k <= 22) {
-    const double v = k < 0 ? (double)w / kPow10[-k] : (double)w * kPow10[k];
-    out = neg ? -v : v;
-    return true;
+  out = decimal_value(neg, w, fast, ex - frac, b, e);
+  return true;
+}
+
+// The common peak line "<digits>[.digits]<sep><digits>[.digits]" + \n, \r\n, \r or
+// the end, parsed in one pass from its first byte (a digit) at p: the two values
+// and p past the line terminator.  `single`: the separator is exactly one space
+// (the binning reader's split(' ')), else one or more spaces/tabs (the general
+// reader's whitespace split).  Any other shape -- a sign, an exponent, a third
+// field, trailing blanks -- returns false with p unchanged, and the caller's
+// line-by-line path decides; the values are parse_float's for the same tokens.
+inline bool fast_peak_line(const char*& p, const char* e, bool single, double& a, double& v) {
+  const char* q = p;
+  uint64_t w1 = 0, w2 = 0;
+  int f1 = 0, f2 = 0;
+  bool k1 = true, k2 = true;
+  const char* b1 = q;
+  if (!scan_unsigned(q, e, w1, k1, f1)) return false;
+  const char* e1 = q;
+  if (q >= e || (*q != ' ' && (single || *q != '\t'))) return false;
+  ++q;
+  if (!single)
+    while (q < e && (*q == ' ' || *q == '\t')) ++q;
+  if (q >= e || (unsigned)(*q - '0') > 9u) return false;
+  const char* b2 = q;
+  if (!scan_unsigned(q, e, w2, k2, f2)) return false;
+  const char* e2 = q;
+  if (q < e) {
+    if (*q == '\n') ++q;
+    else if (*q == '\r') { ++q; if (q < e && *q == '\n') ++q; }
+    else return false;
   }
-  char buf[128];
-  const size_t n = (size_t)(e - b);
-  if (n >= sizeof(buf)) {
-    std::string s(b, e);
-    out = std::strtod(s.c_str(), nullptr);
-  } else {
-    std::memcpy(buf, b, n);
-    buf[n] = 0;
-    out = std::strtod(buf, nullptr);
-  }
+  a = decimal_value(false, w1, k1, -f1, b1, e1);
+  v = decimal_value(false, w2, k2, -f2, b2, e2);
+  p = q;
   return true;
 }
 
@@ -208,6 +277,15 @@ void parse_range(const char* b, const char* e, Chunk& C) {
   const char* p = b;
   auto fail = [&](const char* why) { if (C.error.empty()) C.error = std::string("fallback: ") + why; };
   while (p < e && C.error.empty()) {
+    if (have && !stored && (unsigned)(*p - '0') <= 9u) {  // the common peak line in one pass
+      double a, v;
+      if (fast_peak_line(p, e, true, a, v)) {
+        C.mz.push_back(a);
+        C.it.push_back(v);
+        ++cur_np;
+        continue;
+      }
+    }
     const char *ls, *le;  // universal newlines, like Python text mode: \n, \r\n or \r
     if (!next_line(p, e, ls, le)) { fail("non-ASCII text"); break; }
     const size_t n = (size_t)(le - ls);
@@ -313,6 +391,15 @@ void parse_range_general(const char* b, const char* e, GenChunk& C) {
   const char* p = b;
   auto fail = [&](const char* why) { if (C.error.empty()) C.error = std::string("fallback: ") + why; };
   while (p < e && C.error.empty()) {
+    if (inside && (unsigned)(*p - '0') <= 9u) {  // the common peak line in one pass
+      double a, v;
+      if (fast_peak_line(p, e, false, a, v)) {
+        C.mz.push_back(a);
+        C.it.push_back(v);
+        ++cur_np;
+        continue;
+      }
+    }
     const char *ls, *le;
     if (!next_line(p, e, ls, le)) { fail("non-ASCII text"); break; }
     const char *sb = ls, *se = le;

@@ -263,3 +263,42 @@ def test_native_grouping_equals_ingest_groupings(name, tmp_path):
         np.testing.assert_array_equal(got[1], want[1])
         np.testing.assert_array_equal(got[2], want[2])
         assert [flat.title(s) for s in range(len(flat["key"]))] == flat["titles"]
+
+
+def test_float_parse_equals_python_float(tmp_path):
+    """parse_float (csrc/mgf_io.cpp) == Python float() bit for bit on the number
+    shapes that take each of its three paths: short decimals (Clinger), 16-19
+    significant digits (the x87 extended step: repr of random doubles over many
+    decades, decimals next to double rounding midpoints), and long / huge-exponent
+    forms (strtod)."""
+    rng = np.random.default_rng(11)
+    vals = []
+    x = np.concatenate([rng.uniform(50, 3000, 40000), rng.lognormal(3, 3, 40000),
+                        10.0 ** rng.uniform(-20, 25, 40000)])
+    vals += [repr(float(v)) for v in x]
+    vals += [f"{v:.19g}" for v in x[:20000]]  # 19 digits: w up to 10^19
+    vals += [f"{v:.18e}" for v in x[20000:30000]]
+    # decimals halfway between adjacent doubles (exact midpoints) and a hair off them
+    for v in x[:6000]:
+        a = float(v)
+        b = float(np.nextafter(a, np.inf))
+        from decimal import Decimal, getcontext
+        getcontext().prec = 40
+        mid = (Decimal(a) + Decimal(b)) / 2
+        for d in (mid, mid.next_plus(), mid.next_minus()):
+            vals.append(format(d.quantize(Decimal(1).scaleb(-17)) if abs(d) < 1e3 else d, "f")[:21])
+    vals += ["0", "0.0", "-0.0", "123456789012345678901234.5", "1e300", "2.5e-310", "1" * 25, "9007199254740993",
+             "9007199254740992.5", "18446744073709551615", "0.1", "-17.25"]
+    path = tmp_path / "floats.mgf"
+    with open(path, "w") as fh:
+        for i in range(0, len(vals), 500):
+            fh.write(f"BEGIN IONS\nTITLE=c;s{i}\nPEPMASS=500.0\nCHARGE=2+\n")
+            for v in vals[i:i + 500]:
+                fh.write(f"{1 + i % 7} {v}\n")
+            fh.write("END IONS\n")
+    d = mgf_native.parse_general(str(path))
+    want = np.array([float(v) for v in vals])
+    got = d["inten"]
+    assert len(got) == len(want)
+    bad = np.flatnonzero(got.view(np.uint64) != want.view(np.uint64))
+    assert len(bad) == 0, [(vals[i], got[i], want[i]) for i in bad[:5]]
