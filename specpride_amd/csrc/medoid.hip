@@ -229,7 +229,9 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   __syncthreads();
   if (tid < kWave) {  // n <= 64: wave 0 holds every spectrum
     const bool empty_spec = tid < n && L.soff[tid + 1] == L.soff[tid];
-    if (tid == 0) L.red[1] = __ballot(empty_spec) != 0ull;
+    // the whole wave votes (a ballot inside `if (tid == 0)` would see lane 0 only)
+    const unsigned long long any_empty = __ballot(empty_spec);
+    if (tid == 0) L.red[1] = any_empty != 0ull;
   }
   for (int j = 1 + tid; j < n; j += BLOCK) {
     const int r = L.soff[j];

@@ -577,3 +577,28 @@ def test_bin_mean_kept_fold(gpu):
     csr = _concat(make_clusters_np(20, seed=73), *parts, special, mixed, uns, make_clusters_np(20, seed=74))
     for q in (True, False):
         assert_bin_mean_equal(_bin_mean(csr, apply_peak_quorum=q), c_oracle.bin_mean(csr, apply_peak_quorum=q))
+
+
+def test_medoid_empty_spectrum_positions(gpu):
+    """Empty spectra at every position of small clusters (register kernel), of a
+    wide-kernel cluster (600-peak spectra) and of an MFMA-path cluster (n > 64):
+    an empty spectrum shares its start offset with the next one, so the peak ->
+    spectrum map must not count start offsets (the fuzz test's find: the empty-spectrum
+    vote saw lane 0 only).  Representatives and totals bit-exact vs the oracle."""
+    rng = np.random.default_rng(77)
+    clusters = []
+
+    def spec(n):
+        return {"m/z array": np.sort(rng.uniform(100, 2000, n)), "intensity array": rng.lognormal(3, 1, n),
+                "precursor mz": 500.0, "precursor charge": 2}
+
+    for n in (2, 3, 5, 9, 26, 50, 64):
+        for empties in ([0], [1], [n // 2], [n - 1], [1, 2], list(range(1, n, 3))):
+            clusters.append([spec(0) if j in empties else spec(int(rng.integers(150, 250))) for j in range(n)])
+    clusters.append([spec(0) if j in (1, 7) else spec(600) for j in range(30)])   # wide kernel
+    clusters.append([spec(0) if j in (1, 40) else spec(120) for j in range(90)])  # large path
+    csr = SpectraCSR.from_clusters(clusters)
+    rep, tot = engine.medoid(engine.DeviceBatch.from_host(csr), with_totals=True).to_host()
+    ref_rep, ref_tot = c_oracle.medoid(csr, with_totals=True)
+    np.testing.assert_array_equal(rep, ref_rep)
+    np.testing.assert_array_equal(tot, ref_tot)
