@@ -4,11 +4,13 @@ values and totals included; gap-average group structure exact, values within
 GAP_RTOL).  Each case draws cluster sizes (1..300, heavy tails), spectrum lengths
 (1..900 template peaks), and mutations the reference meets in real files: m/z
 snapped to a coarse grid (several peaks per bin, exact m/z ties), unsorted
-spectra, empty spectra, a mixed-charge cluster, and non-default bin parameters."""
+spectra, empty spectra, a mixed-charge cluster, m/z past the medoid's register
+range and bin range, zero intensities, and non-default bin-mean / gap-average
+parameters; the binned cosine, xcorr distance and best score ride along."""
 import numpy as np
 import pytest
 
-from oracle import c_oracle
+from oracle import c_oracle, np_oracle
 from specpride_amd import engine
 from specpride_amd.csr import SpectraCSR
 from specpride_amd.synthetic import make_clusters_np
@@ -16,7 +18,7 @@ from test_gpu_parity import assert_bin_mean_equal, assert_gap_close
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 24
+N_CASES = 40
 
 
 def _case(seed):
@@ -48,6 +50,15 @@ def _case(seed):
         s0, s1 = csr.cluster_off[c], csr.cluster_off[c + 1]
         if s1 - s0 > 1:
             charge[s1 - 1] = charge[s0] + 1
+    if rng.random() < 0.25:  # m/z past the medoid's register bitmap (3,276.8) and bin range (6,553.6)
+        far = rng.choice(len(mz), max(1, len(mz) // 200), replace=False)
+        mz[far] = rng.choice([3300.0, 7000.0, 15000.0]) + rng.uniform(0, 50, len(far))
+        for s in range(csr.n_spectra):
+            a, b = so[s], so[s + 1]
+            o = np.argsort(mz[a:b], kind="stable")
+            mz[a:b], it[a:b] = mz[a:b][o], it[a:b][o]
+    if rng.random() < 0.2:  # zero intensities
+        it[rng.choice(len(it), max(1, len(it) // 50), replace=False)] = 0.0
     keep_spec = np.ones(csr.n_spectra, bool)
     if rng.random() < 0.3:  # empty spectra (their peaks dropped)
         keep_spec[rng.choice(csr.n_spectra, max(1, csr.n_spectra // 10), replace=False)] = False
@@ -85,5 +96,43 @@ def test_fuzz_medoid(gpu, seed):
 @pytest.mark.parametrize("seed", range(N_CASES))
 def test_fuzz_gap_average(gpu, seed):
     csr, _ = _case(seed)
-    got = engine.gap_average(engine.DeviceBatch.from_host(csr)).to_host()
-    assert_gap_close(got, c_oracle.gap_average(csr), 1000.0)
+    batch = engine.DeviceBatch.from_host(csr)
+    rng = np.random.default_rng(2000 + seed)
+    for kw in (dict(), dict(mz_accuracy=float(rng.choice([0.005, 0.02, 0.05])),
+                            dyn_range=float(rng.choice([10.0, 100.0, 1e4])),
+                            min_fraction=float(rng.choice([0.1, 0.3, 0.8])))):
+        got = engine.gap_average(batch, **kw).to_host()
+        assert_gap_close(got, c_oracle.gap_average(csr, **kw), kw.get("dyn_range", 1000.0))
+
+
+@pytest.mark.parametrize("seed", range(0, N_CASES, 2))
+def test_fuzz_cosine_xcorr_best(gpu, seed):
+    """The side entry points on the same batches: the binned cosine of each
+    cluster's bin-mean consensus vs its members (<= 1e-12 rel), the xcorr distance
+    of random spectrum pairs (exact), the best-score argmax (exact)."""
+    import torch
+
+    csr, _ = _case(seed)
+    batch = engine.DeviceBatch.from_host(csr)
+    cons = engine.bin_mean(batch).to_host()
+    dev = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda:0")  # noqa: E731
+    cos, avg, st = engine.binned_cosine(batch, dev(cons["out_off"]), dev(cons["out_mz"]),
+                                        dev(cons["out_int"])).to_host()
+    wcos, wavg, wst = np_oracle.binned_cosine(csr, cons["out_off"], cons["out_mz"], cons["out_int"])
+    C = csr.n_clusters
+    np.testing.assert_array_equal(st[:C], wst)
+    ok = wst == 0
+    np.testing.assert_allclose(avg[:C][ok], wavg[ok], rtol=1e-12)
+    rng = np.random.default_rng(3000 + seed)
+    pairs = rng.integers(0, csr.n_spectra, (min(500, csr.n_spectra * 3), 2))
+    d = engine.xcorr_distance(batch, dev(pairs)).cpu().numpy()
+    so = csr.spec_off
+    want = np.array([1.0 - np_oracle.xcorr(csr.mz[so[a]:so[a + 1]], csr.mz[so[b]:so[b + 1]]) for a, b in pairs])
+    np.testing.assert_array_equal(d, want)
+    score = rng.integers(0, 4, csr.n_spectra).astype(np.float64)
+    score[rng.random(csr.n_spectra) < 0.1] = np.nan
+    rank = rng.permutation(csr.n_spectra).astype(np.int64)
+    best, bst = engine.best_score(dev(csr.cluster_off), dev(score), dev(rank)).to_host()
+    wbest, wbst = np_oracle.best_score(csr.cluster_off, score, rank)
+    np.testing.assert_array_equal(best[:C], wbest)
+    np.testing.assert_array_equal(bst[:C], wbst)
