@@ -302,3 +302,81 @@ def test_float_parse_equals_python_float(tmp_path):
     assert len(got) == len(want)
     bad = np.flatnonzero(got.view(np.uint64) != want.view(np.uint64))
     assert len(bad) == 0, [(vals[i], got[i], want[i]) for i in bad[:5]]
+
+
+def _rand_num(rng, v, allow_exotic):
+    forms = [lambda: f"{v:.5f}", lambda: repr(float(v)), lambda: f"{v:.2f}", lambda: str(int(v)),
+             lambda: f"{v:.17g}", lambda: f"{v:.8f}".rstrip("0")]
+    if allow_exotic:
+        forms += [lambda: f"{v:.3e}", lambda: f"+{v:.4f}", lambda: f"{v:.4E}", lambda: f"{int(v)}."]
+    return forms[int(rng.integers(0, len(forms)))]()
+
+
+def _rand_mgf(rng, general):
+    """Random MGF text in the shapes real files take: CRLF / CR / LF line ends,
+    trailing blanks, extra peak fields, tab or double separators, exotic number
+    forms, optional params, blank lines."""
+    eol = ["\n", "\r\n", "\r"][int(rng.integers(0, 3))] if rng.random() < 0.3 else "\n"
+    out = []
+    for k in range(int(rng.integers(1, 6))):
+        out.append("BEGIN IONS")
+        out.append(f"TITLE=cluster-{k % 3};mzspec:X:{k}" + (" " if rng.random() < 0.1 else ""))
+        if rng.random() < 0.9:
+            out.append("PEPMASS=" + _rand_num(rng, rng.uniform(300, 1500), rng.random() < 0.3))
+        if rng.random() < 0.9:
+            out.append("CHARGE=" + ["2+", "3+", "2", " 2+ "][int(rng.integers(0, 4))])
+        if rng.random() < 0.5:
+            out.append("RTINSECONDS=" + _rand_num(rng, rng.uniform(0, 3600), False))
+        for _ in range(int(rng.integers(0, 30))):
+            a = _rand_num(rng, rng.uniform(100, 2000), rng.random() < 0.05)
+            b = _rand_num(rng, rng.lognormal(3, 2), rng.random() < 0.05)
+            r = rng.random()
+            if general:
+                sep = " " if r < 0.85 else ["\t", "  ", " \t"][int(rng.integers(0, 3))]
+            else:
+                sep = " " if r < 0.97 else ["\t", "  "][int(rng.integers(0, 2))]
+            line = a + sep + b
+            if rng.random() < 0.05:
+                line += " 7"
+            if rng.random() < 0.05:
+                line += " "
+            out.append(line)
+            if rng.random() < 0.02:
+                out.append("")
+        out.append("END IONS")
+        out.append("")
+    return eol.join(out) + eol
+
+
+@pytest.mark.parametrize("general", [False, True])
+def test_random_mgf_text_native_equals_python(tmp_path, general):
+    """Native parse == the Python reader on 300 random files per grammar: equal
+    values (bit for bit) where the native subset applies, the Python reader's own
+    result or exception otherwise (the CLIs' fallback)."""
+    rng = np.random.default_rng(5 + general)
+    n_native = 0
+    for i in range(300):
+        p = tmp_path / f"r{i}.mgf"
+        p.write_bytes(_rand_mgf(rng, general).encode())
+        if general:
+            try:
+                mgf_native.parse_general(str(p))
+            except ValueError as e:
+                assert "fallback" in str(e)
+                continue
+            _check_general_equal(str(p))
+            n_native += 1
+        else:
+            try:
+                want = mgf_native._read_binning_py(str(p))
+            except Exception as e:  # noqa: BLE001 -- the reference's own exception
+                with pytest.raises(type(e)):
+                    mgf_native.read_binning_mgf(str(p))
+                continue
+            assert mgf_native.read_binning_mgf(str(p)) == want
+            try:
+                mgf_native.parse_native(str(p))
+                n_native += 1
+            except ValueError:
+                pass
+    assert n_native > 100  # most files take the native path
