@@ -19,7 +19,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-STAMPS_LIB = os.path.join(REPO, "specpride_amd", "lib", "libspecpride_hip_stamps.so")
+STAMPS_LIB = os.environ.get("SPX_STAMPS_LIB") or os.path.join(REPO, "specpride_amd", "lib", "libspecpride_hip_stamps.so")
 
 
 def build_stamps():
