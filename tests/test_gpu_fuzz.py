@@ -91,6 +91,11 @@ def test_fuzz_medoid(gpu, seed):
     ref_rep, ref_tot = c_oracle.medoid(csr, with_totals=True)
     np.testing.assert_array_equal(rep, ref_rep)
     np.testing.assert_array_equal(tot, ref_tot)
+    tol = float(np.random.default_rng(4000 + seed).choice([0.02, 0.05, 0.3, 1.0]))  # other xcorr tolerances
+    rep, tot = engine.medoid(engine.DeviceBatch.from_host(csr), tolerance=tol, with_totals=True).to_host()
+    ref_rep, ref_tot = c_oracle.medoid(csr, tol=tol, with_totals=True)
+    np.testing.assert_array_equal(rep, ref_rep)
+    np.testing.assert_array_equal(tot, ref_tot)
 
 
 @pytest.mark.parametrize("seed", range(N_CASES))
