@@ -141,3 +141,41 @@ def test_fuzz_cosine_xcorr_best(gpu, seed):
     wbest, wbst = np_oracle.best_score(csr.cluster_off, score, rank)
     np.testing.assert_array_equal(best[:C], wbest)
     np.testing.assert_array_equal(bst[:C], wbst)
+
+
+@pytest.mark.parametrize("seed", range(1, N_CASES, 2))
+def test_fuzz_precursor_modes(gpu, seed):
+    """The gap-average CLI's precursor choices (average_spectrum_clustering.py:106-148,
+    --pepmass / --rt) on the fuzz batches, cluster by cluster against the numpy
+    restatement of the reference helpers: pepmass, charge and RT bit-exact
+    (tie-free masses: the reference's argsort is unstable on ties past 16)."""
+    csr, _ = _case(seed)
+    # the synthetic precursors repeat within a cluster (5 decimals); a tie in the
+    # neutral masses makes the reference's pick depend on numpy's unstable argsort
+    # (and on the host's SIMD sort), so the masses are made distinct here
+    csr = SpectraCSR(csr.cluster_off, csr.spec_off, csr.mz, csr.inten,
+                     csr.prec_mz + 1e-7 * np.arange(csr.n_spectra), csr.charge, csr.rt)
+    batch = engine.DeviceBatch.from_host(csr)
+    co = csr.cluster_off
+    H = engine.PROTON
+    for pm, rtm in (("lower_median", "mass_lower_median"), ("lower_median", "median"),
+                    ("neutral_average", "median"), ("naive_average", "mass_lower_median")):
+        got = engine.gap_average(batch, pepmass=pm, rt=rtm).to_host()
+        for c in range(csr.n_clusters):
+            s0, s1 = co[c], co[c + 1]
+            if s1 == s0:
+                continue
+            prec, ch, rt = csr.prec_mz[s0:s1], csr.charge[s0:s1], csr.rt[s0:s1]
+            if pm == "naive_average":
+                want = np_oracle.naive_average_mass_and_charge(prec, ch)
+                if want is None:
+                    assert got["status"][c] == engine.STATUS_MIXED_CHARGE, c
+                    continue
+            elif pm == "neutral_average":
+                want = np_oracle.neutral_average_mass_and_charge(prec, ch, H)
+            else:
+                want = np_oracle.lower_median_mass(prec, ch, H)
+            wrt = (np_oracle.lower_median_mass_rt(prec, ch, rt, H) if rtm == "mass_lower_median"
+                   else np_oracle.median_rt(rt))
+            assert got["prec"][c] == want[0] and got["charge"][c] == want[1], (pm, c)
+            assert got["rt"][c] == wrt or (np.isnan(wrt) and np.isnan(got["rt"][c])), (rtm, c)
