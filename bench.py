@@ -438,6 +438,35 @@ def bin_mean_shapes(args, out):
     out["bin_mean_shapes"] = res
 
 
+def gap_average_shapes(args, out):
+    """Gap-average off the headline's shape, the same batches as bin_mean_shapes:
+    600-peak spectra (thousands of occupied 0.01-Da buckets per cluster: the wide
+    kernel) and the configs[3] skewed law (its n = 5,000 giants: the global kernel)."""
+    import torch
+
+    from specpride_amd import engine
+    from specpride_amd.synthetic import make_clusters_torch
+
+    res = {}
+    for name, kw in (("skewed_config3", dict(n_clusters=20000, seed=4, skewed=True, forced_large=4, large_size=5000)),
+                     ("long_spectra_600", dict(n_clusters=20000, seed=6, n_template=600))):
+        t = make_clusters_torch(**kw)
+        batch = engine.DeviceBatch.from_device(t)
+        ga = engine.gap_average(batch)
+        torch.cuda.synchronize()
+        st = ga.status.cpu().numpy()[:batch.n_clusters]
+        kept = int(ga.count[:batch.n_clusters].sum().item())
+        ms = time_launches(lambda: engine.gap_average(batch, out=ga), 3, torch.cuda.current_stream())
+        res[name] = {"clusters": batch.n_clusters, "peaks": batch.n_peaks, "ms": round(ms, 3),
+                     "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1),
+                     "ok_clusters": int((st == 0).sum()),
+                     "roofline": roofline("spx_gap_average", "all gap-average kernels", consensus_bytes(batch, kept),
+                                          ms)}
+        del ga, batch, t
+        torch.cuda.empty_cache()
+    out["gap_average_shapes"] = res
+
+
 def tier2(args, out):
     """SURVEY.md §8(d) tier 2 at the headline's size (configs[4], 385k clusters, a
     32 GB packed host CSR in pageable memory): H2D (engine.DeviceBatch.from_host:
@@ -493,6 +522,7 @@ def main():
         config3(args, out)
         bin_mean_shapes(args, out)
         medoid_shapes(args, out)
+        gap_average_shapes(args, out)
         tier2(args, out)
         if args.ns_clusters > 0:
             north_star(args, out)

@@ -87,18 +87,24 @@ struct GapState {
   int wcap, dcap;
 };
 
-struct GapSmem {
+template <int DCAP>
+struct GapSmemT {
   unsigned long long bitmap[GA_WMAX];
   uint16_t wprefix[GA_WMAX];
-  uint32_t cnt[GA_DCAP];
-  uint32_t gcnt[GA_DCAP];
-  uint64_t kmin[GA_DCAP];
-  uint64_t kmax[GA_DCAP];
+  uint32_t cnt[DCAP];
+  uint32_t gcnt[DCAP];
+  uint64_t kmin[DCAP];
+  uint64_t kmax[DCAP];
   int tmp[GA_BLOCK / kWave + 1];
   int votes[2 * GA_NW];
   double red[GA_BLOCK / kWave * 3];
   int prank[2 * GA_NW * kWave];  // per-wave partial precursor ranks (mass, RT)
 };
+using GapSmem = GapSmemT<GA_DCAP>;
+// The wide kernel (what the LDS kernel defers for its bucket cap: spectra of hundreds of
+// peaks give clusters thousands of occupied 0.01-Da buckets): 4,608 slots, 147 KB of
+// LDS, one workgroup per CU
+constexpr int GA_WDCAP = 4608;
 
 __device__ __forceinline__ double nan_d() { return __longlong_as_double(0x7ff8000000000000ll); }
 
@@ -625,7 +631,7 @@ __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P,
 __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v, GapParams P, PeaksOut out,
                                                                    double* prec_out, int32_t* charge_out,
                                                                    double* rt_out, int32_t* status,
-                                                                   int32_t* deferred, int32_t* n_deferred) {
+                                                                   StripedList deferred) {
   __shared__ GapSmem L;
   const int64_t c = blockIdx.x;
   SPX_STAMP(0);
@@ -637,12 +643,39 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   if (st == kDeferred) {
     if (threadIdx.x == 0) {
       status[c] = kDeferred;
-      deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+      striped_push(deferred, (int32_t)c);
     }
     return;
   }
   gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank);
   SPX_STAMP(7);
+}
+
+// The LDS kernel's leftovers (striped list), grid-stride, one 147 KB workgroup per
+// CU; what this one cannot hold either (a bucket range past the bitmap, more than
+// GA_WDCAP buckets, a bucket spanning mz_accuracy) goes on to the global kernel.
+__global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v, GapParams P, PeaksOut out,
+                                                                    double* prec_out, int32_t* charge_out,
+                                                                    double* rt_out, int32_t* status,
+                                                                    StripedList list, int32_t* deferred,
+                                                                    int32_t* n_deferred) {
+  __shared__ GapSmemT<GA_WDCAP> L;
+  __shared__ int32_t lbase[kListStripes + 1];
+  const int32_t nl = striped_prefix(list, lbase);
+  GapState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.gcnt, L.kmin, L.kmax, GA_WMAX, GA_WDCAP};
+  for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
+    const int64_t c = striped_at(list, lbase, i);
+    const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
+    PrecLanes pl{0, 0.0, 0.0};
+    if (pn <= kWave) pl = prec_lanes(v, ps0, pn);
+    const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
+    if (st == kDeferred) {
+      if (threadIdx.x == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;  // status stays kDeferred
+    } else {
+      gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank);
+    }
+    __syncthreads();  // the LDS is reused by the next cluster
+  }
 }
 
 // Scratch slice of the deferred path: every array starts 256-B aligned (the

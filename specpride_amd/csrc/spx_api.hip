@@ -372,7 +372,9 @@ size_t spx_gap_average_workspace_size(const spx_csr* csr, const spx_gap_params* 
   if (!csr || !params || !info) return 0;
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
-  return align256(sizeof(int32_t)) * 2 + align256(sizeof(int32_t) * (size_t)std::max<int64_t>(C, 1)) +
+  const size_t Cm = (size_t)std::max<int64_t>(C, 1);
+  return align256(sizeof(int32_t)) * 2 + align256(spx::kListCountBytes) + align256(sizeof(int32_t) * Cm) +
+         align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
          (size_t)gap_fallback_grid(C, params, info) *
              (size_t)spx::gap_slice_bytes(gap_wcap(params, info), (int)std::min<int64_t>(dcap, INT32_MAX));
 }
@@ -393,7 +395,11 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
   int32_t* n_def = w.take<int32_t>(1);
   int32_t* unresolved = w.take<int32_t>(1);
-  int32_t* def = w.take<int32_t>((size_t)C);
+  spx::StripedList wide;  // the LDS kernel's leftovers for the wide kernel
+  wide.counts = w.take<int32_t>((size_t)spx::kListStripes * spx::kListLine);
+  wide.cap = spx::striped_cap(C);
+  int32_t* def = w.take<int32_t>((size_t)C);  // the wide kernel's leftovers for the global kernel
+  wide.items = w.take<int32_t>((size_t)wide.cap * spx::kListStripes);
   char* scratch = w.base + w.used;
   spx::GapParams P;
   P.mz_accuracy = params->mz_accuracy;
@@ -409,10 +415,15 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   const int wcap = gap_wcap(params, info);
   const int dcap = (int)std::min<int64_t>(std::max<int64_t>(1, info->max_cluster_peaks), INT32_MAX);
 
-  if (hipMemsetAsync(n_def, 0, 512, s) != hipSuccess) return check_launch("spx_gap_average memset");
+  // n_def, unresolved and the striped list's counters: the first 512 B + kListCountBytes
+  if (hipMemsetAsync(n_def, 0, 512 + spx::kListCountBytes, s) != hipSuccess)
+    return check_launch("spx_gap_average memset");
   hipLaunchKernelGGL(spx::gap_average_lds_kernel, dim3((unsigned)C), dim3(spx::GA_BLOCK), 0, s, V, P, O, pepmass_out,
-                     charge_out, rt_out, status, def, n_def);
+                     charge_out, rt_out, status, wide);
   if (int rc = check_launch("gap_average_lds_kernel")) return rc;
+  hipLaunchKernelGGL(spx::gap_average_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 256))),
+                     dim3(spx::GA_BLOCK), 0, s, V, P, O, pepmass_out, charge_out, rt_out, status, wide, def, n_def);
+  if (int rc = check_launch("gap_average_wide_kernel")) return rc;
   spx::GapParams P2 = P;  // half-width buckets: no gap can hide inside one
   P2.bucket_w = params->mz_accuracy * 0.5;
   P2.inv_bucket_w = 1.0 / P2.bucket_w;

@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--medoid", action="store_true")
+    ap.add_argument("--gap", action="store_true")
     ap.add_argument("--shapes", default="skewed_config3,long_spectra_600")
     a = ap.parse_args()
     res = {}
@@ -53,6 +54,15 @@ def main():
             res[f"md_{name}_ms"] = round(ms, 4)
             res[f"md_{name}_digest"] = digest(md.rep[:C])
             del md
+        if a.gap:
+            ga = engine.gap_average(batch)
+            torch.cuda.synchronize()
+            ms = bench.time_launches(lambda: engine.gap_average(batch, out=ga), a.reps, torch.cuda.current_stream())
+            res[f"ga_{name}_ms"] = round(ms, 4)
+            r = ga.to_host()
+            res[f"ga_{name}_ok"] = int((r["status"] == 0).sum())
+            res[f"ga_{name}_frac"] = round(bench.consensus_bytes(batch, int(r["out_off"][-1])) / (ms * 1e-3) / 8e12, 4)
+            del ga
         del batch, t
         torch.cuda.empty_cache()
     print(json.dumps(res))
