@@ -98,9 +98,11 @@ struct GapSmemT {
   int tmp[GA_BLOCK / kWave + 1];
   int votes[2 * GA_NW];
   double red[GA_BLOCK / kWave * 3];
-  int prank[2 * GA_NW * kWave];  // per-wave partial precursor ranks (mass, RT)
+  int prank[2 * GA_NW * kWave];  // per-wave partial precursor ranks (mass, RT); n > 64: the rank stage
+  long long sel[4];              // n > 64: prec_select_block's picks
 };
 using GapSmem = GapSmemT<GA_DCAP>;
+static_assert(sizeof(GapSmem::prank) >= GA_BLOCK * sizeof(double), "the rank stage fits the prank words");
 // The wide kernel (what the LDS kernel defers for its bucket cap: spectra of hundreds of
 // peaks give clusters thousands of occupied 0.01-Da buckets): 4,608 slots, 147 KB of
 // LDS, one workgroup per CU
@@ -220,7 +222,10 @@ __device__ PrecSummary precursor_summary_wave(const PrecLanes& pl, int n, const 
 
 // Run by one whole wave.  Ranks are stable (ties by index), which is what
 // numpy's argsort returns for n <= 16 and for tie-free input.
-__device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n, const GapParams& P) {
+// sel (optional): the ranks' picks, computed block-wide by prec_select_block --
+// sel[0] the lower-median mass index, sel[1] / sel[2] the RT ranks (n-1)//2 and n//2.
+__device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n, const GapParams& P,
+                                         const long long* sel = nullptr) {
   if (n <= kWave) return precursor_summary_wave(prec_lanes(v, s0, n), (int)n, P);
   PrecSummary R;
   const int lane = lane_id();
@@ -231,8 +236,8 @@ __device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n
   };
   // lower-median index of the neutral masses: rank == (n-1)//2
   const int64_t want = (n - 1) / 2;
-  int64_t lm = -1;
-  for (int64_t i0 = 0; i0 < n; i0 += kWave) {
+  int64_t lm = sel ? (int64_t)sel[0] : -1;
+  for (int64_t i0 = 0; !sel && i0 < n; i0 += kWave) {
     const int64_t i = i0 + lane;
     int64_t rank = -1;
     if (i < n) {
@@ -249,7 +254,10 @@ __device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n
   // median RT (np.median): middle element(s) of the sorted values
   double rt_lo = 0.0, rt_hi = 0.0;
   const int64_t k_lo = (n - 1) / 2, k_hi = n / 2;
-  if (P.rt_mode == 0) {
+  if (P.rt_mode == 0 && sel) {
+    rt_lo = v.rt[s0 + sel[1]];
+    rt_hi = v.rt[s0 + sel[2]];
+  } else if (P.rt_mode == 0) {
     for (int64_t i0 = 0; i0 < n; i0 += kWave) {
       const int64_t i = i0 + lane;
       int64_t rank = -1;
@@ -300,6 +308,44 @@ __device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n
     if (isnan(rt_lo) || isnan(rt_hi)) R.rt = nan_d();
   }
   return R;
+}
+
+// The O(n^2) stable ranks of precursor_summary for n > 64, spread over the whole
+// block instead of one wave (the skewed law's n = 5,000 giants spent ~58 ms of a
+// 78 ms batch in the one-wave loops): each thread ranks its i's against every j,
+// the j's staged through `stage` (GA_BLOCK doubles of LDS).  Same comparisons, so
+// the same picks: sel[0] = the lower-median mass index, sel[1] / sel[2] = the RT
+// ranks (n-1)//2 and n//2 (rt_mode 0).  Ranks are unique (ties by index), so each
+// pick has one writer.  Call with the whole block; ends with a barrier.
+__device__ void prec_select_block(const CsrView& v, int64_t s0, int64_t n, const GapParams& P, double* stage,
+                                  long long* sel) {
+  const int tid = threadIdx.x;
+  const double H = P.proton;
+  auto pass = [&](auto value, int64_t want0, int64_t want1, long long* out0, long long* out1) {
+    for (int64_t i0 = 0; i0 < n; i0 += GA_BLOCK) {  // uniform
+      const int64_t i = i0 + tid;
+      const double xi = i < n ? value(i) : 0.0;
+      int64_t rank = 0;
+      for (int64_t j0 = 0; j0 < n; j0 += GA_BLOCK) {  // uniform
+        __syncthreads();  // the previous chunk is consumed
+        stage[tid] = j0 + tid < n ? value(j0 + tid) : 0.0;
+        __syncthreads();
+        const int m = (int)(n - j0 < GA_BLOCK ? n - j0 : GA_BLOCK);
+        for (int k = 0; k < m; ++k) {
+          const double xj = stage[k];
+          rank += lt_nan_last(xj, xi) || (!lt_nan_last(xi, xj) && j0 + k < i);
+        }
+      }
+      if (i < n && rank == want0) *out0 = i;
+      if (out1 && i < n && rank == want1) *out1 = i;
+    }
+  };
+  pass([&](int64_t i) {
+    const double z = (double)v.charge[s0 + i];
+    return v.prec_mz[s0 + i] * z - z * H;  // (m*c - c*H), no contraction: precursor_summary's mass
+  }, (n - 1) / 2, -1, &sel[0], nullptr);
+  if (P.rt_mode == 0) pass([&](int64_t i) { return v.rt[s0 + i]; }, (n - 1) / 2, n / 2, &sel[1], &sel[2]);
+  __syncthreads();
 }
 
 // Every peak of [p0, p1) once, GA_BATCH loads in flight per thread (indices
@@ -599,9 +645,12 @@ template <class PrefixT>
 __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P, int64_t c, int32_t st,
                                            const PeaksOut& out, double* prec_out, int32_t* charge_out,
                                            double* rt_out, int32_t* status, const PrecLanes* pl = nullptr,
-                                           const int* prank = nullptr) {
+                                           const int* prank = nullptr, double* stage = nullptr,
+                                           long long* sel = nullptr) {
   const int64_t s0 = v.cluster_off[c], n = v.cluster_off[c + 1] - s0;
   if (st == kDeferred) return;
+  const bool big = n > kWave && stage != nullptr;  // uniform
+  if (big) prec_select_block(v, s0, n, P, stage, sel);
   if (wave_id() == 0) {
     PrecSummary R{nan_d(), nan_d(), 0, kOk};
     if (prank && pl && n > 0 && n <= kWave) {
@@ -614,7 +663,8 @@ __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P,
       }
       R = precursor_summary_wave(*pl, (int)n, P, &K);
     } else if (n > 0) {
-      R = (pl && n <= kWave) ? precursor_summary_wave(*pl, (int)n, P) : precursor_summary(v, s0, n, P);
+      R = (pl && n <= kWave) ? precursor_summary_wave(*pl, (int)n, P)
+                             : precursor_summary(v, s0, n, P, big ? sel : nullptr);
     }
     if (lane_id() == 0) {
       // the reference computes the precursor first (:161-163): its error wins
@@ -647,7 +697,8 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
     }
     return;
   }
-  gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank);
+  gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank,
+                       reinterpret_cast<double*>(L.prank), L.sel);
   SPX_STAMP(7);
 }
 
@@ -672,7 +723,8 @@ __global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v
     if (st == kDeferred) {
       if (threadIdx.x == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;  // status stays kDeferred
     } else {
-      gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank);
+      gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank,
+                           reinterpret_cast<double*>(L.prank), L.sel);
     }
     __syncthreads();  // the LDS is reused by the next cluster
   }
@@ -707,6 +759,8 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
   __shared__ int tmp[GA_BLOCK / kWave + 1];
   __shared__ int votes[2 * GA_NW];
   __shared__ double red[GA_BLOCK / kWave * 3];
+  __shared__ double stage[GA_BLOCK];
+  __shared__ long long sel[4];
   char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
   const GapSliceLayout Lo = gap_slice_layout(wcap, dcap);
   GapState<uint32_t> S;
@@ -727,7 +781,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
       // reported, never approximated (the host re-runs it through the sort path)
       if (threadIdx.x == 0) { status[c] = kDeferred; atomicAdd(unresolved, 1); }
     } else {
-      gap_finish<uint32_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status);
+      gap_finish<uint32_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, nullptr, nullptr, stage, sel);
     }
     __syncthreads();
   }
