@@ -103,6 +103,8 @@ struct GapSmemT {
 };
 using GapSmem = GapSmemT<GA_DCAP>;
 static_assert(sizeof(GapSmem::prank) >= GA_BLOCK * sizeof(double), "the rank stage fits the prank words");
+static_assert(GA_BLOCK * sizeof(double) >= (264 + GA_BLOCK / 64 + 1) * 4, "the radix select's words fit the stage");
+static_assert(GA_BLOCK >= 256, "one thread per radix bucket");
 // The wide kernel (what the LDS kernel defers for its bucket cap: spectra of hundreds of
 // peaks give clusters thousands of occupied 0.01-Da buckets): 4,608 slots, 147 KB of
 // LDS, one workgroup per CU
@@ -215,7 +217,7 @@ __device__ PrecSummary precursor_summary_wave(const PrecLanes& pl, int n, const 
     R.rt = readlane_f64(ri, lm);
   } else {
     R.rt = (n & 1) ? rt_lo : (0.0 + rt_lo + rt_hi) / 2.0;
-    if (isnan(rt_lo) || isnan(rt_hi)) R.rt = nan_d();
+    if (__ballot(valid && isnan(ri)) != 0ull) R.rt = nan_d();  // np.median: any NaN -> NaN
   }
   return R;
 }
@@ -305,7 +307,10 @@ __device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n
     R.rt = v.rt[s0 + lm];
   } else {
     R.rt = (n & 1) ? rt_lo : (0.0 + rt_lo + rt_hi) / 2.0;
-    if (isnan(rt_lo) || isnan(rt_hi)) R.rt = nan_d();
+    bool rt_nan = false;  // np.median: any NaN -> NaN (NaN ranks last, so it is rarely a middle pick)
+    for (int64_t i0 = 0; i0 < n && !rt_nan; i0 += kWave)
+      rt_nan = __ballot(i0 + lane < n && isnan(v.rt[s0 + (i0 + lane < n ? i0 + lane : 0)])) != 0ull;
+    if (rt_nan) R.rt = nan_d();
   }
   return R;
 }
@@ -317,10 +322,92 @@ __device__ PrecSummary precursor_summary(const CsrView& v, int64_t s0, int64_t n
 // the same picks: sel[0] = the lower-median mass index, sel[1] / sel[2] = the RT
 // ranks (n-1)//2 and n//2 (rt_mode 0).  Ranks are unique (ties by index), so each
 // pick has one writer.  Call with the whole block; ends with a barrier.
+// lt_nan_last as an unsigned order: -0 and +0 equal, every NaN one key above +inf
+__device__ __forceinline__ uint64_t prec_key(double x) {
+  if (isnan(x)) return ~0ull;
+  return f64_order_key(x == 0.0 ? 0.0 : x);
+}
+
+// The index whose stable rank (lt_nan_last, ties by index) is `want`, for large n:
+// an 8-pass radix select over prec_key (8-bit digits, LDS histogram) finds the
+// want-th smallest key K and how many of K's equal keys precede the pick, then one
+// ordered scan over the K's finds it by index.  O(n) per pass instead of O(n^2):
+// the same element as prec_select_block's rank loops.  ws: 320 words of LDS.
+// Call with the whole block; every thread gets the index.
+template <class F>
+__device__ int64_t prec_radix_select(F value, int64_t n, int64_t want, uint32_t* ws) {
+  const int tid = threadIdx.x;
+  uint32_t* hist = ws;                                          // 256 counts
+  unsigned long long* ctl = reinterpret_cast<unsigned long long*>(ws + 256);  // digit, rank left, pick
+  int* tmp = reinterpret_cast<int*>(ws + 264);                  // GA_NW + 1 scan words
+  uint64_t prefix = 0;
+  int64_t rem = want;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    const uint64_t hmask = shift == 56 ? 0ull : (~0ull << (shift + 8));
+    if (tid < 256) hist[tid] = 0u;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += GA_BLOCK) {
+      const uint64_t k = prec_key(value(i));
+      if ((k & hmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < kWave) {
+      const uint32_t h0 = hist[4 * tid], h1 = hist[4 * tid + 1], h2 = hist[4 * tid + 2], h3 = hist[4 * tid + 3];
+      const int64_t s = (int64_t)h0 + h1 + h2 + h3;
+      const int64_t inc = wave_inclusive_sum<int64_t, false>(s);
+      int64_t c = inc - s;
+      if (c <= rem && rem < inc) {  // one lane: the digit is in its 4 bins
+        int q = 0;
+        if (rem >= c + h0) { c += h0; q = 1; }
+        if (q == 1 && rem >= c + h1) { c += h1; q = 2; }
+        if (q == 2 && rem >= c + h2) { c += h2; q = 3; }
+        ctl[0] = (unsigned long long)(4 * tid + q);
+        ctl[1] = (unsigned long long)(rem - c);
+      }
+    }
+    __syncthreads();
+    prefix |= (uint64_t)ctl[0] << shift;
+    rem = (int64_t)ctl[1];
+  }
+  // K = prefix; the pick is the rem-th (0-based) element with key K in index order
+  int64_t base = 0;
+  for (int64_t i0 = 0; i0 < n && base <= rem; i0 += GA_BLOCK) {  // uniform
+    const int64_t i = i0 + tid;
+    const int f = i < n && prec_key(value(i)) == prefix;
+    int tot;
+    const int o = block_exclusive_scan<GA_BLOCK, int>(f, tmp, tot);
+    if (f && base + o == rem) ctl[2] = (unsigned long long)i;
+    base += tot;
+  }
+  __syncthreads();
+  const int64_t pick = (int64_t)ctl[2];
+  __syncthreads();  // ctl is reused by the next call
+  return pick;
+}
+
+// Past this many spectra the precursor picks take the radix select
+constexpr int64_t GA_RADIX_N = 512;
+
 __device__ void prec_select_block(const CsrView& v, int64_t s0, int64_t n, const GapParams& P, double* stage,
                                   long long* sel) {
   const int tid = threadIdx.x;
   const double H = P.proton;
+  if (n > GA_RADIX_N) {
+    uint32_t* ws = reinterpret_cast<uint32_t*>(stage);
+    const int64_t m = prec_radix_select([&](int64_t i) {
+      const double z = (double)v.charge[s0 + i];
+      return v.prec_mz[s0 + i] * z - z * H;  // (m*c - c*H), no contraction: precursor_summary's mass
+    }, n, (n - 1) / 2, ws);
+    int64_t r0 = 0, r1 = 0;
+    if (P.rt_mode == 0) {
+      auto rt = [&](int64_t i) { return v.rt[s0 + i]; };
+      r0 = prec_radix_select(rt, n, (n - 1) / 2, ws);
+      r1 = prec_radix_select(rt, n, n / 2, ws);
+    }
+    if (tid == 0) { sel[0] = m; sel[1] = r0; sel[2] = r1; }
+    __syncthreads();
+    return;
+  }
   auto pass = [&](auto value, int64_t want0, int64_t want1, long long* out0, long long* out1) {
     for (int64_t i0 = 0; i0 < n; i0 += GA_BLOCK) {  // uniform
       const int64_t i = i0 + tid;
@@ -369,6 +456,100 @@ __device__ __forceinline__ void gap_peaks(const CsrView& v, int64_t p0, int64_t 
       if (k < p1) f(k, m[u], it[u]);
     }
   }
+}
+
+// ------------------------------------------------- per-slot / per-group steps
+// Shared by gap_body and the giant-cluster pipeline (kL: LDS state, LDS-only
+// barriers; otherwise global scratch and full barriers).
+template <bool kL>
+__device__ __forceinline__ void gap_bar() {
+  if constexpr (kL) lds_barrier();
+  else __syncthreads();
+}
+
+// 4: gaps between consecutive occupied buckets -> emitted group per slot (cnt[d]
+// becomes slot d's group, gcnt the group counts), the group-sum words zeroed.
+// kOk with E groups, kDeferred (a bucket spans mz_accuracy) or kNoGap.
+template <bool kL, class PrefixT>
+__device__ __forceinline__ int32_t gap_groups(const GapState<PrefixT>& S, const GapParams& P, int D, int* tmp,
+                                              int* votes, int& E) {
+  const int tid = threadIdx.x;
+  auto bar = []() __attribute__((always_inline)) { gap_bar<kL>(); };
+  const int per = (D + GA_BLOCK - 1) / GA_BLOCK;
+  const int d0 = tid * per;
+  int my_gaps = 0, split = 0;
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d >= D) break;
+    const double mn = f64_from_order_key(S.kmin[d]), mx = f64_from_order_key(S.kmax[d]);
+    split |= (mx - mn) >= P.mz_accuracy;  // a gap could hide inside the bucket
+    if (d + 1 < D) my_gaps += (f64_from_order_key(S.kmin[d + 1]) - mx) >= P.mz_accuracy;
+  }
+  if (block_any<GA_BLOCK, kL>(split, votes, 1)) return kDeferred;
+  int m_gaps;
+  int g = block_exclusive_scan<GA_BLOCK, int, kL>(my_gaps, tmp, m_gaps);
+  if (m_gaps == 0) return kNoGap;
+  E = m_gaps >= 2 ? m_gaps : 2;
+  for (int j = 0; j < per; ++j) {
+    const int d = d0 + j;
+    if (d >= D) break;
+    const int eg = m_gaps >= 2 ? min(g, m_gaps - 1) : g;
+    atomicAdd(&S.gcnt[eg], S.cnt[d]);
+    const bool gap_after = d + 1 < D &&
+        (f64_from_order_key(S.kmin[d + 1]) - f64_from_order_key(S.kmax[d])) >= P.mz_accuracy;
+    S.cnt[d] = (uint32_t)eg;
+    g += gap_after;
+  }
+  bar();
+  for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
+  bar();
+  return kOk;
+}
+
+// 6: min_fraction filter, dynamic range, ordered output of cluster c's E groups
+// (fixed-point sums at scales 2^sc_m / 2^sc_i): kOk or kEmpty.
+template <bool kL, class PrefixT>
+__device__ __forceinline__ int32_t gap_emit(const GapState<PrefixT>& S, const GapParams& P, int64_t c, int64_t n,
+                                            int64_t N, int64_t p0, int E, int sc_m, int sc_i, const PeaksOut& out,
+                                            int* tmp, double* red, int* votes) {
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const double min_len = P.min_fraction * (double)n;
+  const int gper = (E + GA_BLOCK - 1) / GA_BLOCK;
+  const int e0 = tid * gper;
+  auto isum = [&](int e) -> double { return ldexp((double)(int64_t)S.kmax[e], -sc_i); };
+  double gmax = -__longlong_as_double(0x7ff0000000000000ll);
+  int anyg = 0;
+  for (int j = 0; j < gper; ++j) {
+    const int e = e0 + j;
+    if (e < E && (double)S.gcnt[e] >= min_len) {
+      gmax = fmax(gmax, isum(e) / (double)n);
+      anyg = 1;
+    }
+  }
+  gmax = wave_max_dpp(gmax);
+  if (lane == 0) red[wid] = gmax;
+  if (!block_any<GA_BLOCK, kL>(anyg, votes, 1)) return kEmpty;
+  for (int w = 0; w < GA_BLOCK / kWave; ++w) gmax = fmax(gmax, red[w]);
+  const double thr = gmax / P.dyn_range;
+  int mine = 0;
+  for (int j = 0; j < gper; ++j) {
+    const int e = e0 + j;
+    if (e < E && (double)S.gcnt[e] >= min_len && isum(e) / (double)n >= thr) ++mine;
+  }
+  int total;
+  int o = block_exclusive_scan<GA_BLOCK, int, kL>(mine, tmp, total);
+  for (int j = 0; j < gper; ++j) {
+    const int e = e0 + j;
+    if (e >= E || (double)S.gcnt[e] < min_len) continue;
+    const double iv = isum(e) / (double)n;
+    if (!(iv >= thr)) continue;
+    SPX_GUARD(o < N, "gap out c=%ld o=%d N=%ld\n", (long)c, o, (long)N)
+    out.mz[p0 + o] = ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e];
+    out.inten[p0 + o] = iv;
+    ++o;
+  }
+  if (tid == 0) out.count[c] = total;
+  return kOk;
 }
 
 // --------------------------------------------------------------- the body
@@ -554,36 +735,8 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   bar();
 
   SPX_STAMP(4);
-  // 4: gaps between consecutive occupied buckets -> emitted group per slot
-  const int per = (D + GA_BLOCK - 1) / GA_BLOCK;
-  const int d0 = tid * per;
-  int my_gaps = 0, split = 0;
-  for (int j = 0; j < per; ++j) {
-    const int d = d0 + j;
-    if (d >= D) break;
-    const double mn = f64_from_order_key(S.kmin[d]), mx = f64_from_order_key(S.kmax[d]);
-    split |= (mx - mn) >= P.mz_accuracy;  // a gap could hide inside the bucket
-    if (d + 1 < D) my_gaps += (f64_from_order_key(S.kmin[d + 1]) - mx) >= P.mz_accuracy;
-  }
-  if (any(split, 1)) return kDeferred;
-  int m_gaps;
-  int g = block_exclusive_scan<GA_BLOCK, int, kL>(my_gaps, tmp, m_gaps);
-  if (m_gaps == 0) return kNoGap;
-  const int E = m_gaps >= 2 ? m_gaps : 2;
-  for (int j = 0; j < per; ++j) {
-    const int d = d0 + j;
-    if (d >= D) break;
-    const int eg = m_gaps >= 2 ? min(g, m_gaps - 1) : g;
-    atomicAdd(&S.gcnt[eg], S.cnt[d]);
-    const bool gap_after = d + 1 < D &&
-        (f64_from_order_key(S.kmin[d + 1]) - f64_from_order_key(S.kmax[d])) >= P.mz_accuracy;
-    S.cnt[d] = (uint32_t)eg;
-    g += gap_after;
-  }
-  bar();
-  for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
-  bar();
-
+  int E;
+  if (const int32_t st = gap_groups<kL>(S, P, D, tmp, votes, E); st != kOk) return st;
   SPX_STAMP(5);
   // 5: fixed-point group sums (exact integer adds: order-independent)
   int ex_m, ex_i;
@@ -601,44 +754,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   bar();
 
   SPX_STAMP(6);
-  // 6: min_fraction filter, dynamic range, ordered output
-  const double min_len = P.min_fraction * (double)n;
-  const int gper = (E + GA_BLOCK - 1) / GA_BLOCK;
-  const int e0 = tid * gper;
-  auto isum = [&](int e) -> double { return ldexp((double)(int64_t)S.kmax[e], -sc_i); };
-  double gmax = -__longlong_as_double(0x7ff0000000000000ll);
-  int anyg = 0;
-  for (int j = 0; j < gper; ++j) {
-    const int e = e0 + j;
-    if (e < E && (double)S.gcnt[e] >= min_len) {
-      gmax = fmax(gmax, isum(e) / (double)n);
-      anyg = 1;
-    }
-  }
-  gmax = wave_max_dpp(gmax);
-  if (lane == 0) red[wid] = gmax;
-  if (!any(anyg, 1)) return kEmpty;
-  for (int w = 0; w < GA_BLOCK / kWave; ++w) gmax = fmax(gmax, red[w]);
-  const double thr = gmax / P.dyn_range;
-  int mine = 0;
-  for (int j = 0; j < gper; ++j) {
-    const int e = e0 + j;
-    if (e < E && (double)S.gcnt[e] >= min_len && isum(e) / (double)n >= thr) ++mine;
-  }
-  int total;
-  int o = block_exclusive_scan<GA_BLOCK, int, kL>(mine, tmp, total);
-  for (int j = 0; j < gper; ++j) {
-    const int e = e0 + j;
-    if (e >= E || (double)S.gcnt[e] < min_len) continue;
-    const double iv = isum(e) / (double)n;
-    if (!(iv >= thr)) continue;
-    SPX_GUARD(o < N, "gap out c=%ld o=%d N=%ld\n", (long)c, o, (long)N)
-    out.mz[p0 + o] = ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e];
-    out.inten[p0 + o] = iv;
-    ++o;
-  }
-  if (tid == 0) out.count[c] = total;
-  return kOk;
+  return gap_emit<kL>(S, P, c, n, N, p0, E, sc_m, sc_i, out, tmp, red, votes);
 }
 
 template <class PrefixT>
@@ -749,19 +865,39 @@ __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
   return L;
 }
 
-__global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v, GapParams P, PeaksOut out,
-                                                                      double* prec_out, int32_t* charge_out,
-                                                                      double* rt_out, int32_t* status,
-                                                                      const int32_t* deferred,
-                                                                      const int32_t* n_deferred, char* scratch,
-                                                                      int64_t slice_bytes, int wcap, int dcap,
-                                                                      int32_t* unresolved) {
-  __shared__ int tmp[GA_BLOCK / kWave + 1];
-  __shared__ int votes[2 * GA_NW];
-  __shared__ double red[GA_BLOCK / kWave * 3];
-  __shared__ double stage[GA_BLOCK];
-  __shared__ long long sel[4];
-  char* base = scratch + (int64_t)blockIdx.x * slice_bytes;
+// ------------------------------------------------------- giant clusters
+// A cluster of more than GA_GIANT_N peaks (the skewed law's n = 5,000 giants hold
+// ~1.1M) is too much for one workgroup: the global kernel hands it to a pipeline
+// whose per-peak passes (1 extrema, 2 bitmap, 3 slot extrema, 5 group sums) spread
+// the cluster's peaks over the whole grid in tiles, with the per-slot and
+// per-group steps (prefix, 4 gaps, 6 emit + precursor) one workgroup per giant in
+// between.  Same integer atomics, same group structure, same fixed-point sums:
+// the results equal gap_body's.  Each giant works in its own slice of an arena
+// (slots for min(N, buckets in range)), taken by the global kernel's hand-off;
+// a giant the arena or the record table cannot take stays in the global kernel.
+constexpr int64_t GA_GIANT_N = 65536;
+constexpr int GA_GMAX = 256;                      // giant records per call
+constexpr int64_t GA_TILE = 2 * GA_BATCH * GA_BLOCK;  // peaks per tile
+constexpr int GA_GIANT_GRID = 1024;               // tile kernels' workgroups
+constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS first (50 KB)
+
+struct GapGiant {  // zeroed by the call's memset
+  unsigned long long lo_inv, hi_key, imax_key;  // ~order key of the min m/z, order keys of max m/z, max |intensity|
+  long long off;                                // its arena slice
+  int32_t c, dcap, ok, bad, status, D, E, pad;
+};
+
+struct GiantArgs {
+  CsrView v;
+  GapParams P;
+  GapGiant* giants;
+  const int32_t* n_giant;
+  int gmax;
+  char* arena;
+  int wcap;
+};
+
+__device__ __forceinline__ GapState<uint32_t> gap_slice_state(char* base, int wcap, int dcap) {
   const GapSliceLayout Lo = gap_slice_layout(wcap, dcap);
   GapState<uint32_t> S;
   S.bitmap = reinterpret_cast<unsigned long long*>(base + Lo.bitmap);
@@ -772,9 +908,285 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
   S.kmax = reinterpret_cast<uint64_t*>(base + Lo.kmax);
   S.wcap = wcap;
   S.dcap = dcap;
+  return S;
+}
+
+// The giant's m/z extent as gap_body's pass 1 leaves it (lo, hi, imax; kb, nw)
+struct GiantExtent {
+  double lo, hi, imax;
+  int64_t kb, nw;
+};
+__device__ __forceinline__ GiantExtent giant_extent(const GapGiant& H, const GapParams& P) {
+  GiantExtent X;
+  X.lo = f64_from_order_key(~H.lo_inv);
+  X.hi = f64_from_order_key(H.hi_key);
+  X.imax = f64_from_order_key(H.imax_key);
+  X.kb = floor_div_exact(X.lo, P.bucket_w, P.inv_bucket_w);
+  X.nw = (floor_div_exact(X.hi, P.bucket_w, P.inv_bucket_w) - X.kb) / 64 + 1;
+  return X;
+}
+
+// The per-peak passes over every giant's tiles: PASS 1 extrema (and the slices'
+// bitmaps zeroed), 2 bucket bitmap, 3 slot m/z extent, 5 group sums and counts.
+// The (giant, tile) pairs of all giants form one index space, striped over the grid.
+template <int PASS>
+__global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) {
+  __shared__ double red[GA_NW * 3];
+  __shared__ int votes[2 * GA_NW];
+  __shared__ unsigned long long agg_m[PASS == 5 ? GA_GAGG : 1], agg_i[PASS == 5 ? GA_GAGG : 1];
+  __shared__ uint32_t agg_c[PASS == 5 ? GA_GAGG : 1];
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const int ng = min(*A.n_giant, A.gmax);
+  auto peaks_of = [&](const GapGiant& H, int64_t& p0, int64_t& p1) {
+    p0 = A.v.spec_off[A.v.cluster_off[H.c]];
+    p1 = A.v.spec_off[A.v.cluster_off[H.c + 1]];
+  };
+  // a giant's tiles in this pass (0: not in it)
+  auto tiles_of = [&](const GapGiant& H) -> int64_t {
+    if (!H.ok) return 0;
+    if (PASS > 1) {
+      if (H.bad || H.status != kOk) return 0;
+      if (giant_extent(H, A.P).nw > A.wcap) return 0;  // the prefix step defers it
+    }
+    int64_t p0, p1;
+    peaks_of(H, p0, p1);
+    return (p1 - p0 + GA_TILE - 1) / GA_TILE;
+  };
+  if constexpr (PASS == 1) {
+    for (int g = 0; g < ng; ++g) {
+      if (!A.giants[g].ok) continue;
+      unsigned long long* bm = gap_slice_state(A.arena + A.giants[g].off, A.wcap, A.giants[g].dcap).bitmap;
+      for (int64_t w = (int64_t)blockIdx.x * GA_BLOCK + tid; w < A.wcap; w += (int64_t)gridDim.x * GA_BLOCK)
+        bm[w] = 0ull;
+    }
+  }
+  int g = 0, cur = -1, E = 0, sc_m = 0, sc_i = 0;
+  bool agg = false;
+  int64_t gbase = 0, gtiles = ng > 0 ? tiles_of(A.giants[0]) : 0, p0 = 0, p1 = 0, kb = 0;
+  GapState<uint32_t> S{};
+  auto flush = [&]() __attribute__((always_inline)) {  // PASS 5: the LDS sums of giant `cur`
+    if constexpr (PASS == 5) {
+      if (agg) {
+        lds_barrier();
+        for (int e = tid; e < E; e += GA_BLOCK) {
+          if (agg_c[e]) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[e]), agg_m[e]);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[e]), agg_i[e]);
+            atomicAdd(&S.gcnt[e], agg_c[e]);
+          }
+        }
+        lds_barrier();
+      }
+    }
+  };
+  for (int64_t u = blockIdx.x;; u += gridDim.x) {  // uniform
+    while (g < ng && u >= gbase + gtiles) {
+      gbase += gtiles;
+      if (++g < ng) gtiles = tiles_of(A.giants[g]);
+    }
+    if (g >= ng) break;
+    const GapGiant& H = A.giants[g];
+    if (g != cur) {  // this workgroup's first tile of giant g
+      flush();
+      cur = g;
+      peaks_of(H, p0, p1);
+      S = gap_slice_state(A.arena + H.off, A.wcap, H.dcap);
+      if constexpr (PASS > 1) {
+        const GiantExtent X = giant_extent(H, A.P);
+        kb = X.kb;
+        if constexpr (PASS == 5) {
+          const int64_t N = p1 - p0;
+          int ex_m, ex_i;
+          frexp(fmax(fabs(X.lo), fabs(X.hi)) * (double)N, &ex_m);
+          frexp(X.imax * (double)N, &ex_i);
+          sc_m = 61 - ex_m;
+          sc_i = 61 - ex_i;
+          // few groups: this workgroup's sums and counts in LDS first, one global add
+          // per group at the end (integer adds: the same totals)
+          E = H.E;
+          agg = E <= GA_GAGG;
+          if (agg) {
+            for (int e = tid; e < E; e += GA_BLOCK) { agg_m[e] = 0ull; agg_i[e] = 0ull; agg_c[e] = 0u; }
+            lds_barrier();
+          }
+        }
+      }
+    }
+    const int64_t t0 = p0 + (u - gbase) * GA_TILE, t1 = min(p1, t0 + GA_TILE);
+    if constexpr (PASS == 1) {
+      double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
+      int bad = 0;
+      gap_peaks<true>(A.v, t0, t1, [&](int64_t, double m, double it) {
+        bad |= !isfinite(m) || !isfinite(it);
+        lo = fmin(lo, m);
+        hi = fmax(hi, m);
+        imax = fmax(imax, fabs(it));
+      });
+      lo = wave_min_dpp(lo);
+      hi = wave_max_dpp(hi);
+      imax = wave_max_dpp(imax);
+      if (lane == 0) { red[wid] = lo; red[GA_NW + wid] = hi; red[2 * GA_NW + wid] = imax; }
+      const int anybad = block_any<GA_BLOCK, true>(bad, votes, 0);  // its barrier orders red too
+      if (tid == 0) {
+        for (int w = 1; w < GA_NW; ++w) {
+          lo = fmin(lo, red[w]);
+          hi = fmax(hi, red[GA_NW + w]);
+          imax = fmax(imax, red[2 * GA_NW + w]);
+        }
+        GapGiant& Hw = A.giants[g];
+        if (anybad) atomicOr(&Hw.bad, 1);
+        if (lo <= hi) {
+          atomicMax(&Hw.lo_inv, ~(unsigned long long)f64_order_key(lo));
+          atomicMax(&Hw.hi_key, (unsigned long long)f64_order_key(hi));
+          atomicMax(&Hw.imax_key, (unsigned long long)f64_order_key(imax));
+        }
+      }
+      lds_barrier();  // red and votes are reused by the next tile
+    } else {
+      gap_peaks<PASS == 5>(A.v, t0, t1, [&](int64_t, double m, double it) {
+        const int64_t b = floor_div_exact(m, A.P.bucket_w, A.P.inv_bucket_w) - kb;
+        // bits and extrema only grow / shrink, so a stale read that says "no
+        // change" is still right: the atomic is issued only when it can matter
+        if constexpr (PASS == 2) {
+          const unsigned long long bit = 1ull << (b & 63);
+          if (!(S.bitmap[b >> 6] & bit)) atomicOr(&S.bitmap[b >> 6], bit);
+        } else if constexpr (PASS == 3) {  // the counts come with pass 5's group sums
+          const int slot = bitmap_rank(S.bitmap, S.wprefix, b);
+          const unsigned long long key = f64_order_key(m);
+          unsigned long long* kmin = reinterpret_cast<unsigned long long*>(&S.kmin[slot]);
+          unsigned long long* kmax = reinterpret_cast<unsigned long long*>(&S.kmax[slot]);
+          if (key < *kmin) atomicMin(kmin, key);
+          if (key > *kmax) atomicMax(kmax, key);
+        } else {
+          const uint32_t eg = S.cnt[bitmap_rank(S.bitmap, S.wprefix, b)];
+          const unsigned long long qm = (unsigned long long)__double2ll_rn(ldexp(m, sc_m));
+          const unsigned long long qi = (unsigned long long)__double2ll_rn(ldexp(it, sc_i));
+          if (agg) {
+            atomicAdd(&agg_m[eg], qm);
+            atomicAdd(&agg_i[eg], qi);
+            atomicAdd(&agg_c[eg], 1u);
+          } else {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), qm);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[eg]), qi);
+            atomicAdd(&S.gcnt[eg], 1u);
+          }
+        }
+      });
+    }
+  }
+  flush();
+}
+
+// The per-giant steps, a workgroup per giant: STEP 0 the bitmap prefix (and the
+// slots zeroed), 4 the gaps and groups, 6 the emit, precursor and status.
+template <int STEP>
+__global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, PeaksOut out, double* prec_out,
+                                                                 int32_t* charge_out, double* rt_out,
+                                                                 int32_t* status, int32_t* unresolved) {
+  __shared__ int tmp[GA_NW + 1];
+  __shared__ int votes[2 * GA_NW];
+  __shared__ double red[GA_NW * 3];
+  __shared__ double stage[GA_BLOCK];
+  __shared__ long long sel[4];
+  const int tid = threadIdx.x;
+  const int ng = min(*A.n_giant, A.gmax);
+  for (int g = blockIdx.x; g < ng; g += gridDim.x) {
+    GapGiant& H = A.giants[g];
+    if (!H.ok) continue;  // uniform
+    const int64_t c = H.c;
+    const GapState<uint32_t> S = gap_slice_state(A.arena + H.off, A.wcap, H.dcap);
+    int32_t st = H.bad ? kNonFinite : H.status;
+    if constexpr (STEP == 0) {
+      if (st != kOk) continue;
+      const GiantExtent X = giant_extent(H, A.P);
+      int D = 0;
+      if (X.nw > S.wcap) {
+        st = kDeferred;
+      } else {
+        D = bitmap_prefix<GA_BLOCK, uint32_t, false>(S.bitmap, S.wprefix, (int)X.nw, tmp);
+        if (D > S.dcap) st = kDeferred;
+      }
+      if (st == kOk) {
+        for (int d = tid; d < D; d += GA_BLOCK) {
+          S.cnt[d] = 0u;
+          S.gcnt[d] = 0u;
+          S.kmin[d] = ~0ull;
+          S.kmax[d] = 0ull;
+        }
+      }
+      if (tid == 0) { H.D = D; H.status = st; }
+    } else if constexpr (STEP == 4) {
+      if (st != kOk) continue;
+      int E = 0;
+      st = gap_groups<false>(S, A.P, H.D, tmp, votes, E);
+      if (tid == 0) { H.E = E; H.status = st; }
+    } else {
+      const int64_t s0 = A.v.cluster_off[c], n = A.v.cluster_off[c + 1] - s0;
+      const int64_t p0 = A.v.spec_off[s0], N = A.v.spec_off[A.v.cluster_off[c + 1]] - p0;
+      if (st == kOk) {
+        const GiantExtent X = giant_extent(H, A.P);
+        int ex_m, ex_i;
+        frexp(fmax(fabs(X.lo), fabs(X.hi)) * (double)N, &ex_m);
+        frexp(X.imax * (double)N, &ex_i);
+        st = gap_emit<false>(S, A.P, c, n, N, p0, H.E, 61 - ex_m, 61 - ex_i, out, tmp, red, votes);
+      }
+      if (st == kDeferred) {
+        if (tid == 0) { status[c] = kDeferred; atomicAdd(unresolved, 1); }
+      } else {
+        gap_finish<uint32_t>(A.v, A.P, c, st, out, prec_out, charge_out, rt_out, status, nullptr, nullptr, stage,
+                             sel);
+      }
+    }
+    __syncthreads();  // the LDS is reused by the next giant
+  }
+}
+
+__global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v, GapParams P, PeaksOut out,
+                                                                      double* prec_out, int32_t* charge_out,
+                                                                      double* rt_out, int32_t* status,
+                                                                      const int32_t* deferred,
+                                                                      const int32_t* n_deferred, char* scratch,
+                                                                      int64_t slice_bytes, int wcap, int dcap,
+                                                                      int32_t* unresolved, GapGiant* giants,
+                                                                      int32_t* n_giant, int gmax,
+                                                                      unsigned long long* arena_used,
+                                                                      long long arena_bytes) {
+  __shared__ int tmp[GA_BLOCK / kWave + 1];
+  __shared__ int votes[2 * GA_NW];
+  __shared__ double red[GA_BLOCK / kWave * 3];
+  __shared__ double stage[GA_BLOCK];
+  __shared__ long long sel[4];
+  __shared__ int handed;
+  const GapState<uint32_t> S = gap_slice_state(scratch + (int64_t)blockIdx.x * slice_bytes, wcap, dcap);
   const int32_t nd = *n_deferred;
   for (int32_t i = blockIdx.x; i < nd; i += gridDim.x) {
     const int64_t c = deferred[i];
+    const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+    const int64_t N = v.spec_off[s1] - v.spec_off[s0];
+    if (s1 - s0 >= 2 && N > GA_GIANT_N) {  // uniform: hand it to the giant pipeline if it fits
+      if (threadIdx.x == 0) {
+        int h = 0;
+        const int g = atomicAdd(n_giant, 1);
+        if (g < gmax) {
+          const int dg = (int)(N < (int64_t)wcap * 64 ? N : (int64_t)wcap * 64);  // D <= both
+          const long long need = (long long)gap_slice_layout(wcap, dg).total;
+          const long long off = (long long)atomicAdd(arena_used, (unsigned long long)need);
+          if (off + need <= arena_bytes) {
+            GapGiant& H = giants[g];
+            H.c = (int32_t)c;
+            H.dcap = dg;
+            H.off = off;
+            H.ok = 1;
+            h = 1;
+          }
+        }
+        handed = h;
+      }
+      __syncthreads();
+      const int h = handed;
+      __syncthreads();
+      if (h) continue;
+    }
     int32_t st = gap_body(v, P, S, c, out, tmp, red, votes);
     if (st == kDeferred) {
       // bucket range beyond the scratch, or a bucket spanning >= mz_accuracy:

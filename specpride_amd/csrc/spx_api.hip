@@ -103,6 +103,19 @@ int64_t bin_mean_fallback_grid(int64_t C, const spx_bin_params* params, int64_t 
   return fallback_grid_sized(C, spx::bin_mean_slice_bytes(bin_words(params), dcap));
 }
 
+// The giant pipeline's arena (gap_average.hip, GA_GIANT_N): none when no cluster can
+// be a giant, else room for the giants the batch can hold, within a 1 GiB budget
+// (a giant it cannot take stays in the global kernel).
+int64_t gap_giant_arena(const spx_csr* csr, const spx_gap_params* params, const spx_batch_info* info) {
+  const int64_t maxp = info->max_cluster_peaks;
+  if (maxp <= spx::GA_GIANT_N) return 0;
+  const int wcap = gap_wcap(params, info);
+  const int64_t dg = std::min<int64_t>(maxp, (int64_t)wcap * 64);
+  const int64_t per = spx::gap_slice_bytes(wcap, (int)std::min<int64_t>(dg, INT32_MAX));
+  const int64_t giants = std::min<int64_t>(spx::GA_GMAX, csr->n_peaks / (spx::GA_GIANT_N + 1));
+  return std::min<int64_t>(int64_t(1) << 30, per * std::max<int64_t>(giants, 1));
+}
+
 int64_t gap_fallback_grid(int64_t C, const spx_gap_params* params, const spx_batch_info* info) {
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   return fallback_grid_sized(C, spx::gap_slice_bytes(gap_wcap(params, info), (int)std::min<int64_t>(dcap, INT32_MAX)));
@@ -373,7 +386,9 @@ size_t spx_gap_average_workspace_size(const spx_csr* csr, const spx_gap_params* 
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   const size_t Cm = (size_t)std::max<int64_t>(C, 1);
-  return align256(sizeof(int32_t)) * 2 + align256(spx::kListCountBytes) + align256(sizeof(int32_t) * Cm) +
+  return align256(sizeof(int32_t)) * 3 + align256(sizeof(unsigned long long)) +
+         align256(sizeof(spx::GapGiant) * spx::GA_GMAX) + align256(spx::kListCountBytes) +
+         align256(sizeof(int32_t) * Cm) + (size_t)gap_giant_arena(csr, params, info) +
          align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
          (size_t)gap_fallback_grid(C, params, info) *
              (size_t)spx::gap_slice_bytes(gap_wcap(params, info), (int)std::min<int64_t>(dcap, INT32_MAX));
@@ -395,11 +410,17 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
   int32_t* n_def = w.take<int32_t>(1);
   int32_t* unresolved = w.take<int32_t>(1);
+  int32_t* n_giant = w.take<int32_t>(1);
+  unsigned long long* arena_used = w.take<unsigned long long>(1);
+  spx::GapGiant* giants = w.take<spx::GapGiant>(spx::GA_GMAX);  // the global kernel's giants
   spx::StripedList wide;  // the LDS kernel's leftovers for the wide kernel
   wide.counts = w.take<int32_t>((size_t)spx::kListStripes * spx::kListLine);
+  const size_t zeroed = (size_t)(w.base + w.used - reinterpret_cast<char*>(n_def));
   wide.cap = spx::striped_cap(C);
   int32_t* def = w.take<int32_t>((size_t)C);  // the wide kernel's leftovers for the global kernel
   wide.items = w.take<int32_t>((size_t)wide.cap * spx::kListStripes);
+  const int64_t arena_bytes = gap_giant_arena(csr, params, info);
+  char* arena = w.take<char>((size_t)arena_bytes);
   char* scratch = w.base + w.used;
   spx::GapParams P;
   P.mz_accuracy = params->mz_accuracy;
@@ -415,8 +436,8 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   const int wcap = gap_wcap(params, info);
   const int dcap = (int)std::min<int64_t>(std::max<int64_t>(1, info->max_cluster_peaks), INT32_MAX);
 
-  // n_def, unresolved and the striped list's counters: the first 512 B + kListCountBytes
-  if (hipMemsetAsync(n_def, 0, 512 + spx::kListCountBytes, s) != hipSuccess)
+  // the counters, the giants' records and the striped list's counters
+  if (hipMemsetAsync(n_def, 0, zeroed, s) != hipSuccess)
     return check_launch("spx_gap_average memset");
   hipLaunchKernelGGL(spx::gap_average_lds_kernel, dim3((unsigned)C), dim3(spx::GA_BLOCK), 0, s, V, P, O, pepmass_out,
                      charge_out, rt_out, status, wide);
@@ -427,11 +448,28 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   spx::GapParams P2 = P;  // half-width buckets: no gap can hide inside one
   P2.bucket_w = params->mz_accuracy * 0.5;
   P2.inv_bucket_w = 1.0 / P2.bucket_w;
-  hipLaunchKernelGGL(spx::gap_average_global_kernel, dim3((unsigned)gap_fallback_grid(C, params, info)),
-                     dim3(spx::GA_BLOCK), 0, s, V,
-                     P2, O, pepmass_out, charge_out, rt_out, status, def, n_def, scratch,
-                     spx::gap_slice_bytes(wcap, dcap), wcap, dcap, unresolved);
-  return check_launch("gap_average_global_kernel");
+  const int64_t ggrid = gap_fallback_grid(C, params, info);
+  const int gmax = spx::GA_GMAX;
+  const int64_t slice = spx::gap_slice_bytes(wcap, dcap);
+  hipLaunchKernelGGL(spx::gap_average_global_kernel, dim3((unsigned)ggrid), dim3(spx::GA_BLOCK), 0, s, V, P2, O,
+                     pepmass_out, charge_out, rt_out, status, def, n_def, scratch, slice, wcap, dcap, unresolved,
+                     giants, n_giant, gmax, arena_used, (long long)arena_bytes);
+  if (int rc = check_launch("gap_average_global_kernel")) return rc;
+  if (arena_bytes == 0) return SPX_SUCCESS;  // no cluster of this batch can be a giant
+  // the giant clusters' pipeline
+  const spx::GiantArgs A{V, P2, giants, n_giant, gmax, arena, wcap};
+  const dim3 tiles(spx::GA_GIANT_GRID), per(gmax), blk(spx::GA_BLOCK);
+  hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<1>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<2>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_step_kernel<0>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
+                     unresolved);
+  hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<3>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_step_kernel<4>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
+                     unresolved);
+  hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<5>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_step_kernel<6>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
+                     unresolved);
+  return check_launch("gap_giant pipeline");
 }
 
 // ------------------------------------------------------------------- medoid

@@ -179,3 +179,88 @@ def test_fuzz_precursor_modes(gpu, seed):
                    else np_oracle.median_rt(rt))
             assert got["prec"][c] == want[0] and got["charge"][c] == want[1], (pm, c)
             assert got["rt"][c] == wrt or (np.isnan(wrt) and np.isnan(got["rt"][c])), (rtm, c)
+
+
+def test_precursor_picks_large_clusters(gpu):
+    """Clusters past GA_RADIX_N (512) spectra take the radix select for the
+    precursor picks: the lower-median mass index and the RT median must be the
+    stable ranks' picks (ties by index, NaN last, -0 == +0) exactly as the O(n^2)
+    rank loops give them.  Ties are dense here (masses on a coarse grid, mixed
+    charges, NaN and signed-zero RTs), so the expected pick is numpy's stable
+    argsort -- the definition the kernels implement (the reference's
+    unstable argsort leaves tied picks parity unpinned)."""
+    rng = np.random.default_rng(77)
+    sizes = np.array([65, 511, 512, 513, 700, 1025, 3000, 5000, 2, 1])
+    csr = make_clusters_np(len(sizes), seed=77, sizes=sizes, n_template=5)
+    S = csr.n_spectra
+    charge = rng.choice([2, 3], S).astype(csr.charge.dtype)
+    prec = np.round(rng.uniform(400, 420, S), 1)  # ~200 distinct values: many ties
+    rt = np.round(rng.uniform(0, 50, S), 0)
+    rt[rng.random(S) < 0.05] = 0.0
+    rt[rng.random(S) < 0.05] = -0.0
+    co = csr.cluster_off
+    for nan_c in (0, 4, 8):  # NaN RTs off the middle ranks (np.median -> NaN): block, radix and wave paths
+        rt[co[nan_c] + 1] = np.nan
+    csr = SpectraCSR(csr.cluster_off, csr.spec_off, csr.mz, csr.inten, prec, charge, rt)
+    batch = engine.DeviceBatch.from_host(csr)
+    H = engine.PROTON
+    for rtm in ("mass_lower_median", "median"):
+        got = engine.gap_average(batch, pepmass="lower_median", rt=rtm).to_host()
+        for c in range(csr.n_clusters):
+            s0, s1 = co[c], co[c + 1]
+            n = s1 - s0
+            z = charge[s0:s1].astype(np.float64)
+            mass = prec[s0:s1] * z - z * H
+            lm = int(np.argsort(mass, kind="stable")[(n - 1) // 2])
+            zl = int(charge[s0 + lm])
+            assert got["charge"][c] == zl, (rtm, c)
+            assert got["prec"][c] == (mass[lm] + zl * H) / zl, (rtm, c)
+            wrt = rt[s0 + lm] if rtm == "mass_lower_median" else np_oracle.median_rt(rt[s0:s1])
+            assert got["rt"][c] == wrt or (np.isnan(wrt) and np.isnan(got["rt"][c])), (rtm, c)
+
+
+def test_gap_average_giant_pipeline(gpu):
+    """Clusters past GA_GIANT_N (65,536) peaks go from the global kernel to the
+    tiled giant pipeline, at most GA_GMAX (16) per call; the rest stay in the
+    global kernel.  24 clusters here: 20 giants (so 4 stay behind), one giant with
+    a NaN intensity (SPX_NON_FINITE), giants on a coarse m/z grid (exact ties,
+    several peaks per bucket), a 2-spectrum giant, and small clusters between them.
+    Against the C oracle: group structure exact, values within GAP_RTOL, under the
+    default and non-default parameters."""
+    rng = np.random.default_rng(91)
+    sizes = np.array([300, 5, 400, 2, 260, 280, 3, 350] + [270] * 14 + [1, 330])
+    csr = make_clusters_np(len(sizes), seed=91, sizes=sizes, n_template=300)
+    mz, it = csr.mz.copy(), csr.inten.copy()
+    so, co = csr.spec_off, csr.cluster_off
+    it[so[co[4]] + 17] = np.nan  # cluster 4: non-finite
+    for c in (5, 9, 12):  # coarse grid, spectra kept sorted
+        for s in range(co[c], co[c + 1]):
+            a, b = so[s], so[s + 1]
+            mz[a:b] = np.sort(np.round(mz[a:b] / 0.02) * 0.02)
+    # cluster 3: two spectra of 40,000 peaks each
+    big = [np.sort(rng.uniform(100, 2000, 40000)) for _ in range(2)]
+    parts_mz, parts_it, lens = [], [], []
+    for s in range(csr.n_spectra):
+        if co[3] <= s < co[4]:
+            m = big[s - co[3]]
+            parts_mz.append(m)
+            parts_it.append(rng.uniform(1, 1e4, len(m)))
+        else:
+            parts_mz.append(mz[so[s]:so[s + 1]])
+            parts_it.append(it[so[s]:so[s + 1]])
+        lens.append(len(parts_mz[-1]))
+    spec_off = np.zeros(csr.n_spectra + 1, np.int64)
+    np.cumsum(lens, out=spec_off[1:])
+    csr = SpectraCSR(co, spec_off, np.concatenate(parts_mz), np.concatenate(parts_it), csr.prec_mz,
+                     csr.charge, csr.rt)
+    N = np.diff(spec_off[co])
+    assert (N > 65536).sum() >= 21
+    st = engine.gap_average(engine.DeviceBatch.from_host(csr)).to_host()["status"]
+    assert st[4] == engine.STATUS_NON_FINITE and not np.delete(st, 4).any()
+    # the oracle carries NaN through the sums (the engine reports it instead), so
+    # the values are compared without cluster 4: still 20 giants, 4 past GA_GMAX
+    sub = csr.select([c for c in range(csr.n_clusters) if c != 4])
+    batch = engine.DeviceBatch.from_host(sub)
+    for kw in (dict(), dict(mz_accuracy=0.02, dyn_range=100.0, min_fraction=0.3)):
+        got = engine.gap_average(batch, **kw).to_host()
+        assert_gap_close(got, c_oracle.gap_average(sub, **kw), kw.get("dyn_range", 1000.0))
