@@ -875,7 +875,7 @@ __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
 // the results equal gap_body's.  Each giant works in its own slice of an arena
 // (slots for min(N, buckets in range)), taken by the global kernel's hand-off;
 // a giant the arena or the record table cannot take stays in the global kernel.
-constexpr int64_t GA_GIANT_N = 65536;
+constexpr int64_t GA_GIANT_N = 16384;
 constexpr int GA_GMAX = 256;                      // giant records per call
 constexpr int64_t GA_TILE = 2 * GA_BATCH * GA_BLOCK;  // peaks per tile
 constexpr int GA_GIANT_GRID = 1024;               // tile kernels' workgroups

@@ -220,13 +220,12 @@ def test_precursor_picks_large_clusters(gpu):
 
 
 def test_gap_average_giant_pipeline(gpu):
-    """Clusters past GA_GIANT_N (65,536) peaks go from the global kernel to the
-    tiled giant pipeline, at most GA_GMAX (16) per call; the rest stay in the
-    global kernel.  24 clusters here: 20 giants (so 4 stay behind), one giant with
-    a NaN intensity (SPX_NON_FINITE), giants on a coarse m/z grid (exact ties,
-    several peaks per bucket), a 2-spectrum giant, and small clusters between them.
-    Against the C oracle: group structure exact, values within GAP_RTOL, under the
-    default and non-default parameters."""
+    """Clusters past GA_GIANT_N (16,384) peaks go from the global kernel to the
+    tiled giant pipeline.  24 clusters here: 21 giants, one with a NaN intensity
+    (SPX_NON_FINITE), giants on a coarse m/z grid (exact ties, several peaks per
+    bucket), a 2-spectrum giant, and small clusters between them.  Against the C
+    oracle: group structure exact, values within GAP_RTOL, under the default and
+    non-default parameters."""
     rng = np.random.default_rng(91)
     sizes = np.array([300, 5, 400, 2, 260, 280, 3, 350] + [270] * 14 + [1, 330])
     csr = make_clusters_np(len(sizes), seed=91, sizes=sizes, n_template=300)
@@ -254,13 +253,34 @@ def test_gap_average_giant_pipeline(gpu):
     csr = SpectraCSR(co, spec_off, np.concatenate(parts_mz), np.concatenate(parts_it), csr.prec_mz,
                      csr.charge, csr.rt)
     N = np.diff(spec_off[co])
-    assert (N > 65536).sum() >= 21
+    assert (N > 16384).sum() >= 21
     st = engine.gap_average(engine.DeviceBatch.from_host(csr)).to_host()["status"]
     assert st[4] == engine.STATUS_NON_FINITE and not np.delete(st, 4).any()
     # the oracle carries NaN through the sums (the engine reports it instead), so
-    # the values are compared without cluster 4: still 20 giants, 4 past GA_GMAX
+    # the values are compared without cluster 4
     sub = csr.select([c for c in range(csr.n_clusters) if c != 4])
     batch = engine.DeviceBatch.from_host(sub)
     for kw in (dict(), dict(mz_accuracy=0.02, dyn_range=100.0, min_fraction=0.3)):
         got = engine.gap_average(batch, **kw).to_host()
         assert_gap_close(got, c_oracle.gap_average(sub, **kw), kw.get("dyn_range", 1000.0))
+
+
+def test_gap_average_giant_overflow(gpu):
+    """More giants than the pipeline's GA_GMAX (256) records: 272 clusters of
+    ~18k peaks, each with one peak past the LDS and wide kernels' bucket range
+    (m/z 2,700) so that all of them reach the global kernel.  256 go through the
+    pipeline, the rest stay in the global kernel, and every one matches the C
+    oracle."""
+    C = 272
+    csr = make_clusters_np(C, seed=93, sizes=np.full(C, 60), n_template=300)
+    mz = csr.mz.copy()
+    so, co = csr.spec_off, csr.cluster_off
+    for c in range(C):
+        s0 = co[c]
+        mz[so[s0 + 1] - 1] = 2700.0 + 0.5 * (c % 7)  # the first spectrum's last peak
+    csr = SpectraCSR(co, so, mz, csr.inten, csr.prec_mz, csr.charge, csr.rt)
+    N = np.diff(so[co])
+    assert (N > 16384).sum() > 256
+    batch = engine.DeviceBatch.from_host(csr)
+    got = engine.gap_average(batch).to_host()
+    assert_gap_close(got, c_oracle.gap_average(csr), 1000.0)
