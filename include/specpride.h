@@ -132,6 +132,9 @@ typedef struct spx_gap_params {
   int32_t rt_mode;      /* spx_rt_mode */
 } spx_gap_params;
 
+/* The workspace holds the global kernel's scratch slices and, when
+ * info->max_cluster_peaks > 16,384, an arena of at most 1 GiB for the giant-cluster
+ * pipeline (clusters past 16,384 peaks, tiled over the whole grid). */
 size_t spx_gap_average_workspace_size(const spx_csr *csr, const spx_gap_params *params,
                                       const spx_batch_info *info);
 int spx_gap_average(const spx_csr *csr, const spx_gap_params *params, const spx_batch_info *info,
