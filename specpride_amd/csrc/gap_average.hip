@@ -475,6 +475,54 @@ __device__ __forceinline__ int32_t gap_groups(const GapState<PrefixT>& S, const 
                                               int* votes, int& E) {
   const int tid = threadIdx.x;
   auto bar = []() __attribute__((always_inline)) { gap_bar<kL>(); };
+  if constexpr (!kL) {
+    // Global scratch: each thread's contiguous chunk of D / 512 slots (below) makes
+    // every load a 64-line gather, one dependent round trip per slot (0.87 ms for a
+    // 380k-slot giant).  Here: a coalesced sweep for the totals, then rounds of
+    // 8 contiguous slots per thread with a running carry of the gaps before them.
+    constexpr int CH = 8;
+    const double acc = P.mz_accuracy;
+    auto key = [&](const uint64_t* a, int d) { return f64_from_order_key(a[d]); };
+    int my_gaps = 0, split = 0;
+    for (int d = tid; d < D; d += GA_BLOCK) {
+      const double mx = key(S.kmax, d);
+      split |= (mx - key(S.kmin, d)) >= acc;  // a gap could hide inside the bucket
+      if (d + 1 < D) my_gaps += (key(S.kmin, d + 1) - mx) >= acc;
+    }
+    if (block_any<GA_BLOCK, kL>(split, votes, 1)) return kDeferred;
+    int m_gaps;
+    block_exclusive_scan<GA_BLOCK, int, kL>(my_gaps, tmp, m_gaps);
+    if (m_gaps == 0) return kNoGap;
+    E = m_gaps >= 2 ? m_gaps : 2;
+    int carry = 0;  // gaps before this round's first slot
+    for (int r0 = 0; r0 < D; r0 += GA_BLOCK * CH) {  // uniform
+      const int db = r0 + tid * CH;
+      int f[CH], mine = 0;
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {  // f[k]: a gap between slots d - 1 and d
+        const int d = db + k;
+        f[k] = d > 0 && d < D && (key(S.kmin, d) - key(S.kmax, d - 1)) >= acc;
+        mine += f[k];
+      }
+      int tot;
+      int g = carry + block_exclusive_scan<GA_BLOCK, int, kL>(mine, tmp, tot);
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int d = db + k;
+        if (d < D) {
+          g += f[k];
+          const int eg = m_gaps >= 2 ? min(g, m_gaps - 1) : g;
+          if (const uint32_t k_cnt = S.cnt[d]) atomicAdd(&S.gcnt[eg], k_cnt);  // giants count in pass 5
+          S.cnt[d] = (uint32_t)eg;
+        }
+      }
+      carry += tot;
+    }
+    bar();
+    for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
+    bar();
+    return kOk;
+  }
   const int per = (D + GA_BLOCK - 1) / GA_BLOCK;
   const int d0 = tid * per;
   int my_gaps = 0, split = 0;
