@@ -125,7 +125,7 @@ def load_pmc_traffic(kernel: str, batch):
 def load_shape_traffic(key: str):
     """HBM bytes per call of an off-shape run (all the entry point's kernels), from
     the committed PMC passes of tools/gpu/shapes_pmc.sh over the same synthetic
-    batch (profiles/pmc_traffic_shapes.json, keys bm_<shape> / md_<shape>)."""
+    batch (profiles/pmc_traffic_shapes.json, keys bm_<shape> / md_<shape> / ga_<shape>)."""
     try:
         with open(os.path.join(REPO, "profiles", "pmc_traffic_shapes.json")) as fh:
             return json.load(fh).get(key)
@@ -441,7 +441,7 @@ def bin_mean_shapes(args, out):
 def gap_average_shapes(args, out):
     """Gap-average off the headline's shape, the same batches as bin_mean_shapes:
     600-peak spectra (thousands of occupied 0.01-Da buckets per cluster: the wide
-    kernel) and the configs[3] skewed law (its n = 5,000 giants: the global kernel)."""
+    kernel) and the configs[3] skewed law (its giants: the tiled giant pipeline)."""
     import torch
 
     from specpride_amd import engine
@@ -461,7 +461,7 @@ def gap_average_shapes(args, out):
                      "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1),
                      "ok_clusters": int((st == 0).sum()),
                      "roofline": roofline("spx_gap_average", "all gap-average kernels", consensus_bytes(batch, kept),
-                                          ms)}
+                                          ms, load_shape_traffic(f"ga_{name}"))}
         del ga, batch, t
         torch.cuda.empty_cache()
     out["gap_average_shapes"] = res

@@ -9,7 +9,13 @@ cd "$R"
 rm -rf gpurun_out/shapes_pmc && mkdir -p gpurun_out/shapes_pmc
 export TMPDIR=/tmp
 O=gpurun_out/shapes_pmc
-for S in "skewed_config3 bm" "long_spectra_600 bm" "long_spectra_600 md"; do
+# SHAPES_PMC (optional): a comma-separated subset, e.g. "skewed_config3 ga,long_spectra_600 ga"
+if [ -n "$SHAPES_PMC" ]; then
+  IFS=',' read -ra LIST <<< "$SHAPES_PMC"
+else
+  LIST=("skewed_config3 bm" "long_spectra_600 bm" "long_spectra_600 md" "skewed_config3 ga" "long_spectra_600 ga")
+fi
+for S in "${LIST[@]}"; do
   set -- $S
   N="$2_$1"
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$R/$O/$N/f" -o f --output-format csv -- python3 tools/run_shape.py $1 3 $2 > $O/$N.f.log 2>&1 || { tail -5 $O/$N.f.log; exit 1; }

@@ -1,6 +1,6 @@
 """Run one off-shape batch of bench.bin_mean_shapes / bench.medoid_shapes a few
 times (profiling driver): python tools/run_shape.py skewed_config3|long_spectra_600
-[reps] [bm|md]."""
+[reps] [bm|md|ga]."""
 import os
 import sys
 
@@ -22,6 +22,12 @@ if which == "md":
         engine.medoid(batch, out=md, check=False)
     torch.cuda.synchronize()
     print("ok", int((md.rep[:batch.n_clusters] < 0).sum().item()))
+elif which == "ga":
+    ga = engine.gap_average(batch)
+    for _ in range(reps):
+        engine.gap_average(batch, out=ga)
+    torch.cuda.synchronize()
+    print("ok", int((ga.status[:batch.n_clusters] != 0).sum().item()))
 else:
     bm = engine.bin_mean(batch)
     for _ in range(reps):

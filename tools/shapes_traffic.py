@@ -23,8 +23,9 @@ def counter_sum(d, name):
     tot = collections.defaultdict(float)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Kernel_Name"].startswith("spx::") and r["Counter_Name"] == name:
-                tot[r["Kernel_Name"].split("(")[0][5:]] += float(r["Counter_Value"])
+            kn = r["Kernel_Name"][5:] if r["Kernel_Name"].startswith("void ") else r["Kernel_Name"]  # templates
+            if kn.startswith("spx::") and r["Counter_Name"] == name:
+                tot[kn.split("(")[0][5:]] += float(r["Counter_Value"])
     return tot
 
 
