@@ -41,8 +41,9 @@ def main(root):
         times = {}
         for s in glob.glob(os.path.join(d, "kt", "**", "*kernel_stats.csv"), recursive=True):
             for r in csv.DictReader(open(s)):
-                if r["Name"].startswith("spx::"):
-                    times[r["Name"].split("(")[0][5:]] = (float(r["TotalDurationNs"]) / CALLS / 1e3)
+                kn = r["Name"][5:] if r["Name"].startswith("void ") else r["Name"]  # templates
+                if kn.startswith("spx::"):
+                    times[kn.split("(")[0][5:]] = (float(r["TotalDurationNs"]) / CALLS / 1e3)
         print(f"== {key}: {out[key] / 1e9:.3f} GB per call")
         for k in sorted(set(per_k) | set(times), key=lambda k: -times.get(k, 0.0)):
             if per_k.get(k, 0.0) > 1e6 or times.get(k, 0.0) > 5.0:
