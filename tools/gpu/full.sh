@@ -1,22 +1,20 @@
-#!/bin/bash
-# Round evidence: all GPU tests -> smoke -> bench (with extras) -> rocprofv3 kernel stats
-# of the headline bench -> PMC passes on the bench configuration.  Stops at the first failure.
-set -o pipefail
-R=${GRAFT_REPO_ROOT:-$PWD}
-cd "$R"
-mkdir -p gpurun_out
+#!/usr/bin/env bash
+# One GPU-box pass: parity tests, smoke, headline bench and a rocprofv3 kernel-trace summary.
+# Usage (from this container):  gpurun --timeout 1000 -- 'bash tools/gpu/full.sh r03_v12'
+# Every GPU step has its own time limit and the steps are chained with &&, so the first
+# failure (fault, abort, timeout) ends the script. Results land under gpurun_out/.
+set -euo pipefail
+tag="${1:-run}"
+root="${GRAFT_REPO_ROOT:-$(pwd)}"
+out="$root/gpurun_out"
+mkdir -p "$out"
+cd "$root"
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  > "$out/${tag}_gpu_tests.txt" 2>&1
+timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke(); print("SMOKE OK")' \
+  > "$out/${tag}_smoke.txt" 2>&1
+timeout -k 10 400 python bench.py > "$out/${tag}_bench.json" 2> "$out/${tag}_bench.err"
+cd /tmp
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
-rc=$?
-echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
-tail -3 gpurun_out/gpu_tests.log
-[ $rc -eq 0 ] || { grep -E "^(FAILED|E  )" gpurun_out/gpu_tests.log | head -30; exit 1; }
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -5 gpurun_out/smoke.log; exit 1; }
-tail -1 gpurun_out/smoke.log
-timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
-tail -1 gpurun_out/bench.log
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/prof.log 2>&1 || { tail -5 gpurun_out/prof.log; exit 1; }
-tail -1 gpurun_out/prof.log
-[ -n "$NO_PMC" ] && exit 0
-CLUSTERS=${PMC_CLUSTERS:-385000} bash tools/gpu/pmc.sh > gpurun_out/pmc.log 2>&1 || { tail -5 gpurun_out/pmc.log; exit 1; }
-echo pmc done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof_${tag}" -o run \
+  -- python3 "$root/bench.py" --steps 5 --warmup 2 > "$out/${tag}_prof_bench.log" 2>&1
