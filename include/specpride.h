@@ -61,7 +61,7 @@ typedef enum spx_status {
   SPX_MIXED_CHARGE = 1, /* binning.py:205-206 AssertionError / :131 ValueError   */
   SPX_NO_GAP = 2,       /* average_spectrum_clustering.py:69 IndexError          */
   SPX_EMPTY = 3,        /* average_spectrum_clustering.py:95 ValueError (max())  */
-  SPX_NON_FINITE = 4,   /* NaN/inf m/z or intensity in a gap-average cluster     */
+  SPX_NON_FINITE = 4,   /* spx_best_score: only NaN scores (gap-average carries NaN/inf as the reference does) */
   SPX_UNRESOLVED = 100  /* outside the engine's limits            */
 } spx_status;
 
@@ -134,7 +134,11 @@ typedef struct spx_gap_params {
 
 /* The workspace holds the global kernel's scratch slices and, when
  * info->max_cluster_peaks > 16,384, an arena of at most 1 GiB for the giant-cluster
- * pipeline (clusters past 16,384 peaks, tiled over the whole grid). */
+ * pipeline (clusters past 16,384 peaks, tiled over the whole grid).
+ * NaN / +-inf m/z or intensities give what the reference's numpy arithmetic gives
+ * (NaN sorts last, inf - inf = NaN in the cumsum differences, np.max propagates
+ * NaN): such a cluster is OK, possibly with NaN/inf values or no peaks, never an
+ * error status (average_spectrum_clustering.py:59-98). */
 size_t spx_gap_average_workspace_size(const spx_csr *csr, const spx_gap_params *params,
                                       const spx_batch_info *info);
 int spx_gap_average(const spx_csr *csr, const spx_gap_params *params, const spx_batch_info *info,

@@ -130,6 +130,8 @@ typedef struct { double mz, it; int64_t idx; } peak_t;
 
 static int cmp_peak(const void *x, const void *y) {
   const peak_t *a = (const peak_t *)x, *b = (const peak_t *)y;
+  const int an = isnan(a->mz), bn = isnan(b->mz);
+  if (an != bn) return an - bn;  /* np.argsort: NaN last */
   if (a->mz < b->mz) return -1;
   if (a->mz > b->mz) return 1;
   return (a->idx > b->idx) - (a->idx < b->idx);

@@ -54,8 +54,6 @@ def _raise_for(status):
         raise ValueError(_EMPTY_MSG)
     if status == engine.STATUS_MIXED_CHARGE:
         raise ValueError("There are different charge states in the cluster. Cannot average precursor m/z.")
-    if status == engine.STATUS_NON_FINITE:
-        raise ValueError("non-finite m/z or intensity in cluster (unsupported)")
     raise RuntimeError(f"gap-average failed with status {status}")
 
 

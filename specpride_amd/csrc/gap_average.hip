@@ -85,6 +85,7 @@ struct GapState {
   uint64_t* kmin;       // per slot min m/z key, later group fixed-point m/z sum
   uint64_t* kmax;       // per slot max m/z key, later group fixed-point intensity sum
   int wcap, dcap;
+  uint32_t* flags = nullptr;  // global scratch only: per emitted group, the non-finite classes it holds
 };
 
 template <int DCAP>
@@ -854,7 +855,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   PrecLanes pl{0, 0.0, 0.0};
   if (pn <= kWave) pl = prec_lanes(v, ps0, pn);
   const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
-  if (st == kDeferred) {
+  if (st == kDeferred || st == kNonFinite) {  // non-finite: the global kernel's gap_body_nf
     if (threadIdx.x == 0) {
       status[c] = kDeferred;
       striped_push(deferred, (int32_t)c);
@@ -884,7 +885,7 @@ __global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v
     PrecLanes pl{0, 0.0, 0.0};
     if (pn <= kWave) pl = prec_lanes(v, ps0, pn);
     const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
-    if (st == kDeferred) {
+    if (st == kDeferred || st == kNonFinite) {
       if (threadIdx.x == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;  // status stays kDeferred
     } else {
       gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank,
@@ -897,7 +898,7 @@ __global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v
 // Scratch slice of the deferred path: every array starts 256-B aligned (the
 // 64-bit atomics on kmin/kmax fault on a misaligned address).
 struct GapSliceLayout {
-  int64_t bitmap, wprefix, cnt, gcnt, kmin, kmax, total;
+  int64_t bitmap, wprefix, cnt, gcnt, kmin, kmax, flags, total;
 };
 __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
   GapSliceLayout L;
@@ -909,6 +910,7 @@ __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
   L.gcnt = take((int64_t)dcap * 4);
   L.kmin = take((int64_t)dcap * 8);
   L.kmax = take((int64_t)dcap * 8);
+  L.flags = take((int64_t)dcap * 4);
   L.total = o;
   return L;
 }
@@ -954,9 +956,303 @@ __device__ __forceinline__ GapState<uint32_t> gap_slice_state(char* base, int wc
   S.gcnt = reinterpret_cast<uint32_t*>(base + Lo.gcnt);
   S.kmin = reinterpret_cast<uint64_t*>(base + Lo.kmin);
   S.kmax = reinterpret_cast<uint64_t*>(base + Lo.kmax);
+  S.flags = reinterpret_cast<uint32_t*>(base + Lo.flags);
   S.wcap = wcap;
   S.dcap = dcap;
   return S;
+}
+
+// ------------------------------------------------------ non-finite clusters
+// A cluster holding a NaN or +-inf m/z or intensity: gap_body reports it
+// (kNonFinite) and the LDS and wide kernels hand it on, so only the global kernel
+// and the giant pipeline's last step run this body.  It reproduces what the
+// reference's own arithmetic does with such values (average_spectrum_clustering.py:59-98):
+//  * np.argsort puts -inf first, then the finite m/z, then +inf, NaN last;
+//  * np.diff >= acc holds from -inf to anything finite or +inf and from a finite
+//    m/z to +inf, never across a NaN difference (inf - inf, x - NaN): the -inf
+//    peaks are true group 0, the +inf and NaN peaks join the last true group;
+//  * a cumsum difference cm[e-1] - cm[s-1] is finite while everything up to the
+//    group's end is, +-inf when the group brings the first inf of one sign, and
+//    NaN otherwise (inf - inf, NaN) -- per column from the group's classes and the
+//    OR of the classes of the groups before it (nf_value);
+//  * np.max propagates NaN: a kept NaN intensity makes the threshold NaN and
+//    nothing is kept (no error).
+// The finite m/z take gap_body's buckets and slots; sums are the same fixed point
+// over the finite values.  Global scratch (S.flags), full barriers.
+constexpr uint32_t NF_MZ_NINF = 1u, NF_MZ_PINF = 2u, NF_MZ_NAN = 4u;  // intensity classes: << 3
+
+// 0 finite, 1 +inf, 2 -inf, 3 NaN: a cumsum over values of these classes
+__device__ __forceinline__ int nf_state(uint32_t f) {
+  f &= 7u;
+  if ((f & NF_MZ_NAN) || (f & 3u) == 3u) return 3;
+  return (f & NF_MZ_PINF) ? 1 : ((f & NF_MZ_NINF) ? 2 : 0);
+}
+// cm[e-1] - cm[s-1] (or cm[e-1] alone for s = 0) from the classes before the group (pre)
+// and in it (grp); `fin` is the value when everything up to the group's end is finite
+__device__ __forceinline__ double nf_value(uint32_t pre, uint32_t grp, double fin) {
+  const int a = nf_state(pre | grp);
+  if (a == 0) return fin;
+  if (a == 3 || nf_state(pre) != 0) return nan_d();
+  const double inf = __longlong_as_double(0x7ff0000000000000ll);
+  return a == 1 ? inf : -inf;
+}
+
+__device__ int32_t gap_body_nf(const CsrView& v, const GapParams& P, const GapState<uint32_t>& S, int64_t c,
+                               const PeaksOut& out, int* tmp, double* red, int* votes, uint32_t* ored) {
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1], n = s1 - s0;
+  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1], N = p1 - p0;
+  const double INF = __longlong_as_double(0x7ff0000000000000ll);
+  if (n == 0) return kNoGap;
+  auto emit_kept = [&](auto keep_at, auto mz_at, auto it_at, int64_t count) {  // ordered compaction
+    int64_t base = 0;
+    for (int64_t k0 = 0; k0 < count; k0 += GA_BLOCK) {  // uniform
+      const int64_t k = k0 + tid;
+      const int keep = k < count && keep_at(k);
+      int tot;
+      const int o = block_exclusive_scan<GA_BLOCK, int>(keep, tmp, tot);
+      if (keep) {
+        out.mz[p0 + base + o] = mz_at(k);
+        out.inten[p0 + base + o] = it_at(k);
+      }
+      base += tot;
+    }
+    if (tid == 0) out.count[c] = base;
+  };
+  if (n == 1) {  // passthrough + the dynamic-range filter (:88-98), NaN-propagating max
+    double mx = -INF;
+    int nanf = 0;
+    for (int64_t k = p0 + tid; k < p1; k += GA_BLOCK) {
+      const double it = v.inten[k];
+      nanf |= isnan(it);
+      mx = fmax(mx, it);
+    }
+    mx = wave_max_dpp(mx);
+    if (lane == 0) red[wid] = mx;
+    const int any_nan = block_any<GA_BLOCK, false>(nanf, votes, 0);
+    for (int w = 0; w < GA_NW; ++w) mx = fmax(mx, red[w]);
+    __syncthreads();
+    if (N == 0) return kEmpty;
+    const double thr = any_nan ? nan_d() : mx / P.dyn_range;
+    emit_kept([&](int64_t k) { return v.inten[p0 + k] >= thr; }, [&](int64_t k) { return v.mz[p0 + k]; },
+              [&](int64_t k) { return v.inten[p0 + k]; }, N);
+    return kOk;
+  }
+  if (N < 2) return kNoGap;
+
+  // 1: the finite m/z extent, max |finite intensity|, the non-finite m/z classes
+  double lo = INF, hi = -INF, imax = 0.0;
+  int cn = 0, cp = 0, cq = 0;
+  gap_peaks<true>(v, p0, p1, [&](int64_t, double m, double it) {
+    if (isfinite(m)) {
+      lo = fmin(lo, m);
+      hi = fmax(hi, m);
+    } else if (isnan(m)) {
+      ++cq;
+    } else if (m > 0.0) {
+      ++cp;
+    } else {
+      ++cn;
+    }
+    if (isfinite(it)) imax = fmax(imax, fabs(it));
+  });
+  lo = wave_min_dpp(lo);
+  hi = wave_max_dpp(hi);
+  imax = wave_max_dpp(imax);
+  if (lane == 0) { red[wid] = lo; red[GA_NW + wid] = hi; red[2 * GA_NW + wid] = imax; }
+  int n_ninf, n_pinf, n_nan;
+  block_exclusive_scan<GA_BLOCK, int>(cn, tmp, n_ninf);  // its barriers order red too
+  block_exclusive_scan<GA_BLOCK, int>(cp, tmp, n_pinf);
+  block_exclusive_scan<GA_BLOCK, int>(cq, tmp, n_nan);
+  for (int w = 0; w < GA_NW; ++w) {
+    lo = fmin(lo, red[w]);
+    hi = fmax(hi, red[GA_NW + w]);
+    imax = fmax(imax, red[2 * GA_NW + w]);
+  }
+  __syncthreads();
+  const int64_t Nf = N - n_ninf - n_pinf - n_nan;
+
+  // 2-4 over the finite m/z: buckets, slots, their extents, the finite gaps
+  int D = 0, fin_gaps = 0;
+  int64_t kb = 0;
+  const double acc = P.mz_accuracy;
+  auto key = [&](const uint64_t* a, int d) { return f64_from_order_key(a[d]); };
+  if (Nf > 0) {  // uniform
+    kb = floor_div_exact(lo, P.bucket_w, P.inv_bucket_w);
+    const int64_t nw = (floor_div_exact(hi, P.bucket_w, P.inv_bucket_w) - kb) / 64 + 1;
+    if (nw > S.wcap) return kDeferred;
+    for (int64_t w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
+    __syncthreads();
+    gap_peaks<false>(v, p0, p1, [&](int64_t, double m, double) {
+      if (isfinite(m)) {
+        const int64_t b = floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
+        atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
+      }
+    });
+    __syncthreads();
+    D = bitmap_prefix<GA_BLOCK, uint32_t, false>(S.bitmap, S.wprefix, (int)nw, tmp);
+    if (D > S.dcap) return kDeferred;
+    for (int d = tid; d < D; d += GA_BLOCK) {
+      S.cnt[d] = 0u;
+      S.kmin[d] = ~0ull;
+      S.kmax[d] = 0ull;
+    }
+    __syncthreads();
+    gap_peaks<false>(v, p0, p1, [&](int64_t, double m, double) {
+      if (isfinite(m)) {
+        const int slot = bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
+        const uint64_t k = f64_order_key(m);
+        atomicAdd(&S.cnt[slot], 1u);
+        atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)k);
+        atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)k);
+      }
+    });
+    __syncthreads();
+    int split = 0, my_gaps = 0;
+    for (int d = tid; d < D; d += GA_BLOCK) {
+      const double mx = key(S.kmax, d);
+      split |= (mx - key(S.kmin, d)) >= acc;  // a gap could hide inside the bucket
+      if (d + 1 < D) my_gaps += (key(S.kmin, d + 1) - mx) >= acc;
+    }
+    if (block_any<GA_BLOCK, false>(split, votes, 1)) return kDeferred;
+    block_exclusive_scan<GA_BLOCK, int>(my_gaps, tmp, fin_gaps);
+  }
+  // the boundaries: after the -inf peaks, the finite gaps, before the +inf peaks
+  const int b0 = (n_ninf > 0 && (Nf > 0 || n_pinf > 0)) ? 1 : 0;
+  const int be = (n_pinf > 0 && Nf > 0) ? 1 : 0;
+  const int M = b0 + fin_gaps + be;
+  if (M == 0) return kNoGap;
+  const int E = M >= 2 ? M : 2;
+  if (E > S.dcap) return kDeferred;
+  auto emitted = [&](int g) { return M >= 2 ? min(g, M - 1) : g; };  // the last two true groups merged (:79)
+  for (int e = tid; e < E; e += GA_BLOCK) {
+    S.gcnt[e] = 0u;
+    S.flags[e] = 0u;
+  }
+  __syncthreads();
+  // each finite slot's emitted group (rounds of 8 contiguous slots, as gap_groups)
+  constexpr int CH = 8;
+  int carry = 0;
+  for (int r0 = 0; r0 < D; r0 += GA_BLOCK * CH) {  // uniform
+    const int db = r0 + tid * CH;
+    int f[CH], mine = 0;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int d = db + k;
+      f[k] = d > 0 && d < D && (key(S.kmin, d) - key(S.kmax, d - 1)) >= acc;
+      mine += f[k];
+    }
+    int tot;
+    int g = b0 + carry + block_exclusive_scan<GA_BLOCK, int>(mine, tmp, tot);
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int d = db + k;
+      if (d < D) {
+        g += f[k];
+        const int eg = emitted(g);
+        atomicAdd(&S.gcnt[eg], S.cnt[d]);
+        S.cnt[d] = (uint32_t)eg;
+      }
+    }
+    carry += tot;
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += GA_BLOCK) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
+  __syncthreads();
+
+  // 5: fixed-point sums of the finite values, the non-finite m/z's counts, the classes
+  int ex_m, ex_i;
+  frexp(Nf > 0 ? fmax(fabs(lo), fabs(hi)) * (double)N : 0.0, &ex_m);
+  frexp(imax * (double)N, &ex_i);
+  const int sc_m = 61 - ex_m, sc_i = 61 - ex_i;
+  gap_peaks<true>(v, p0, p1, [&](int64_t, double m, double it) {
+    uint32_t fl = 0u;
+    int eg;
+    if (isfinite(m)) {
+      eg = (int)S.cnt[bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb)];
+      atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), (unsigned long long)__double2ll_rn(ldexp(m, sc_m)));
+    } else {
+      eg = emitted(m == -INF ? 0 : M);  // -inf: group 0; +inf and NaN: the last true group
+      atomicAdd(&S.gcnt[eg], 1u);
+      fl = isnan(m) ? NF_MZ_NAN : (m > 0.0 ? NF_MZ_PINF : NF_MZ_NINF);
+    }
+    if (isfinite(it))
+      atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[eg]), (unsigned long long)__double2ll_rn(ldexp(it, sc_i)));
+    else
+      fl |= (isnan(it) ? NF_MZ_NAN : (it > 0.0 ? NF_MZ_PINF : NF_MZ_NINF)) << 3;
+    if (fl) atomicOr(&S.flags[eg], fl);
+  });
+  __syncthreads();
+
+  // 6: values in group order (classes of the groups before each one), min_fraction,
+  // the NaN-propagating max, the dynamic-range filter, ordered output
+  const int gper = (E + GA_BLOCK - 1) / GA_BLOCK;
+  const int e0 = tid * gper;
+  uint32_t mine = 0u;
+  for (int j = 0; j < gper && e0 + j < E; ++j) mine |= S.flags[e0 + j];
+  ored[tid] = mine;
+  __syncthreads();
+  uint32_t pre = 0u;
+  for (int t = 0; t < tid; ++t) pre |= ored[t];
+  const double min_len = P.min_fraction * (double)n;
+  auto values = [&](int e, uint32_t pf, double& vm, double& vi) {
+    const uint32_t gf = S.flags[e];
+    vm = nf_value(pf, gf, ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e]);
+    vi = nf_value(pf >> 3, gf >> 3, ldexp((double)(int64_t)S.kmax[e], -sc_i) / (double)n);
+  };
+  double gmax = -INF;
+  int anyg = 0, gnan = 0;
+  {
+    uint32_t pf = pre;
+    for (int j = 0; j < gper && e0 + j < E; ++j) {
+      const int e = e0 + j;
+      double vm, vi;
+      values(e, pf, vm, vi);
+      pf |= S.flags[e];
+      if ((double)S.gcnt[e] >= min_len) {
+        anyg = 1;
+        if (isnan(vi)) gnan = 1;
+        else gmax = fmax(gmax, vi);
+      }
+    }
+  }
+  gmax = wave_max_dpp(gmax);
+  if (lane == 0) red[wid] = gmax;
+  const int any_kept = block_any<GA_BLOCK, false>(anyg, votes, 0);
+  const int any_nan = block_any<GA_BLOCK, false>(gnan, votes, 1);
+  for (int w = 0; w < GA_NW; ++w) gmax = fmax(gmax, red[w]);
+  __syncthreads();
+  if (!any_kept) return kEmpty;
+  const double thr = any_nan ? nan_d() : gmax / P.dyn_range;  // NaN: nothing passes `>=`
+  int cntk = 0;
+  {
+    uint32_t pf = pre;
+    for (int j = 0; j < gper && e0 + j < E; ++j) {
+      const int e = e0 + j;
+      double vm, vi;
+      values(e, pf, vm, vi);
+      pf |= S.flags[e];
+      cntk += (double)S.gcnt[e] >= min_len && vi >= thr;
+    }
+  }
+  int total;
+  int o = block_exclusive_scan<GA_BLOCK, int>(cntk, tmp, total);
+  {
+    uint32_t pf = pre;
+    for (int j = 0; j < gper && e0 + j < E; ++j) {
+      const int e = e0 + j;
+      double vm, vi;
+      values(e, pf, vm, vi);
+      pf |= S.flags[e];
+      if ((double)S.gcnt[e] >= min_len && vi >= thr) {
+        out.mz[p0 + o] = vm;
+        out.inten[p0 + o] = vi;
+        ++o;
+      }
+    }
+  }
+  if (tid == 0) out.count[c] = total;
+  return kOk;
 }
 
 // The giant's m/z extent as gap_body's pass 1 leaves it (lo, hi, imax; kb, nw)
@@ -1171,7 +1467,10 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, P
     } else {
       const int64_t s0 = A.v.cluster_off[c], n = A.v.cluster_off[c + 1] - s0;
       const int64_t p0 = A.v.spec_off[s0], N = A.v.spec_off[A.v.cluster_off[c + 1]] - p0;
-      if (st == kOk) {
+      if (H.bad) {  // NaN / inf: one workgroup runs the whole giant in its slice
+        st = gap_body_nf(A.v, A.P, S, c, out, tmp, red, votes, reinterpret_cast<uint32_t*>(stage));
+        __syncthreads();
+      } else if (st == kOk) {
         const GiantExtent X = giant_extent(H, A.P);
         int ex_m, ex_i;
         frexp(fmax(fabs(X.lo), fabs(X.hi)) * (double)N, &ex_m);
@@ -1236,6 +1535,10 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
       if (h) continue;
     }
     int32_t st = gap_body(v, P, S, c, out, tmp, red, votes);
+    if (st == kNonFinite) {
+      __syncthreads();
+      st = gap_body_nf(v, P, S, c, out, tmp, red, votes, reinterpret_cast<uint32_t*>(stage));
+    }
     if (st == kDeferred) {
       // bucket range beyond the scratch, or a bucket spanning >= mz_accuracy:
       // reported, never approximated (the host re-runs it through the sort path)

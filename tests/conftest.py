@@ -29,8 +29,8 @@ def load_json(name):
         return json.load(fh)
 
 
-BIN_SETS = ["edge", "synthetic", "params_b", "params_c", "mixed_charge"]
-GAP_SETS = ["edge", "synthetic", "params_b", "params_c"]
+BIN_SETS = ["edge", "synthetic", "params_b", "params_c", "mixed_charge", "nonfinite"]
+GAP_SETS = ["edge", "synthetic", "params_b", "params_c", "nonfinite", "nonfinite_b"]
 
 
 def bin_params(z):

@@ -15,6 +15,8 @@ Fixtures:
   bin_mean_<set>.npz        combine_bin_mean() per cluster (binning.py:170-231)
   bin_mean_cli_in.mgf/out   binning.py main() end to end (binning.py:250-302)
   gap_average_<set>.npz     average_spectrum() per cluster (average_spectrum_clustering.py:26-103)
+  *_nonfinite*              NaN / inf m/z and intensities: combine_bin_mean, average_spectrum and the
+                            binning CLI (``python tests/golden/make_golden.py nonfinite`` regenerates them)
   precursor_helpers.npz     lower_median_mass & co (average_spectrum_clustering.py:106-148)
   medoid_<set>.npz          most_similar_representative.main() reps (most_similar_representative.py:22-115)
   pairwise_sum.npz          numpy pairwise summation (the reduction pandas .sum() runs)
@@ -281,6 +283,163 @@ def gen_gap_average(asc):
                             status=np.array(status, np.int32),
                             params=np.array([p["mz_accuracy"], p["dyn_range"], p["min_fraction"]], np.float64))
         print(f"gap_average_{name}: {len(clusters)} clusters, {out_off[-1]} output peaks, status {status[:12]}")
+
+
+NAN, INF = float("nan"), float("inf")
+
+
+def gap_nonfinite_clusters(rng):
+    """NaN / +-inf m/z and intensities (no reference test covers them; these pin
+    what average_spectrum returns: argsort puts NaN last, diff >= acc is False
+    across NaN, the cumsum differences go inf/NaN, np.max propagates NaN)."""
+    S = lambda mz, it: {"m/z array": np.array(mz, float), "intensity array": np.array(it, float)}  # noqa: E731
+    cl = []
+    cl.append([S([100, NAN, 200], [1, 2, 3]), S([100, 200], [1, 3])])             # NaN m/z joins the last group
+    cl.append([S([100, 200], [1, NAN]), S([100, 200], [1, 1])])                    # NaN intensity: max NaN -> empty
+    cl.append([S([100, 200, 300], [NAN, 1, 1]), S([100, 200, 300], [1, 1, 1])])    # NaN in the first group
+    cl.append([S([100, 150, 200, 300], [1, NAN, 2, 3]), S([100, 200, 300], [1, 2, 3]),
+               S([100, 200, 300], [1, 2, 3])])                                     # NaN in a dropped group
+    cl.append([S([100, 200, 300, 400], [1, 2, 3, 4]), S([100, 200, 300, 400, 500], [1, 2, 3, 4, NAN]),
+               S([100, 200, 300, 400], [1, 2, 3, 4]), S([100, 200, 300, 400], [1, 2, 3, 4]),
+               S([100, 200, 300, 400], [1, 2, 3, 4])])                             # NaN in a dropped LAST group
+    cl.append([S([100, 200, 300], [1, INF, 3]), S([100, 200, 300], [1, 2, 3])])    # +inf intensity: keep inf only
+    cl.append([S([100, 200, 300, 400], [1, INF, 3, 4]), S([100, 200, 300, 400], [1, 2, 3, 4])])  # inf - inf
+    cl.append([S([100, 200, 300], [1, -INF, 3]), S([100, 200, 300], [1, 2, 3])])   # -inf intensity dropped
+    cl.append([S([100, 200, 300], [1, -INF, 3]), S([100, 200, 300], [1, INF, 3])])  # inf + -inf in one group
+    cl.append([S([100, 200, 300, 400], [-INF, 1, 3, 1]), S([100, 200, 300, 400], [1, 2, 3, 1])])  # -inf first
+    cl.append([S([100, 200, INF], [1, 2, 3]), S([100, 200], [1, 2])])             # +inf m/z
+    cl.append([S([100, 200, 300, INF], [1, 2, 3, 9]), S([100, 200, 300], [1, 2, 3])])  # +inf m/z, 3 groups
+    cl.append([S([-INF, 100, 200], [5, 1, 2]), S([100, 200], [1, 2])])            # -inf m/z
+    cl.append([S([-INF, 100, 200, 300], [5, 1, 2, 3]), S([-INF, 100, 200, 300], [5, 1, 2, 3])])
+    cl.append([S([-INF], [1]), S([INF], [1])])                                     # -inf | +inf
+    cl.append([S([-INF, NAN], [1, 2]), S([INF], [1])])
+    cl.append([S([-INF], [1]), S([-INF], [1])])                                    # no gap (NaN diff)
+    cl.append([S([NAN, NAN], [1, 2]), S([NAN], [3])])                              # all NaN -> IndexError
+    cl.append([S([100], [1]), S([NAN], [2])])                                      # finite + NaN -> IndexError
+    cl.append([S([100, 200, INF, NAN], [1, 1, 1, 1]), S([100, 200], [1, 1])])     # +inf then NaN
+    cl.append([S([100, 200, INF], [1, 1, 1]), S([150, INF, INF], [1, 1, 1])])      # inf - inf diff
+    cl.append([S([100, 200, NAN, NAN], [1, 2, 3, 4]), S([100, 200, NAN], [1, 2, 5]), S([100, 300], [1, 2])])
+    cl.append([S([100, 200, 300], [1, NAN, 3])])                                   # n=1: NaN max -> empty
+    cl.append([S([100, 200, 300], [1, INF, 3])])                                   # n=1: inf max
+    cl.append([S([NAN, 200, INF], [1, 2, 3])])                                     # n=1: m/z passthrough
+    cl.append([S([100, 200, 300], [-INF, 2, 3])])                                  # n=1: -inf dropped
+    cl.append([S([100, 200, 300], [5, 2, 3]), S([100, 200, 300], [NAN, NAN, NAN])])
+    cl.append([S([100, 100.004, 100.008, 200], [1, NAN, 1, 2]), S([100.002, 200], [1, 2])])
+    # synthetic clusters with a few entries replaced (m/z and intensity, all kinds)
+    base = make_clusters_np(40, seed=55, max_size=12, n_template=30)
+    for c in range(base.n_clusters):
+        sp = []
+        for s in range(base.cluster_off[c], base.cluster_off[c + 1]):
+            mz, it = base.spectrum(s)
+            mz, it = mz.copy(), it.copy()
+            if c % 4 != 0:
+                k = int(rng.integers(0, 3))
+                for _ in range(k):
+                    j = int(rng.integers(0, len(mz))) if len(mz) else 0
+                    if not len(mz):
+                        break
+                    v = [NAN, INF, -INF][int(rng.integers(0, 3))]
+                    if (c + s) % 3 == 0:
+                        it[j] = v
+                    else:
+                        mz[j] = v
+            sp.append(S(mz, it))
+        cl.append(sp)
+    return cl
+
+
+def bin_mean_nonfinite_clusters():
+    cl = []
+    cl.append([_spec([100.5, NAN, 200.0], [1, 2, 3]), _spec([100.5, 200.0], [1, 2])])       # NaN m/z masked
+    cl.append([_spec([100.5, INF, -INF, 300.0], [1, 2, 3, 4]), _spec([100.5, 300.0], [5, 6])])  # inf m/z masked
+    cl.append([_spec([100.5, 200.0], [NAN, 2]), _spec([100.5, 200.0], [1, 2])])             # NaN intensity bin
+    cl.append([_spec([100.5, 200.0], [INF, 2]), _spec([100.5, 200.0], [1, 2])])             # +inf bin
+    cl.append([_spec([100.5, 200.0], [-INF, 2]), _spec([100.5, 200.0], [INF, 2])])          # inf + -inf -> NaN
+    cl.append([_spec([100.5, 200.0], [1e39, 2]), _spec([100.5, 200.0], [1, 2])])            # f32 overflow
+    cl.append([_spec([150.001, NAN, 150.005], [10, 20, 40]), _spec([150.003], [1])])        # last wins past NaN
+    cl.append([_spec([150.001, 150.005], [10, NAN]), _spec([150.003], [1])])                # last is NaN
+    cl.append([_spec([150.001, 150.005], [NAN, 10]), _spec([150.003], [1])])                # NaN overwritten
+    cl.append([_spec([NAN, NAN], [1, 2]), _spec([NAN], [3])])                               # nothing in range
+    cl.append([_spec([200.0, 300.0], [1, 2])] * 3 + [_spec([200.0, 300.0], [NAN, INF])])  # 4 spectra, quorum 2
+    return cl
+
+
+def gen_nonfinite(binning, asc):
+    """bin_mean_nonfinite.npz / gap_average_nonfinite.npz: the reference run on
+    NaN / inf m/z and intensity (same layouts as the other bin_mean_* / gap_average_* sets)."""
+    rsc = binning.RepresentativeSpectrumCreator(verbose=0)
+    clusters = bin_mean_nonfinite_clusters()
+    out_mz, out_int, out_off, prec, charge, status = [], [], [0], [], [], []
+    with np.errstate(all="ignore"):
+        for pl in clusters:
+            r = rsc.combine_bin_mean(pl)
+            status.append(STATUS_OK)
+            out_mz.append(r["mzs"])
+            out_int.append(r["intensities"])
+            out_off.append(out_off[-1] + len(r["mzs"]))
+            prec.append(float(r["precursor_mz"]))
+            charge.append(int(r["precursor_charge"]))
+    csr = peaklists_to_csr(clusters)
+    np.savez_compressed(os.path.join(HERE, "bin_mean_nonfinite.npz"), **_csr_arrays(csr),
+                        out_off=np.array(out_off, np.int64), out_mz=_concat(out_mz),
+                        out_int=_concat(out_int), out_prec=np.array(prec), out_charge=np.array(charge, np.int32),
+                        status=np.array(status, np.int32),
+                        params=np.array([100, 2000, 0.02, 1.0], np.float64))
+    print(f"bin_mean_nonfinite: {len(clusters)} clusters, {out_off[-1]} output peaks")
+
+    # the binning CLI end to end on non-finite number tokens (float() spellings)
+    in_path = os.path.join(HERE, "bin_mean_cli_nonfinite_in.mgf")
+    out_path = os.path.join(HERE, "bin_mean_cli_nonfinite_out.mgf")
+    recs = [("c1", "u1", ["100.5 nan", "200.0 2.0", "300.0 inf"]),
+            ("c1", "u2", ["100.5 1.0", "200.0 -inf", "300.0 3.0"]),
+            ("c2", "u3", ["150.0 NaN", "1e999 5.0", "250.0 Infinity", "260.0 1e999"]),
+            ("c2", "u4", ["150.0 4.0", "250.0 -Infinity", "260.0 2.5"]),
+            ("c3", "u5", ["120.0 1e39", "130.0 -nan", "140.0 +inf"]),
+            ("c3", "u6", ["120.0 1.0", "130.0 2.0", "140.0 INF"])]
+    with open(in_path, "w") as fh:
+        for cid, usi, peaks in recs:
+            fh.write(f"BEGIN IONS\nTITLE={cid};{usi}\nPEPMASS=500.25\nCHARGE=2+\n")
+            fh.write("".join(p + "\n" for p in peaks))
+            fh.write("END IONS\n\n")
+    env = dict(os.environ, PYTHONPATH=STUBS)
+    with tempfile.TemporaryDirectory() as td:
+        r = subprocess.run([sys.executable, os.path.join(REF_SRC, "binning.py"), "--mgf_file", in_path,
+                            "--out", os.path.join(td, "out.mgf")], env=env, cwd=td, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(r.stderr)
+        with open(os.path.join(td, "out.mgf")) as src, open(out_path, "w") as dst:
+            dst.write(src.read())
+    print("bin_mean_cli_nonfinite: ok")
+
+    rng = np.random.default_rng(606)
+    sets = {"nonfinite": (gap_nonfinite_clusters(rng), dict())}
+    sets["nonfinite_b"] = (sets["nonfinite"][0], dict(mz_accuracy=0.02, dyn_range=100, min_fraction=0.3))
+    for name, (clusters, kw) in sets.items():
+        out_mz, out_int, out_off, status = [], [], [0], []
+        for sp in clusters:
+            try:
+                with np.errstate(all="ignore"):
+                    r = asc.average_spectrum(sp, "t", **kw)
+            except IndexError:
+                status.append(STATUS_NO_GAP)
+                out_off.append(out_off[-1])
+                continue
+            except ValueError:
+                status.append(STATUS_EMPTY)
+                out_off.append(out_off[-1])
+                continue
+            status.append(STATUS_OK)
+            out_mz.append(np.asarray(r["m/z array"], np.float64))
+            out_int.append(np.asarray(r["intensity array"], np.float64))
+            out_off.append(out_off[-1] + len(r["m/z array"]))
+        csr = SpectraCSR.from_clusters(clusters)
+        p = dict(mz_accuracy=asc.DIFF_THRESH, dyn_range=asc.DYN_RANGE, min_fraction=asc.MIN_FRACTION)
+        p.update(kw)
+        np.savez_compressed(os.path.join(HERE, f"gap_average_{name}.npz"), **_csr_arrays(csr),
+                            out_off=np.array(out_off, np.int64), out_mz=_concat(out_mz), out_int=_concat(out_int),
+                            status=np.array(status, np.int32),
+                            params=np.array([p["mz_accuracy"], p["dyn_range"], p["min_fraction"]], np.float64))
+        print(f"gap_average_{name}: {len(clusters)} clusters, {out_off[-1]} output peaks, status {status[:30]}")
 
 
 def gen_precursor_helpers(asc):
@@ -655,9 +814,13 @@ def main():
     if sys.argv[1:] == ["maracluster"]:
         gen_maracluster(binning)
         return
+    if sys.argv[1:] == ["nonfinite"]:
+        gen_nonfinite(binning, asc)
+        return
     gen_bin_mean(binning)
     gen_bin_mean_cli()
     gen_gap_average(asc)
+    gen_nonfinite(binning, asc)
     gen_precursor_helpers(asc)
     gen_pairwise()
     gen_medoid(msr)

@@ -221,17 +221,23 @@ def test_precursor_picks_large_clusters(gpu):
 
 def test_gap_average_giant_pipeline(gpu):
     """Clusters past GA_GIANT_N (16,384) peaks go from the global kernel to the
-    tiled giant pipeline.  24 clusters here: 21 giants, one with a NaN intensity
-    (SPX_NON_FINITE), giants on a coarse m/z grid (exact ties, several peaks per
-    bucket), a 2-spectrum giant, and small clusters between them.  Against the C
-    oracle: group structure exact, values within GAP_RTOL, under the default and
-    non-default parameters."""
+    tiled giant pipeline.  24 clusters here: 21 giants, one with a NaN intensity and
+    one with NaN / +-inf m/z (both go to gap_body_nf), giants on a coarse m/z grid
+    (exact ties, several peaks per bucket), a 2-spectrum giant, and small clusters
+    between them.  Against the C oracle (the reference's NaN arithmetic): group
+    structure exact, values within GAP_RTOL, under the default and non-default
+    parameters."""
     rng = np.random.default_rng(91)
     sizes = np.array([300, 5, 400, 2, 260, 280, 3, 350] + [270] * 14 + [1, 330])
     csr = make_clusters_np(len(sizes), seed=91, sizes=sizes, n_template=300)
     mz, it = csr.mz.copy(), csr.inten.copy()
     so, co = csr.spec_off, csr.cluster_off
-    it[so[co[4]] + 17] = np.nan  # cluster 4: non-finite
+    it[so[co[4]] + 17] = np.nan  # cluster 4: a NaN intensity
+    mz[so[co[7]] + 3] = np.nan   # cluster 7: NaN and +inf m/z (the merged last group)
+    mz[so[co[7] + 5] + 9] = np.inf
+    mz[so[co[13] + 9] + 1] = -np.inf  # cluster 13: -inf m/z (group 0; every later m/z NaN)
+    top = so[co[10]] + int(np.argmax(mz[so[co[10]]:so[co[11]]]))
+    it[top] = np.inf  # cluster 10: +inf intensity in the last group
     for c in (5, 9, 12):  # coarse grid, spectra kept sorted
         for s in range(co[c], co[c + 1]):
             a, b = so[s], so[s + 1]
@@ -254,15 +260,15 @@ def test_gap_average_giant_pipeline(gpu):
                      csr.charge, csr.rt)
     N = np.diff(spec_off[co])
     assert (N > 16384).sum() >= 21
-    st = engine.gap_average(engine.DeviceBatch.from_host(csr)).to_host()["status"]
-    assert st[4] == engine.STATUS_NON_FINITE and not np.delete(st, 4).any()
-    # the oracle carries NaN through the sums (the engine reports it instead), so
-    # the values are compared without cluster 4
-    sub = csr.select([c for c in range(csr.n_clusters) if c != 4])
-    batch = engine.DeviceBatch.from_host(sub)
+    batch = engine.DeviceBatch.from_host(csr)
     for kw in (dict(), dict(mz_accuracy=0.02, dyn_range=100.0, min_fraction=0.3)):
         got = engine.gap_average(batch, **kw).to_host()
-        assert_gap_close(got, c_oracle.gap_average(sub, **kw), kw.get("dyn_range", 1000.0))
+        assert not got["status"].any()
+        assert got["out_off"][5] == got["out_off"][4]  # the NaN intensity: max NaN -> nothing kept
+        o = got["out_off"]
+        assert o[14] > o[13] and np.isnan(got["out_mz"][o[13]:o[14]]).all()  # after -inf: cm differences NaN
+        assert np.isfinite(got["out_int"][o[13]:o[14]]).all()
+        assert_gap_close(got, c_oracle.gap_average(csr, **kw), kw.get("dyn_range", 1000.0))
 
 
 def test_gap_average_giant_overflow(gpu):

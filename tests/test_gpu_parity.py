@@ -190,10 +190,34 @@ def test_gap_average_deterministic_and_nonfinite(gpu, synth):
     r2 = engine.gap_average(b).to_host()
     for k in ("out_off", "out_mz", "out_int", "status"):
         np.testing.assert_array_equal(r1[k], r2[k])
+    # NaN sorts last and never opens a gap: [100, 100, NaN] has no gap -> the reference's IndexError
     bad = SpectraCSR.from_clusters([[{"m/z array": [100.0, np.nan], "intensity array": [1.0, 2.0]},
                                      {"m/z array": [100.0], "intensity array": [1.0]}]])
     r = engine.gap_average(engine.DeviceBatch.from_host(bad)).to_host()
-    assert r["status"][0] == engine.STATUS_NON_FINITE
+    assert r["status"][0] == engine.STATUS_NO_GAP
+
+
+def test_gap_average_nonfinite_mixed_into_large_batch(gpu, synth):
+    """Non-finite peaks sprinkled into a batch of ordinary clusters (every kernel of
+    the chain sees its share) against the numpy oracle -- the reference's own
+    arithmetic -- and no cluster status other than the oracle's."""
+    sub = synth.select(range(400))
+    rng = np.random.default_rng(12)
+    mz, it = sub.mz.copy(), sub.inten.copy()
+    for c in range(0, sub.n_clusters, 3):
+        a, b = sub.spec_off[sub.cluster_off[c]], sub.spec_off[sub.cluster_off[c + 1]]
+        for j in rng.integers(a, b, size=int(rng.integers(1, 4))):
+            v = [np.nan, np.inf, -np.inf][int(rng.integers(0, 3))]
+            if rng.random() < 0.5:
+                mz[j] = v
+            else:
+                it[j] = v
+    bad = SpectraCSR(sub.cluster_off, sub.spec_off, mz, it, sub.prec_mz, sub.charge, sub.rt)
+    for kw in (dict(), dict(mz_accuracy=0.02, dyn_range=100.0, min_fraction=0.3)):
+        got = engine.gap_average(engine.DeviceBatch.from_host(bad), **kw).to_host()
+        with np.errstate(all="ignore"):
+            ref = np_oracle.gap_average(bad, **kw)
+        assert_gap_close(got, ref, kw.get("dyn_range", 1000.0))
 
 
 def test_empty_batch_and_empty_clusters(gpu):

@@ -37,6 +37,30 @@ def test_binning_cli_byte_identical(gpu, tmp_path):
         assert out.read_bytes() == fh.read()
 
 
+def test_binning_cli_nonfinite_byte_identical(gpu, tmp_path):
+    """nan / inf / Infinity / 1e999 number tokens (Python float() spellings) through
+    the binning CLI: the same file as the reference's run (make_golden.py nonfinite)."""
+    out = tmp_path / "merged.mgf"
+    with contextlib.redirect_stdout(io.StringIO()):
+        binning.main(["--mgf_file", os.path.join(GOLDEN, "bin_mean_cli_nonfinite_in.mgf"), "--out", str(out)])
+    with open(os.path.join(GOLDEN, "bin_mean_cli_nonfinite_out.mgf"), "rb") as fh:
+        assert out.read_bytes() == fh.read()
+
+
+def test_average_spectrum_nonfinite_no_error(gpu):
+    """The reference returns output on NaN input (no exception): NaN m/z joins the
+    last group, a kept NaN intensity makes np.max NaN and keeps nothing."""
+    S = lambda mz, it: {"m/z array": np.array(mz, float), "intensity array": np.array(it, float)}  # noqa: E731
+    r = asc.average_spectrum([S([100, np.nan, 200], [1, 2, 3]), S([100, 200], [1, 3])])
+    np.testing.assert_array_equal(r["m/z array"], [100.0, np.nan])
+    np.testing.assert_array_equal(r["intensity array"], [1.0, 4.0])
+    r = asc.average_spectrum([S([100, 200], [1, np.nan]), S([100, 200], [1, 1])])
+    assert len(r["m/z array"]) == 0 and len(r["intensity array"]) == 0
+    r = asc.average_spectrum([S([100, 200, np.inf], [1, 2, 3]), S([100, 200], [1, 2])])
+    np.testing.assert_array_equal(r["m/z array"], [100.0, np.inf])
+    np.testing.assert_array_equal(r["intensity array"], [1.0, 3.5])
+
+
 def test_medoid_noncontiguous_runs(gpu, tmp_path):
     g = load_json("medoid_noncontiguous.json")
     spectra = read_mgf(os.path.join(GOLDEN, "medoid_noncontiguous.mgf"))
