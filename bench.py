@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="headline only (profiling runs)")
     ap.add_argument("--cpu-sample", type=int, default=2000, help="clusters in the CPU-baseline sample (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tier2-chunk-mb", type=int, default=2048, help="tier-2 pipeline chunk (MB of peaks)")
     return ap.parse_args()
 
 
@@ -152,6 +153,15 @@ def time_launches(fn, reps, stream):
     e1.record(stream)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps
+
+
+def kernel_ms(name: str) -> float:
+    """Average duration of one kernel's launches since _lib.profile_enable (HIP events
+    the library records around that launch on the caller's stream)."""
+    from specpride_amd import _lib
+
+    ms, n = _lib.profile_read(name)
+    return ms / n if n else float("nan")
 
 
 def cpu_baseline(n_clusters: int, seed: int):
@@ -272,10 +282,18 @@ def headline(args, rank, world, local, out):
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     value = world * batch.n_clusters * args.steps / elapsed
 
-    # per-kernel timing: HIP events on the stream the kernels are launched on
+    # per-kernel timing, after the timed region: HIP events on the stream the kernels
+    # are launched on -- around each whole entry point, and (spx_profile_*) around
+    # its dominant kernel's own launch inside the library
+    from specpride_amd import _lib
+
     reps = max(3, args.steps)
-    bm_ms = time_launches(lambda: engine.bin_mean(batch, out=bm), reps, stream)
-    md_ms = time_launches(lambda: engine.medoid(batch, out=md, check=False), reps, stream)
+    _lib.profile_enable(True)
+    bm_ms_ep = time_launches(lambda: engine.bin_mean(batch, out=bm), reps, stream)
+    md_ms_ep = time_launches(lambda: engine.medoid(batch, out=md, check=False), reps, stream)
+    bm_ms = kernel_ms("bin_mean_reg_kernel")
+    md_ms = kernel_ms("medoid_reg_kernel")
+    _lib.profile_enable(False)
     bm_bytes = consensus_bytes(batch, kept)
     out.update({
         "metric": "clusters/sec (whole node) for medoid + binned consensus",
@@ -302,7 +320,8 @@ def headline(args, rank, world, local, out):
                              load_pmc_traffic("bin_mean_reg_kernel", batch)),
         "roofline_medoid": roofline("spx_medoid", "medoid_reg_kernel", medoid_bytes(batch), md_ms,
                                     load_pmc_traffic("medoid_reg_kernel", batch)),
-        "kernels": {"spx_bin_mean_ms": round(bm_ms, 4), "spx_medoid_ms": round(md_ms, 4)},
+        "kernels": {"spx_bin_mean_ms": round(bm_ms_ep, 4), "spx_medoid_ms": round(md_ms_ep, 4),
+                    "bin_mean_reg_kernel_ms": round(bm_ms, 4), "medoid_reg_kernel_ms": round(md_ms, 4)},
     })
     if gat is not None:
         out["config"]["gathered_clusters_per_step"] = total_c
@@ -313,11 +332,14 @@ def headline(args, rank, world, local, out):
         torch.cuda.synchronize()
         gst = ga.status.cpu().numpy()[:batch.n_clusters]
         gkept = int(ga.count[:batch.n_clusters].sum().item())
+        _lib.profile_enable(True)
         ga_ms = time_launches(lambda: engine.gap_average(batch, out=ga), reps, stream)
+        ga_k = kernel_ms("gap_average_lds_kernel")
+        _lib.profile_enable(False)
         out["gap_average"] = {"clusters_per_s": round(batch.n_clusters / (ga_ms * 1e-3), 1), "launch_ms": round(ga_ms, 4),
-                              "ok_clusters": int((gst == 0).sum()),
+                              "lds_kernel_ms": round(ga_k, 4), "ok_clusters": int((gst == 0).sum()),
                               "roofline": roofline("spx_gap_average", "gap_average_lds_kernel",
-                                                   consensus_bytes(batch, gkept), ga_ms,
+                                                   consensus_bytes(batch, gkept), ga_k,
                                                    load_pmc_traffic("gap_average_lds_kernel", batch))}
         del ga
     del bm, md, bufs, batch, t
@@ -353,7 +375,26 @@ def north_star(args, out):
                             "clusters_per_s": round(batch.n_clusters * steps / dt, 1),
                             "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "all_resolved": ok,
                             "hbm_gb_resident": round(torch.cuda.max_memory_allocated() / 1e9, 1)}
-    del bm, md, batch, t
+    del bm, md
+    torch.cuda.empty_cache()
+    # configs[2]'s method on the same 1M clusters: gap-average (average_spectrum_clustering.py:151-165);
+    # configs[2] shards it over 8 GPUs, here one MI355X holds all of it
+    ga = engine.gap_average(batch)
+    torch.cuda.synchronize()
+    gst = ga.status.cpu().numpy()[:batch.n_clusters]
+    gkept = int(ga.count[:batch.n_clusters].sum().item())
+    from specpride_amd import _lib
+
+    _lib.profile_enable(True)
+    ga_ms = time_launches(lambda: engine.gap_average(batch, out=ga), 3, torch.cuda.current_stream())
+    ga_k = kernel_ms("gap_average_lds_kernel")
+    _lib.profile_enable(False)
+    out["north_star_1m"]["gap_average"] = {
+        "ms": round(ga_ms, 3), "clusters_per_s": round(batch.n_clusters / (ga_ms * 1e-3), 1),
+        "ok_clusters": int((gst == 0).sum()), "lds_kernel_ms": round(ga_k, 3),
+        "roofline": roofline("spx_gap_average", "gap_average_lds_kernel", consensus_bytes(batch, gkept), ga_k),
+        "hbm_gb_resident": round(torch.cuda.max_memory_allocated() / 1e9, 1)}
+    del ga, batch, t
     torch.cuda.empty_cache()
 
 
@@ -369,13 +410,47 @@ def config3(args, out):
     md = engine.medoid(batch, check=True)
     torch.cuda.synchronize()
     ok = bool(np.all(md.rep.cpu().numpy()[:batch.n_clusters] >= 0))
+    from specpride_amd import _lib
+
+    _lib.profile_enable(True)
     ms = time_launches(lambda: engine.medoid(batch, out=md, check=False), 5, torch.cuda.current_stream())
+    gram_ms = kernel_ms("medoid_gram_reg_kernel")
+    _lib.profile_enable(False)
     sizes = np.diff(batch.host_cluster_off)
+    ops = gram_ops(t, batch)
+    tops = ops / (gram_ms * 1e-3) / 1e12
     out["config3_medoid"] = {"clusters": batch.n_clusters, "spectra": batch.n_spectra, "max_n": int(sizes.max()),
                              "large_clusters": int((sizes > 64).sum()), "medoid_ms": round(ms, 3),
-                             "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1), "all_resolved": ok}
+                             "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1), "all_resolved": ok,
+                             "roofline": {"bound": "mfma", "kernel": "medoid_gram_reg_kernel",
+                                          "achieved": round(tops, 1), "peak": I8_DENSE_TOPS, "unit": "TOP/s",
+                                          "frac": round(tops / I8_DENSE_TOPS, 4), "traffic": None,
+                                          "launch_ms": round(gram_ms, 4), "algorithmic_ops": int(ops),
+                                          "ops_definition": "sum over the large-path clusters of 2*n(n+1)/2*K_c, "
+                                                            "K_c = distinct ceil(mz/0.1) bins of the cluster",
+                                          "entry_point": "spx_medoid"}}
     del md, batch, t
     torch.cuda.empty_cache()
+
+
+def gram_ops(t, batch) -> int:
+    """Algorithmic int ops of the large-cluster Gram: 2*n(n+1)/2*K_c
+    per cluster the MFMA path takes (n > 64 or past the small kernels' peak cap),
+    K_c its distinct ceil(mz/0.1) bins (most_similar_representative.py:88-93)."""
+    from specpride_amd.csr import SpectraCSR
+
+    co, so = batch.host_cluster_off, batch.host_spec_off
+    n = np.diff(co)
+    p = so[co[1:]] - so[co[:-1]]
+    big = np.flatnonzero((n > 64) | (p > 32768))
+    sub = SpectraCSR.select_from_device(t, big)
+    ops = 0
+    for k in range(sub.n_clusters):
+        a, b = sub.spec_off[sub.cluster_off[k]], sub.spec_off[sub.cluster_off[k + 1]]
+        kc = len(np.unique(np.ceil(sub.mz[a:b] / 0.1)))
+        nn = int(sub.cluster_off[k + 1] - sub.cluster_off[k])
+        ops += 2 * (nn * (nn + 1) // 2) * kc
+    return ops
 
 
 def medoid_shapes(args, out):
@@ -469,14 +544,17 @@ def gap_average_shapes(args, out):
 
 def tier2(args, out):
     """SURVEY.md §8(d) tier 2 at the headline's size (configs[4], 385k clusters, a
-    32 GB packed host CSR in pageable memory): H2D (engine.DeviceBatch.from_host:
-    spx_copy_h2d's pinned staging pool) -> spx_bin_mean + spx_medoid -> compaction
-    and D2H of the consensus peaks and representatives.  Never `value`."""
+    32 GB packed host CSR in pageable memory) through pipeline.HostPipeline: chunks of
+    whole clusters, H2D of chunk k+1 (spx_copy_h2d) overlapped with chunk k's
+    spx_bin_mean + spx_medoid and chunk k-1's compaction + D2H, device slots allocated
+    once (the first pass) and reused.  Timed: the second pass, host CSR in -> host
+    results out.  Never `value`."""
     import torch
 
-    from specpride_amd import engine
     from specpride_amd.csr import SpectraCSR
+    from specpride_amd.pipeline import HostPipeline
     from specpride_amd.synthetic import make_clusters_torch
+    from specpride_amd import engine
 
     t = make_clusters_torch(args.clusters, seed=args.seed + 11)
     h = {k: engine.to_host_array(t[k]) for k in ("cluster_off", "spec_off", "mz", "inten", "prec_mz", "charge", "rt")}
@@ -484,30 +562,29 @@ def tier2(args, out):
     torch.cuda.empty_cache()
     csr = SpectraCSR(h["cluster_off"], h["spec_off"], h["mz"], h["inten"], h["prec_mz"], h["charge"], h["rt"])
     nbytes = sum(a.nbytes for a in h.values())
+    pipe = HostPipeline(chunk_bytes=args.tier2_chunk_mb << 20)
     best = None
-    for _ in range(2):  # the first pass allocates the staging pool and the device memory
+    for rep_i in range(3):  # pass 0 allocates the device slots and the pinned staging pool
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        batch = engine.DeviceBatch.from_host(csr)
-        t1 = time.perf_counter()
-        bm = engine.bin_mean(batch)
-        md = engine.medoid(batch)
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        r = bm.to_host()
-        rep, _ = md.to_host()
-        t3 = time.perf_counter()
-        ok = bool(np.all(r["status"] == 0) and np.all(rep >= 0))
-        cur = {"clusters": batch.n_clusters, "host_bytes": int(nbytes), "h2d_s": round(t1 - t0, 4),
-               "h2d_GBs": round(nbytes / (t1 - t0) / 1e9, 2), "kernels_s": round(t2 - t1, 4),
-               "d2h_s": round(t3 - t2, 4), "d2h_bytes": int(16 * r["out_off"][-1] + 8 * len(rep)),
-               "clusters_per_s": round(batch.n_clusters / (t3 - t0), 1), "all_ok": ok}
+        r = pipe.run(csr)
+        dt = time.perf_counter() - t0
+        if rep_i == 0:
+            continue
+        ok = bool(np.all(r["status"] == 0) and np.all(r["rep"] >= 0))
+        tm = pipe.timing
+        cur = {"clusters": csr.n_clusters, "host_bytes": int(nbytes), "total_s": round(dt, 4),
+               "clusters_per_s": round(csr.n_clusters / dt, 1), "host_GBs": round(nbytes / dt / 1e9, 2),
+               "chunks": tm["chunks"], "chunk_mb": args.tier2_chunk_mb,
+               "h2d_issue_s": round(tm["h2d_host_s"], 4), "readback_s": round(tm["readback_s"], 4),
+               "kernels_s": round(tm["kernel_ms"] * 1e-3, 4),
+               "d2h_bytes": int(16 * r["out_off"][-1] + 8 * len(r["rep"])), "all_ok": ok}
         if best is None or cur["clusters_per_s"] > best["clusters_per_s"]:
             best = cur
-        del batch, bm, md, r, rep
-        torch.cuda.empty_cache()
+        del r
     out["tier2_host_inclusive"] = best
-    del csr, h
+    del pipe, csr, h
+    torch.cuda.empty_cache()
 
 
 def main():

@@ -235,6 +235,14 @@ int spx_copy_d2h(void *dst_host, const void *src_device, size_t nbytes, void *st
 int spx_abi_version(void);
 const char *spx_last_error(void); /* thread-local text of the last failure */
 
+/* Diagnostics (bench.py's per-kernel rooflines).  spx_profile_enable(1) brackets the
+ * launches of bin_mean_reg_kernel, medoid_reg_kernel, medoid_gram_reg_kernel,
+ * gap_average_lds_kernel and gap_average_wide_kernel with HIP events on the caller's
+ * stream (and resets the sums); spx_profile_read syncs on them and returns the summed
+ * duration and the launch count of one kernel.  Off by default: nothing recorded. */
+int spx_profile_enable(int on);
+int spx_profile_read(const char *kernel, double *total_ms, int64_t *launches);
+
 #ifdef __cplusplus
 }
 #endif

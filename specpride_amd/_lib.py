@@ -67,7 +67,7 @@ class SpxCosineParams(ctypes.Structure):
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_bin_mean_stage", "spx_gap_average_workspace_size", "spx_gap_average",
             "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
             "spx_compact_peaks", "spx_copy_h2d", "spx_copy_d2h",
-            "spx_abi_version", "spx_last_error"]
+            "spx_abi_version", "spx_last_error", "spx_profile_enable", "spx_profile_read"]
 
 SPX_ABI_VERSION = 2
 _lib = None
@@ -144,10 +144,24 @@ def lib():
     L.spx_best_score.argtypes = [_p, _p, _p, _p, _p, _p]
     L.spx_copy_h2d.argtypes = [_p, _p, _sz, _p]
     L.spx_copy_d2h.argtypes = [_p, _p, _sz, _p]
+    L.spx_profile_enable.argtypes = [_i32]
+    L.spx_profile_read.argtypes = [ctypes.c_char_p, _p, _p]
     if L.spx_abi_version() != SPX_ABI_VERSION:
         raise RuntimeError(f"libspecpride_hip ABI {L.spx_abi_version()} != {SPX_ABI_VERSION}")
     _lib = L
     return L
+
+
+def profile_enable(on: bool = True) -> None:
+    """Per-kernel event timing of the dominant kernels (spx_profile_enable)."""
+    check(lib().spx_profile_enable(int(bool(on))), "spx_profile_enable")
+
+
+def profile_read(kernel: str):
+    """(summed ms, launches) of one profiled kernel since profile_enable."""
+    ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
+    check(lib().spx_profile_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)), "spx_profile_read")
+    return ms.value, n.value
 
 
 def check(rc: int, what: str) -> None:

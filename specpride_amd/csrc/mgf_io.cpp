@@ -224,15 +224,18 @@ inline bool fast_peak_line(const char*& p, const char* e, bool single, double& a
 
 // One line of [p, e): [ls, le) without its terminator (\n, \r\n or \r: Python's
 // universal newlines), p advanced past it; false if the line holds a non-ASCII
-// byte (one pass over the bytes).
+// or a NUL byte (one pass over the bytes; titles cross the ABI as NUL-terminated
+// text, so a NUL inside one would cut every later title short).
 inline bool next_line(const char*& p, const char* e, const char*& ls, const char*& le) {
   ls = p;
   const char* q = p;
   unsigned char hi = 0;
+  bool nul = false;
   for (; q < e; ++q) {
     const unsigned char c = (unsigned char)*q;
     if (c == '\n' || c == '\r') break;
     hi |= c;
+    nul |= c == 0;
   }
   le = q;
   if (q < e) {
@@ -244,7 +247,7 @@ inline bool next_line(const char*& p, const char* e, const char*& ls, const char
     }
   }
   p = q;
-  return hi < 0x80;
+  return hi < 0x80 && !nul;
 }
 
 bool parse_charge(const char* b, const char* e, int64_t& out) {
@@ -287,7 +290,7 @@ void parse_range(const char* b, const char* e, Chunk& C) {
       }
     }
     const char *ls, *le;  // universal newlines, like Python text mode: \n, \r\n or \r
-    if (!next_line(p, e, ls, le)) { fail("non-ASCII text"); break; }
+    if (!next_line(p, e, ls, le)) { fail("non-ASCII or NUL text"); break; }
     const size_t n = (size_t)(le - ls);
     // peak lines first (most lines; none of the keywords below starts with a digit)
     if (n >= 1 && *ls >= '0' && *ls <= '9') {
@@ -401,7 +404,7 @@ void parse_range_general(const char* b, const char* e, GenChunk& C) {
       }
     }
     const char *ls, *le;
-    if (!next_line(p, e, ls, le)) { fail("non-ASCII text"); break; }
+    if (!next_line(p, e, ls, le)) { fail("non-ASCII or NUL text"); break; }
     const char *sb = ls, *se = le;
     strip(sb, se);
     const size_t n = (size_t)(se - sb);
@@ -856,6 +859,8 @@ void index_span(const char* b, size_t size, size_t lo, size_t hi, int general, I
       const char *tb = (general ? sb : ls) + 6, *te = general ? se : le;
       if (!general) strip(tb, te);
       title.assign(tb, te);
+      // titles cross the ABI NUL-terminated and '\n'-joined: a NUL would cut the rest
+      if (std::memchr(tb, 0, (size_t)(te - tb)) && X.error.empty()) X.error = "fallback: NUL byte in a TITLE";
     } else if (se - sb == 8 && std::memcmp(sb, "END IONS", 8) == 0) {
       has_end = true;
     } else if (se > sb && ((*(general ? sb : ls) >= '0' && *(general ? sb : ls) <= '9') ||
@@ -884,6 +889,7 @@ void index_stripes(const char* b, size_t size, size_t lo, size_t hi, int general
     X.end.insert(X.end.end(), x.end.begin(), x.end.end());
     X.npk.insert(X.npk.end(), x.npk.begin(), x.npk.end());
     X.titles += x.titles;
+    if (X.error.empty()) X.error = x.error;
   }
 }
 

@@ -77,7 +77,7 @@ class DeviceBatch:
     """A SpectraCSR mirrored into HBM, with the host metadata the ABI needs."""
 
     def __init__(self, tensors: dict, host_cluster_off: np.ndarray, host_spec_off: np.ndarray,
-                 max_mz_span: float, cluster_ids=None, titles=None):
+                 max_mz_span: float, cluster_ids=None, titles=None, buffers: Optional[dict] = None):
         self.t = tensors
         self.n_clusters = int(tensors["n_clusters"])
         self.n_spectra = int(tensors["n_spectra"])
@@ -93,7 +93,10 @@ class DeviceBatch:
                                _ptr(tensors.get("rt")))
         self.cluster_ids = cluster_ids or []
         self.titles = titles or []
-        self._ws = {}
+        self._ws = {}  # host-side facts of THIS batch (workspace sizes, large-path flags)
+        # workspace tensors by entry point; a caller streaming many batches through the
+        # same device memory (pipeline.HostPipeline) passes one dict to all of them
+        self._bufs = buffers if buffers is not None else {}
 
     @classmethod
     def from_host(cls, csr: SpectraCSR, device="cuda") -> "DeviceBatch":
@@ -125,10 +128,11 @@ class DeviceBatch:
     def workspace(self, key: str, nbytes: int):
         import torch
 
-        ws = self._ws.get(key)
+        ws = self._bufs.get(key)
         if ws is None or ws.numel() < nbytes:
+            self._bufs.pop(key, None)
             ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.t["mz"].device)
-            self._ws[key] = ws
+            self._bufs[key] = ws
         return ws
 
     @property
@@ -262,7 +266,7 @@ class PeaksResult:
         of kept peaks skips the one host read of the count sum (no sync)."""
         import torch
 
-        st = stream if stream is not None else (self.stream or torch.cuda.current_stream())
+        st = stream if stream is not None else (self.stream or torch.cuda.current_stream(self.count.device))
         C = self.batch.n_clusters
         with torch.cuda.stream(st):
             out_off = torch.zeros(C + 1, dtype=torch.int64, device=self.count.device)
@@ -291,8 +295,8 @@ class PeaksResult:
         if packed_readback(self.batch):
             return self._to_host_small()
         out_off, mz, inten = self.compact()
-        if self.stream is not None:
-            torch.cuda.current_stream().wait_stream(self.stream)
+        if self.stream is not None:  # the readback copies run on the batch device's current stream
+            torch.cuda.current_stream(self.batch.device).wait_stream(self.stream)
         d = dict(out_off=out_off.cpu().numpy(), out_mz=to_host_array(mz), out_int=to_host_array(inten),
                  status=self.status.cpu().numpy(), prec=self.prec.cpu().numpy(), charge=self.charge.cpu().numpy())
         if self.rt is not None:
@@ -306,7 +310,7 @@ class PeaksResult:
 
         C, P = self.batch.n_clusters, self.batch.n_peaks
         if self.stream is not None:
-            torch.cuda.current_stream().wait_stream(self.stream)
+            torch.cuda.current_stream(self.batch.device).wait_stream(self.stream)
         items = [("count", self.count[:C]), ("status", self.status[:C]), ("prec", self.prec[:C]),
                  ("charge", self.charge[:C]), ("mz", self.mz[:P]), ("inten", self.inten[:P])]
         if self.rt is not None:

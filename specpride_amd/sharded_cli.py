@@ -88,7 +88,12 @@ def rank_index(path, general: bool, group=None):
     order, so their concatenation is ``mgf_native.index(path, general)``)."""
     world, rank = shard.world_rank(group)
     size = os.path.getsize(path)
-    mine = mgf_native.index_range(path, general, rank * size // world, (rank + 1) * size // world)
+    try:
+        mine = mgf_native.index_range(path, general, rank * size // world, (rank + 1) * size // world)
+    except ValueError:  # outside the native subset (e.g. a NUL byte in a title): every rank agrees
+        mine = None
+    if not shard.all_true(mine is not None, group):
+        return None
     if world == 1:
         return mine
     titles = "\n".join(mine["titles"]).encode("utf-8", errors="surrogateescape")
@@ -103,9 +108,12 @@ def _load_my_clusters(path, general: bool, groups: Callable, method: str, group)
     """Index -> grouping -> plan -> parse own records.  Returns (ids, records,
     sizes, parts, mine, X, flat, ok): cluster ids, record indices in CSR order,
     members per cluster, the plan, this rank's clusters, the index, this rank's
-    parse (None if outside the native subset) and whether it is usable."""
+    parse (None if outside the native subset) and whether it is usable; None when
+    the file cannot be indexed natively (every rank then falls back)."""
     world, rank = shard.world_rank(group)
     X = rank_index(path, general, group)
+    if X is None:
+        return None
     ids, records, sizes = groups(X["titles"])
     starts = ingest.cluster_starts(sizes)
     peaks = np.add.reduceat(X["npk"][records], starts[:-1]) if len(records) else np.zeros(0, np.int64)
@@ -132,8 +140,10 @@ def binning(mgf_file: str, out: str, group=None, device=None, compute: Optional[
     from .binning import MIXED_CHARGE_MSG
     from .engine import STATUS_MIXED_CHARGE, STATUS_OK
 
-    ids, _rec, sizes, parts, mine, X, flat, ok = _load_my_clusters(mgf_file, False, ingest.binning_groups,
-                                                                   "bin_mean", group)
+    loaded = _load_my_clusters(mgf_file, False, ingest.binning_groups, "bin_mean", group)
+    if loaded is None:
+        return FALLBACK
+    ids, _rec, sizes, parts, mine, X, flat, ok = loaded
     ok = ok and all(";" in t for t in X["titles"]) and bool(flat["has_prec"].all() and flat["has_charge"].all())
     if not shard.all_true(ok, group):
         return FALLBACK
@@ -162,8 +172,10 @@ def gap_average(input_mgf: str, output, group=None, device=None, compute: Option
     from .engine import STATUS_OK
     from .mgf import write_pyteomics_style
 
-    ids, _rec, sizes, parts, mine, X, flat, ok = _load_my_clusters(input_mgf, True, ingest.gap_average_groups,
-                                                                   "gap_average", group)
+    loaded = _load_my_clusters(input_mgf, True, ingest.gap_average_groups, "gap_average", group)
+    if loaded is None:
+        return FALLBACK
+    ids, _rec, sizes, parts, mine, X, flat, ok = loaded
     ok = ok and bool(flat["has_title"].all())
     if not shard.all_true(ok, group):
         return FALLBACK
@@ -195,8 +207,10 @@ def medoid(inputfile: str, outputfile: str, group=None, device=None, compute: Op
     rank 0 only the representative spectra it chose."""
     import torch
 
-    ids, records, sizes, parts, mine, X, flat, ok = _load_my_clusters(inputfile, True, ingest.medoid_groups,
-                                                                      "medoid", group)
+    loaded = _load_my_clusters(inputfile, True, ingest.medoid_groups, "medoid", group)
+    if loaded is None:
+        return FALLBACK
+    ids, records, sizes, parts, mine, X, flat, ok = loaded
     ok = ok and bool(flat["has_title"].all())
     if not shard.all_true(ok, group):
         return FALLBACK

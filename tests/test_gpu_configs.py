@@ -9,8 +9,8 @@ the north star are quoted on), generated directly in HBM.
   bin-mean + medoid over the whole device batch, size-independent properties
   for every cluster, and a random 2,000-cluster subset of the same device
   batch against the oracle (bit-exact).
-* configs[2] -- one 125k-cluster shard of the 1M-cluster gap-average config
-  (what each of 8 GPUs holds): status 0 and properties for every cluster, a 2,000-cluster
+* configs[2] -- the 1M-cluster gap-average config whole on one GPU (it is sharded
+  over 8 in the config): status 0 and properties for every cluster, a 2,000-cluster
   subset against the numpy oracle (structure exact, values within GAP_RTOL).
 
 Reference semantics: binning.py:170-231 / :291-297, average_spectrum_clustering.py
@@ -97,15 +97,17 @@ def test_config5_full_pipeline_10m_spectra(gpu):
     np.testing.assert_array_equal(md_rep[pick] - co[pick], want - sub.cluster_off[:-1])
 
 
-def test_config2_gap_average_shard_125k(gpu):
-    """configs[2] is 1M clusters over 8 GPUs: one GPU's 125k-cluster shard."""
-    t = make_clusters_torch(125_000, seed=2)
+def test_config2_gap_average_1m_clusters(gpu):
+    """configs[2]: gap-average on 1M synthetic clusters (26M spectra, 5.2G peaks).  The
+    config shards it over 8 GPUs; one MI355X holds all of it (83 GB in, 83 GB out)."""
+    t = make_clusters_torch(1_000_000, seed=2)
     batch = engine.DeviceBatch.from_device(t)
+    assert batch.n_peaks > 5_000_000_000
     ga = engine.gap_average(batch).to_host()
     ok = ga["status"] == 0
     # on this synthetic law every cluster resolves (no SPX_UNRESOLVED, no empty result)
     assert np.all(ok), f"statuses {np.unique(ga['status'], return_counts=True)}"
-    counts = _check_peaks_properties(batch, ga)
+    _check_peaks_properties(batch, ga)
     # groups are disjoint sorted m/z runs: means strictly increase within a cluster
     off = ga["out_off"]
     d = np.diff(ga["out_mz"])
@@ -113,7 +115,7 @@ def test_config2_gap_average_shard_125k(gpu):
     b = off[1:-1] - 1  # d index between cluster c-1's last peak and cluster c's first
     inside[b[(b >= 0) & (b < len(d))]] = False
     assert np.all(d[inside] > 0)
-    assert np.all(counts[~ok] == 0)
+    del d, inside
     rng = np.random.default_rng(2)
     pick = np.sort(rng.choice(batch.n_clusters, 2000, replace=False))
     sub = SpectraCSR.select_from_device(t, pick)

@@ -17,4 +17,8 @@ timeout -k 10 400 python bench.py > "$out/${tag}_bench.json" 2> "$out/${tag}_ben
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof_${tag}" -o run \
-  -- python3 "$root/bench.py" --steps 5 --warmup 2 > "$out/${tag}_prof_bench.log" 2>&1
+  -- python3 "$root/bench.py" --steps 5 --warmup 2 --no-extras --no-cpu-baseline > "$out/${tag}_prof_bench.log" 2>&1
+cd "$root"
+if [ -z "${NO_PMC:-}" ]; then
+  CLUSTERS=385000 bash tools/gpu/pmc.sh > "$out/${tag}_pmc.txt" 2>&1
+fi
