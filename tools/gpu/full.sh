@@ -16,7 +16,7 @@ timeout -k 10 120 python -c 'import __graft_entry__ as g; g.smoke(); print("SMOK
 timeout -k 10 400 python bench.py > "$out/${tag}_bench.json" 2> "$out/${tag}_bench.err"
 cd /tmp
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof_${tag}" -o run \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof_${tag}" -o run --output-format csv \
   -- python3 "$root/bench.py" --steps 5 --warmup 2 --no-extras --no-cpu-baseline > "$out/${tag}_prof_bench.log" 2>&1
 cd "$root"
 if [ -z "${NO_PMC:-}" ]; then
