@@ -490,6 +490,9 @@ constexpr int BR_PFC = SPX_BR_PFC;    // phase-C (m/z, intensity) loads in fligh
 // none 2.24, 6 2.20, 8 2.14 ms); 12 or 20 at 4 waves/SIMD measured 2.28 / 2.23 ms
 // (fewer clusters in flight)
 constexpr int BR_KM = SPX_BR_KM;
+#ifndef SPX_BR_BG
+#define SPX_BR_BG 4  // phase-B steps whose LDS reads issue together (8: 2 VGPRs spilled)
+#endif
 constexpr int BR_W32 = 2 * BM_WMAX;   // 32-bit occupancy words
 // phases C-D accumulator of one slot: (intensity, m/z) sums and the contribution count
 struct alignas(16) BinAcc {
@@ -502,8 +505,10 @@ struct alignas(16) BinAcc {
 struct BinRegSmem {
   union alignas(16) {
     struct {
-      uint32_t bits[BR_W32];
-      uint16_t pre[BR_W32];
+      // + one dummy word per lane past the bitmap: bits 0, prefix BM_DCAP + lane, so
+      // a lane's no-contribution code maps to its own dummy accumulator record
+      uint32_t bits[BR_W32 + kWave];
+      uint16_t pre[BR_W32 + kWave];
     } b;                         // phases A-B
     BinAcc acc[BM_DCAP + kWave];  // phases C-D; [BM_DCAP + lane]: dummies
   } u;
@@ -595,6 +600,10 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     uint4* z = reinterpret_cast<uint4*>(L.u.b.bits) + tid * (BR_WPT / 4);
 #pragma unroll
     for (int k = 0; k < BR_WPT / 4; ++k) z[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (tid < kWave) {  // the dummy words (phase C's accumulators overwrote them)
+      L.u.b.bits[BR_W32 + tid] = 0u;
+      L.u.b.pre[BR_W32 + tid] = (uint16_t)(BM_DCAP + tid);
+    }
   }
   lds_barrier();
   SPX_STAMP(1);
@@ -649,8 +658,8 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       // LDS atomics serialise; distinct words do not)
       atomicOr(&bm32[valid ? key >> 5 : lane], valid ? 1u << (key & 31) : 0u);
       code[j] = valid ? key : -1;
-      // opaque to the compiler: phase B re-tests code >= 0 by a compare instead of
-      // keeping each step's 64-bit valid mask live (50 SGPR pairs: spills)
+      // opaque to the compiler: phase B must not keep each step's 64-bit valid mask
+      // live instead (50 SGPR pairs: spills)
       asm volatile("" : "+v"(code[j]));
     };
 #pragma unroll
@@ -679,14 +688,37 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   // phase C's read-modify-write)
   const int D = reg_prefix(L);
   if (D > BM_DCAP) return kDeferred;
-  reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
-    constexpr int j = decltype(jc)::value;
-    const bool valid = code[j] >= 0;
-    const uint32_t b = (uint32_t)(valid ? code[j] : 0);
-    const uint32_t w = b >> 5;
-    const int slot = (int)L.u.b.pre[w] + __popc(L.u.b.bits[w] & ((1u << (b & 31)) - 1u));
-    code[j] = valid ? slot : BM_DCAP + lane;  // a dummy slot of its own, never read
-  });
+  // Every step is the same two LDS reads and a popcount -- no branch: a code
+  // without contribution (-1: word 0x7FFFFFF, clamped to this lane's dummy word,
+  // bit 31 of an all-zero word) ranks to BM_DCAP + lane -- and a group of
+  // SPX_BR_BG steps issues its reads before the first use (one step at a time, each read
+  // waited for, was ~5k cycles of this phase).
+  {
+    constexpr int G = SPX_BR_BG;
+    int nn = __builtin_amdgcn_readfirstlane(n);
+#pragma unroll
+    for (int j0 = 0; j0 < BR_NMAX; j0 += G) {
+      asm volatile("" : "+s"(nn));  // one uniform guard per group, evaluated in place
+      if (j0 < nn) {
+        uint32_t wb[G], wp[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          if (j0 + q < BR_NMAX) {
+            const uint32_t w = min((uint32_t)code[j0 + q] >> 5, (uint32_t)(BR_W32 + lane));
+            wb[q] = L.u.b.bits[w];
+            wp[q] = L.u.b.pre[w];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+          if (j0 + q < BR_NMAX) {
+            const uint32_t b = (uint32_t)code[j0 + q];
+            code[j0 + q] = (int32_t)wp[q] + __popc(wb[q] & ((1u << (b & 31)) - 1u));
+          }
+        }
+      }
+    }
+  }
   lds_barrier();  // the bitmap is dead: the accumulators take its place
   for (int d = tid; d < D; d += BM_BLOCK) L.u.acc[d] = BinAcc{0.0f, 0.0f, 0u, 0u};
   lds_barrier();
