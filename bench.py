@@ -327,6 +327,21 @@ def headline(args, rank, world, local, out):
         out["config"]["gathered_clusters_per_step"] = total_c
         out["config"]["gathered_peaks_per_step"] = total_p
     if rank == 0 and world == 1 and not args.no_extras:
+        # the same step through the fused entry point (spx_bin_mean_medoid: both register
+        # bodies per workgroup, then each method's leftover chain); results checked equal
+        fbm, fmd = engine.bin_mean_medoid(batch)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(fbm.count[:batch.n_clusters], bm.count[:batch.n_clusters]) and
+                    torch.equal(fmd.rep[:batch.n_clusters], md.rep[:batch.n_clusters]))
+        _lib.profile_enable(True)
+        fu_ms = time_launches(lambda: engine.bin_mean_medoid(batch, out_bm=fbm, out_md=fmd, check=False), reps, stream)
+        fu_k = kernel_ms("bin_mean_medoid_kernel")
+        _lib.profile_enable(False)
+        out["fused_step"] = {"entry_point": "spx_bin_mean_medoid", "ms": round(fu_ms, 4),
+                             "clusters_per_s": round(batch.n_clusters / (fu_ms * 1e-3), 1),
+                             "fused_kernel_ms": round(fu_k, 4), "separate_ms": round(bm_ms_ep + md_ms_ep, 4),
+                             "results_equal_separate": same}
+        del fbm, fmd
         # gap-average consensus on the same resident batch (average_spectrum_clustering.py:26-148)
         ga = engine.gap_average(batch)
         torch.cuda.synchronize()

@@ -13,6 +13,7 @@
  *                       + precursor helpers :106-148 (called from :151-165)
  *   spx_medoid       <- src/most_similar_representative.py:13-19 distance() and the
  *                       per-cluster medoid loop :60-111
+ *   spx_bin_mean_medoid <- both of the above in one pass (the configs[4] pipeline step)
  *   spx_xcorr_distance <- src/most_similar_representative.py:13-19 distance() per pair
  *   spx_binned_cosine  <- src/benchmark.py:10-38  bin_proc / cos_dist / average_cos_dist
  *                       (representative vs its cluster members)
@@ -177,6 +178,18 @@ int spx_medoid_needs_large_path(const int64_t *host_cluster_off, const int64_t *
 int spx_medoid(const spx_csr *csr, const spx_medoid_params *params, int64_t *rep, double *totals,
                void *workspace, size_t workspace_bytes, void *stream);
 
+/* ---- the headline step in one pass: spx_bin_mean + spx_medoid over the same batch
+ *      (SURVEY.md §8(d) configs[4], "medoid + binned consensus").  Each cluster's
+ *      bin-mean and medoid register bodies run back to back in one workgroup
+ *      (bin_mean_medoid_kernel), then each method's own leftover chain; every output
+ *      equals the two separate calls'.  The workspaces are the two calls' own
+ *      (spx_bin_mean_workspace_size / spx_medoid_workspace_size). */
+int spx_bin_mean_medoid(const spx_csr *csr, const spx_bin_params *bin_params, const spx_batch_info *info,
+                        spx_peaks_out *out, double *prec_out, int32_t *charge_out, int32_t *status,
+                        void *bin_workspace, size_t bin_workspace_bytes, const spx_medoid_params *medoid_params,
+                        int64_t *rep, double *totals, void *medoid_workspace, size_t medoid_workspace_bytes,
+                        void *stream);
+
 /* distance(spec1, spec2, 'xcorr') = 1 - xCorrelationPrescore for n_pairs (global
  * spectrum index) pairs: out[p] for pairs[2p], pairs[2p+1].  The per-call API
  * behind most_similar_representative.distance (:13-19); not the batched path. */
@@ -237,7 +250,7 @@ const char *spx_last_error(void); /* thread-local text of the last failure */
 
 /* Diagnostics (bench.py's per-kernel rooflines).  spx_profile_enable(1) brackets the
  * launches of bin_mean_reg_kernel, medoid_reg_kernel, medoid_gram_reg_kernel,
- * gap_average_lds_kernel and gap_average_wide_kernel with HIP events on the caller's
+ * gap_average_lds_kernel, gap_average_wide_kernel and bin_mean_medoid_kernel with HIP events on the caller's
  * stream (and resets the sums); spx_profile_read syncs on them and returns the summed
  * duration and the launch count of one kernel.  Off by default: nothing recorded. */
 int spx_profile_enable(int on);

@@ -65,7 +65,7 @@ class SpxCosineParams(ctypes.Structure):
 
 # every symbol include/specpride.h declares (checked by tests/test_host.py)
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_bin_mean_stage", "spx_gap_average_workspace_size", "spx_gap_average",
-            "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
+            "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_bin_mean_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
             "spx_compact_peaks", "spx_copy_h2d", "spx_copy_d2h",
             "spx_abi_version", "spx_last_error", "spx_profile_enable", "spx_profile_read"]
 
@@ -144,8 +144,11 @@ def lib():
     L.spx_best_score.argtypes = [_p, _p, _p, _p, _p, _p]
     L.spx_copy_h2d.argtypes = [_p, _p, _sz, _p]
     L.spx_copy_d2h.argtypes = [_p, _p, _sz, _p]
-    L.spx_profile_enable.argtypes = [_i32]
-    L.spx_profile_read.argtypes = [ctypes.c_char_p, _p, _p]
+    # symbols added in ABI 2's round 4 (bound when present: A/B runs load older builds)
+    for name, argtypes in (("spx_bin_mean_medoid", [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _p, _p, _p, _p, _sz, _p]),
+                           ("spx_profile_enable", [_i32]), ("spx_profile_read", [ctypes.c_char_p, _p, _p])):
+        if hasattr(L, name):
+            getattr(L, name).argtypes = argtypes
     if L.spx_abi_version() != SPX_ABI_VERSION:
         raise RuntimeError(f"libspecpride_hip ABI {L.spx_abi_version()} != {SPX_ABI_VERSION}")
     _lib = L

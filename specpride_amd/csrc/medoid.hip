@@ -15,6 +15,7 @@
 // bit-packed Gram by AND + popcount).  Large clusters (n > 64, or an LDS
 // overflow) go to a deferred list and through the grid-parallel passes and the
 // MFMA Gram kernel below, with state in a bump-allocated global arena.
+#pragma once
 #include <type_traits>
 
 #include "spx_device.hpp"

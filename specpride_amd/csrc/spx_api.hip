@@ -28,6 +28,7 @@
 #include "binned_cosine.hip"
 #include "gap_average.hip"
 #include "medoid.hip"
+#include "fused.hip"
 #include "transfer.hip"
 
 namespace {
@@ -67,7 +68,7 @@ size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 // caller's stream; spx_profile_read syncs on them and sums.  Off by default: the
 // launch path then records nothing and never synchronises.
 constexpr const char* kProfNames[] = {"bin_mean_reg_kernel", "medoid_reg_kernel", "medoid_gram_reg_kernel",
-                                      "gap_average_lds_kernel", "gap_average_wide_kernel"};
+                                      "gap_average_lds_kernel", "gap_average_wide_kernel", "bin_mean_medoid_kernel"};
 constexpr int kProfN = sizeof(kProfNames) / sizeof(kProfNames[0]);
 struct ProfAcc {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
@@ -325,9 +326,20 @@ size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* par
   return w.used + (size_t)bin_mean_fallback_grid(C, params, dcap) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
-int spx_bin_mean_stage(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
-                       spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* workspace,
-                       size_t workspace_bytes, void* stream, int stage) {
+}  // extern "C"
+
+namespace {
+// The launch that replaces the register kernel's (spx_bin_mean_medoid: the fused
+// kernel), given the call's views; nullptr = bin_mean_reg_kernel itself.
+struct BinMeanHead {
+  int (*launch)(void* ctx, const spx::CsrView& V, const spx::BinMeanParams& P, const spx::PeaksOut& O,
+                double* prec_out, int32_t* charge_out, int32_t* status, const spx::StripedList& rest, hipStream_t s);
+  void* ctx;
+};
+
+int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
+                  spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* workspace,
+                  size_t workspace_bytes, void* stream, int stage, const BinMeanHead* head) {
   if (stage < 0 || stage > 2) return fail(SPX_EINVAL, "spx_bin_mean_stage: stage must be 0, 1 or 2");
   if (!csr_ok(csr) || !params || !info || !out || !out->count || !prec_out || !charge_out || !status)
     return fail(SPX_EINVAL, "spx_bin_mean: null argument");
@@ -380,11 +392,15 @@ int spx_bin_mean_stage(const spx_csr* csr, const spx_bin_params* params, const s
   if (stage != 2) {
     if (hipMemsetAsync(W.counters, 0, 512 + spx::kListCountBytes, s) != hipSuccess)
       return check_launch("spx_bin_mean memset");
-    ProfScope prof(0, s);
-    hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
-                       charge_out, status, W.rest);
-    prof.end();
-    if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
+    if (head) {
+      if (int rc = head->launch(head->ctx, V, P, O, prec_out, charge_out, status, W.rest, s)) return rc;
+    } else {
+      ProfScope prof(0, s);
+      hipLaunchKernelGGL(spx::bin_mean_reg_kernel, dim3((unsigned)C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                         charge_out, status, W.rest);
+      prof.end();
+      if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
+    }
     hipLaunchKernelGGL(spx::bin_mean_wide_kernel, gcl, dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out,
                        status, W.rest, W.def, n_def, W.glist, n_glist);
     if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
@@ -455,6 +471,17 @@ int spx_bin_mean_stage(const spx_csr* csr, const spx_bin_params* params, const s
                      charge_out, status, W.scl, n_scl, W.ranges, W.glist, n_glist);
   if (int rc = check_launch("bin_mean_split_emit_kernel")) return rc;
   return global_pass();
+}
+
+}  // namespace
+
+extern "C" {
+
+int spx_bin_mean_stage(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
+                       spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* workspace,
+                       size_t workspace_bytes, void* stream, int stage) {
+  return bin_mean_impl(csr, params, info, out, prec_out, charge_out, status, workspace, workspace_bytes, stream, stage,
+                       nullptr);
 }
 
 int spx_bin_mean(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info, spx_peaks_out* out,
@@ -616,8 +643,20 @@ int spx_medoid_needs_large_path(const int64_t* hco, const int64_t* hso, int64_t 
   return 0;
 }
 
-int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep, double* totals, void* workspace,
-               size_t workspace_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+// What the fused kernel needs of a medoid call prepared by part 1.
+struct MedoidHead {
+  spx::StripedList wide;
+  spx::MedoidParams P;
+};
+
+// part 0: the whole call; 1: checks, workspace carving and the memset only (the
+// caller launches the head kernel: spx_bin_mean_medoid); 2: everything after the
+// register kernel (the wide kernel and the large path), on the same workspace.
+int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep, double* totals, void* workspace,
+                size_t workspace_bytes, void* stream, int part, MedoidHead* head) {
   if (!csr_ok(csr) || !params || !rep) return fail(SPX_EINVAL, "spx_medoid: null argument");
   if (!(params->tolerance > 0)) return fail(SPX_EINVAL, "spx_medoid: tolerance must be > 0");
   const int64_t C = csr->n_clusters;
@@ -647,12 +686,21 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   // and an empty deferred list (the common case) costs a small launch
   const dim3 grid2(spx::MD_GRIDX, std::min<unsigned>(g, 32u)), blk(spx::MD_BLOCK);
 
-  // n_def, bump and the striped list's counters: the first 512 B + kListCountBytes
-  if (hipMemsetAsync(n_def, 0, 512 + spx::kListCountBytes, s) != hipSuccess) return check_launch("spx_medoid memset");
-  ProfScope prof_reg(1, s);
-  hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, wide);
-  prof_reg.end();
-  if (int rc = check_launch("medoid_reg_kernel")) return rc;
+  if (part != 2) {
+    // n_def, bump and the striped list's counters: the first 512 B + kListCountBytes
+    if (hipMemsetAsync(n_def, 0, 512 + spx::kListCountBytes, s) != hipSuccess) return check_launch("spx_medoid memset");
+  }
+  if (part == 1) {
+    head->wide = wide;
+    head->P = P;
+    return SPX_SUCCESS;
+  }
+  if (part == 0) {
+    ProfScope prof_reg(1, s);
+    hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, wide);
+    prof_reg.end();
+    if (int rc = check_launch("medoid_reg_kernel")) return rc;
+  }
   hipLaunchKernelGGL(spx::medoid_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024))),
                      dim3(spx::MW_BLOCK), 0, s, V, P, rep, totals, wide, def, n_def, meta);
   if (int rc = check_launch("medoid_wide_kernel")) return rc;
@@ -684,6 +732,48 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   if (int rc = check_launch("medoid_combine_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_argmin_kernel, dim3(g), blk, 0, s, meta, n_def, arena, rep);
   return check_launch("medoid_argmin_kernel");
+}
+
+struct FusedCtx {
+  const MedoidHead* md;
+  int64_t* rep;
+  double* totals;
+  int64_t C;
+};
+
+int fused_head(void* ctx, const spx::CsrView& V, const spx::BinMeanParams& P, const spx::PeaksOut& O, double* prec_out,
+               int32_t* charge_out, int32_t* status, const spx::StripedList& rest, hipStream_t s) {
+  const FusedCtx& F = *static_cast<const FusedCtx*>(ctx);
+  ProfScope prof(5, s);
+  hipLaunchKernelGGL(spx::bin_mean_medoid_kernel, dim3((unsigned)F.C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
+                     charge_out, status, rest, F.md->P, F.rep, F.totals, F.md->wide);
+  prof.end();
+  return check_launch("bin_mean_medoid_kernel");
+}
+}  // namespace
+
+extern "C" {
+
+int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep, double* totals, void* workspace,
+               size_t workspace_bytes, void* stream) {
+  return medoid_impl(csr, params, rep, totals, workspace, workspace_bytes, stream, 0, nullptr);
+}
+
+int spx_bin_mean_medoid(const spx_csr* csr, const spx_bin_params* bin_params, const spx_batch_info* info,
+                        spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* bin_workspace,
+                        size_t bin_workspace_bytes, const spx_medoid_params* medoid_params, int64_t* rep,
+                        double* totals, void* medoid_workspace, size_t medoid_workspace_bytes, void* stream) {
+  if (!csr_ok(csr)) return fail(SPX_EINVAL, "spx_bin_mean_medoid: null argument");
+  if (csr->n_clusters == 0) return SPX_SUCCESS;
+  MedoidHead H{};
+  if (int rc = medoid_impl(csr, medoid_params, rep, totals, medoid_workspace, medoid_workspace_bytes, stream, 1, &H))
+    return rc;
+  FusedCtx F{&H, rep, totals, csr->n_clusters};
+  const BinMeanHead head{fused_head, &F};
+  if (int rc = bin_mean_impl(csr, bin_params, info, out, prec_out, charge_out, status, bin_workspace,
+                             bin_workspace_bytes, stream, 0, &head))
+    return rc;
+  return medoid_impl(csr, medoid_params, rep, totals, medoid_workspace, medoid_workspace_bytes, stream, 2, nullptr);
 }
 
 }  // extern "C"

@@ -466,6 +466,53 @@ def medoid(batch: DeviceBatch, tolerance=0.1, with_totals=False, out: Optional[M
     return out
 
 
+def bin_mean_medoid(batch: DeviceBatch, minimum=100.0, maximum=2000.0, binsize=0.02, apply_peak_quorum=True,
+                    tolerance=0.1, out_bm: Optional[PeaksResult] = None, out_md: Optional[MedoidResult] = None,
+                    stream=None, check: bool = True):
+    """bin_mean() and medoid() of the same batch in one pass (spx_bin_mean_medoid: each
+    cluster's two register bodies share one workgroup); results identical to the two
+    calls.  ``check`` as in :func:`medoid` (run-time deferrals re-run by medoid()).
+    Returns (PeaksResult, MedoidResult)."""
+    import torch
+
+    L = _lib.lib()
+    prm = _lib.SpxBinParams(float(minimum), float(maximum), float(binsize), int(apply_peak_quorum is True))
+    need = L.spx_bin_mean_workspace_size(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info))
+    ws_bm = batch.workspace("bin_mean", need)
+    if out_bm is None:
+        mz, it, cnt, st, prec, ch = _alloc_peaks(batch)
+        out_bm = PeaksResult(batch, mz, it, cnt, st, prec, ch)
+    out_bm.stream = stream
+    out_bm.pending = None
+    if out_md is None:
+        out_md = MedoidResult(torch.empty(max(batch.n_clusters, 1), dtype=torch.int64, device=batch.device), None)
+    large = medoid_needs_large_path(batch)
+    extra = batch._ws.get("medoid_extra", ())
+    key = ("medoid_size", tuple(extra))
+    need_md = batch._ws.get(key)
+    if need_md is None:
+        ex = np.ascontiguousarray(extra, np.int64)
+        need_md = L.spx_medoid_workspace_size(batch.host_cluster_off.ctypes.data_as(ctypes.c_void_p),
+                                              batch.host_spec_off.ctypes.data_as(ctypes.c_void_p), batch.n_clusters,
+                                              ex.ctypes.data_as(ctypes.c_void_p) if len(ex) else None, len(ex))
+        if need_md == 0:
+            raise ValueError("spx_medoid_workspace_size: invalid offsets")
+        batch._ws[key] = need_md
+    ws_md = batch.workspace("medoid", need_md)
+    mprm = _lib.SpxMedoidParams(float(tolerance), int(bool(large or extra)))
+    po = _lib.SpxPeaksOut(_ptr(out_bm.mz), _ptr(out_bm.inten), _ptr(out_bm.count))
+    _lib.check(L.spx_bin_mean_medoid(ctypes.byref(batch.csr), ctypes.byref(prm), ctypes.byref(batch.info),
+                                     ctypes.byref(po), _ptr(out_bm.prec), _ptr(out_bm.charge), _ptr(out_bm.status),
+                                     _ptr(ws_bm), ws_bm.numel(), ctypes.byref(mprm), _ptr(out_md.rep),
+                                     _ptr(out_md.totals), _ptr(ws_md), ws_md.numel(), _stream_handle(stream)),
+               "spx_bin_mean_medoid")
+    if check and batch.n_clusters:
+        rep = out_md.rep[:batch.n_clusters]
+        if bool(((rep == REP_DEFERRED) | (rep == REP_ARENA)).any().item()):
+            medoid(batch, tolerance=tolerance, out=out_md, stream=stream, check=True)
+    return out_bm, out_md
+
+
 def xcorr_distance(batch: DeviceBatch, pairs, tolerance=0.1, stream=None):
     """1 - xcorr prescore (most_similar_representative.py:13-19) for (global
     spectrum index) pairs; returns a device f64 tensor."""

@@ -626,3 +626,36 @@ def test_medoid_empty_spectrum_positions(gpu):
     ref_rep, ref_tot = c_oracle.medoid(csr, with_totals=True)
     np.testing.assert_array_equal(rep, ref_rep)
     np.testing.assert_array_equal(tot, ref_tot)
+
+
+@pytest.mark.parametrize("shape", ["synth", "mixed"])
+def test_fused_bin_mean_medoid_equals_separate_calls(gpu, synth, shape):
+    """spx_bin_mean_medoid (one pass, both register bodies per workgroup) against the
+    separate entry points and the C oracle: every output bit-identical.  'mixed' adds
+    clusters past both register kernels (n > 50 / > 64, long spectra, unsorted,
+    mixed charge, empty) so both leftover chains run after the fused head."""
+    if shape == "synth":
+        csr = synth.select(range(800))
+    else:
+        sizes = np.array([3, 51, 65, 130, 2, 1, 0, 40, 7, 300], np.int64)
+        base = make_clusters_np(len(sizes), seed=17, sizes=sizes, n_template=120)
+        long = make_clusters_np(3, seed=18, sizes=np.array([12, 30, 45]), n_template=400)
+        csr = _shuffled(SpectraCSR.from_clusters(
+            [[{"m/z array": m, "intensity array": i, "precursor mz": float(base.prec_mz[base.cluster_off[c]]),
+               "precursor charge": int(base.charge[base.cluster_off[c]])} for m, i in base.cluster(c)]
+             for c in range(base.n_clusters)] +
+            [[{"m/z array": m, "intensity array": i, "precursor mz": 500.0, "precursor charge": 2}
+              for m, i in long.cluster(c)] for c in range(long.n_clusters)]))
+        ch = csr.charge.copy()
+        ch[csr.cluster_off[0] + 1] += 1  # cluster 0: mixed charges (bin-mean's AssertionError status)
+        csr = SpectraCSR(csr.cluster_off, csr.spec_off, csr.mz, csr.inten, csr.prec_mz, ch, csr.rt)
+    b = engine.DeviceBatch.from_host(csr)
+    bm, md = engine.bin_mean_medoid(b)
+    got = bm.to_host()
+    rep, _ = md.to_host()
+    want = _bin_mean(csr)
+    assert_bin_mean_equal(got, want)
+    assert_bin_mean_equal(got, c_oracle.bin_mean(csr))
+    rep2, _ = engine.medoid(engine.DeviceBatch.from_host(csr)).to_host()
+    np.testing.assert_array_equal(rep[:csr.n_clusters], rep2[:csr.n_clusters])
+    np.testing.assert_array_equal(rep[:csr.n_clusters], c_oracle.medoid(csr))

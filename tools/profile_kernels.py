@@ -87,6 +87,12 @@ def main():
         md = engine.medoid(b)
         res["medoid_ms"] = timed(lambda: engine.medoid(b, out=md, check=False))
         res["medoid_digest"] = digest(md.rep)
+    if "fu" in which:  # the fused step (spx_bin_mean_medoid): digests must equal bm's and md's
+        fbm, fmd = engine.bin_mean_medoid(b)
+        res["fused_ms"] = timed(lambda: engine.bin_mean_medoid(b, out_bm=fbm, out_md=fmd, check=False))
+        off, mz, it = fbm.compact()
+        res["fused_bin_mean_digest"] = digest(off, mz, it, fbm.status, fbm.prec, fbm.charge)
+        res["fused_medoid_digest"] = digest(fmd.rep)
     if "ga" in which:
         ga = engine.gap_average(b)
         res["gap_average_ms"] = timed(lambda: engine.gap_average(b, out=ga))
