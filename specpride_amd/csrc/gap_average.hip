@@ -47,6 +47,14 @@ constexpr int GA_NW = GA_BLOCK / kWave;
 #define SPX_GA_UM 20
 #endif
 constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10,240 per cluster: n <= 51 at ~200 peaks)
+#ifndef SPX_GA_DEFERBIG
+#define SPX_GA_DEFERBIG 1  // the LDS kernel hands clusters past its register capacity on unread
+#endif
+#ifndef SPX_GA_WUM
+#define SPX_GA_WUM 20
+#endif
+// the wide kernel's (40 spilled 135 VGPRs even at its 256-VGPR budget)
+constexpr int GA_WUM = SPX_GA_WUM;
 constexpr int GA_WMAX = 3584;  // 229,376 buckets (2,293 Da at 0.01)
 constexpr int GA_DCAP = 1536;  // occupied buckets per cluster
 static_assert(GA_WMAX % GA_BLOCK == 0, "the LDS bitmap is whole words per thread");
@@ -602,7 +610,7 @@ __device__ __forceinline__ int32_t gap_emit(const GapState<PrefixT>& S, const Ga
 }
 
 // --------------------------------------------------------------- the body
-template <class PrefixT>
+template <int UM, bool kDeferBig, class PrefixT>
 __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState<PrefixT>& S, int64_t c,
                             const PeaksOut& out, int* tmp, double* red, int* votes, const PrecLanes* pl = nullptr,
                             int* prank = nullptr) {
@@ -622,20 +630,28 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   if (n == 0) return kNoGap;
 
   // The cluster's m/z values are read from HBM ONCE into registers when they
-  // fit (<= GA_UM per thread = 10,240 peaks: nearly every U{2..50} cluster of
-  // the configs); passes 2-3 run from registers, pass 2's bucket per peak is
-  // kept for pass 3 and pass 3's slot for pass 5 (a u32 each).  Intensities are needed only by
-  // passes 1 and 5 and are streamed there (8 loads in flight), so the register
-  // budget holds twice as many peaks as m/z + intensity pairs would.  Larger
-  // clusters re-read both per pass.
-  const bool inreg = N <= (int64_t)GA_UM * GA_BLOCK;  // uniform
-  double rm[GA_UM];
-  uint32_t tags[GA_UM];  // per register peak: pass 2's bucket, then pass 3's slot (for pass 5)
+  // fit (<= UM per thread: 10,240 peaks); passes 2-3 run from registers, pass 2's bucket per peak is kept for
+  // pass 3 and pass 3's slot for pass 5 (a u32 each).  Intensities are needed
+  // only by passes 1 and 5 and are streamed there (8 loads in flight), so the
+  // register budget holds twice as many peaks as m/z + intensity pairs would.
+  // Larger clusters re-read per pass (the LDS kernel hands them to the wide one
+  // before reading anything).
+  if constexpr (kDeferBig) {
+    // the LDS kernel: to the wide kernel unread.  Tested on an opaque copy of N: the
+    // compiler must not learn that the streamed path below is dead (knowing it, it
+    // schedules the register path into 4 spilled VGPRs: 16.7 -> 17.2 ms, configs[4])
+    int64_t Nd = N;
+    asm volatile("" : "+s"(Nd));
+    if (Nd > (int64_t)UM * GA_BLOCK) return kDeferred;
+  }
+  const bool inreg = N <= (int64_t)UM * GA_BLOCK;  // uniform
+  double rm[UM];
+  uint32_t tags[UM];  // per register peak: pass 2's bucket, then pass 3's slot (for pass 5)
 #pragma unroll
-  for (int q = 0; q < GA_UM; ++q) tags[q] = 0u;
+  for (int q = 0; q < UM; ++q) tags[q] = 0u;
   if (inreg) {
 #pragma unroll
-    for (int u = 0; u < GA_UM; ++u) {
+    for (int u = 0; u < UM; ++u) {
       const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
       const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
       rm[u] = N > 0 ? v.mz[kk] : 0.0;
@@ -654,19 +670,19 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     if (inreg) {
       if (N == 0) return;  // uniform: no peaks (and the batch may hold none to load)
 #pragma unroll
-      for (int u0 = 0; u0 < GA_UM; u0 += 8) {
+      for (int u0 = 0; u0 < UM; u0 += 8) {
         double itb[8];
         if constexpr (kInten) {
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const int64_t k = p0 + (int64_t)(u0 + q) * GA_BLOCK + tid;
-            itb[q] = (u0 + q < GA_UM) ? v.inten[k < p1 ? k : p0] : 0.0;
+            itb[q] = (u0 + q < UM) ? v.inten[k < p1 ? k : p0] : 0.0;
           }
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int u = u0 + q;
-          if (u < GA_UM) {
+          if (u < UM) {
             const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
             int32_t tag = (int32_t)tags[u];
             if (k < p1) f(rm[u], kInten ? itb[q] : 0.0, tag);
@@ -854,7 +870,9 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
   PrecLanes pl{0, 0.0, 0.0};
   if (pn <= kWave) pl = prec_lanes(v, ps0, pn);
-  const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
+  // a cluster past the register capacity goes to the wide kernel unread: streamed
+  // here it would only be deferred after its bitmap pass (600-peak spectra from n ~ 18)
+  const int32_t st = gap_body<GA_UM, SPX_GA_DEFERBIG>(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
   if (st == kDeferred || st == kNonFinite) {  // non-finite: the global kernel's gap_body_nf
     if (threadIdx.x == 0) {
       status[c] = kDeferred;
@@ -884,7 +902,7 @@ __global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v
     const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
     PrecLanes pl{0, 0.0, 0.0};
     if (pn <= kWave) pl = prec_lanes(v, ps0, pn);
-    const int32_t st = gap_body(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
+    const int32_t st = gap_body<GA_WUM, false>(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
     if (st == kDeferred || st == kNonFinite) {
       if (threadIdx.x == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;  // status stays kDeferred
     } else {
@@ -930,6 +948,16 @@ constexpr int GA_GMAX = 256;                      // giant records per call
 constexpr int64_t GA_TILE = 2 * GA_BATCH * GA_BLOCK;  // peaks per tile
 constexpr int GA_GIANT_GRID = 1024;               // tile kernels' workgroups
 constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS first (50 KB)
+// More groups than that (the skewed law's giants: 6.5k-59k, mostly noise groups of
+// one peak): an open-addressing LDS table of HCAP groups per tile (a tile of ~40
+// spectra touches ~1-2k groups), flushed to the slice after each tile -- one global
+// add per (tile, group) instead of per peak.  A peak whose probe runs past
+// GA_HPROBE slots adds globally.  Integer adds, so the totals do not change.
+#ifndef SPX_GA_HASH
+#define SPX_GA_HASH 1
+#endif
+constexpr int GA_HCAP = 2048;
+constexpr int GA_HPROBE = 16;
 
 struct GapGiant {  // zeroed by the call's memset
   unsigned long long lo_inv, hi_key, imax_key;  // ~order key of the min m/z, order keys of max m/z, max |intensity|
@@ -1279,6 +1307,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
   __shared__ int votes[2 * GA_NW];
   __shared__ unsigned long long agg_m[PASS == 5 ? GA_GAGG : 1], agg_i[PASS == 5 ? GA_GAGG : 1];
   __shared__ uint32_t agg_c[PASS == 5 ? GA_GAGG : 1];
+  __shared__ uint32_t hkey[PASS == 5 && SPX_GA_HASH ? GA_HCAP : 1];  // group + 1 (0: empty)
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
   const int ng = min(*A.n_giant, A.gmax);
   auto peaks_of = [&](const GapGiant& H, int64_t& p0, int64_t& p1) {
@@ -1305,9 +1334,29 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
     }
   }
   int g = 0, cur = -1, E = 0, sc_m = 0, sc_i = 0;
-  bool agg = false;
+  bool agg = false, hashed = false;
   int64_t gbase = 0, gtiles = ng > 0 ? tiles_of(A.giants[0]) : 0, p0 = 0, p1 = 0, kb = 0;
   GapState<uint32_t> S{};
+  // the hashed table after a tile: every occupied entry to the slice, the table emptied
+  auto hflush = [&]() __attribute__((always_inline)) {
+    if constexpr (PASS == 5 && SPX_GA_HASH) {
+      lds_barrier();
+      for (int h = tid; h < GA_HCAP; h += GA_BLOCK) {
+        const uint32_t k = hkey[h];
+        if (k) {
+          const uint32_t e = k - 1u;
+          atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[e]), agg_m[h]);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[e]), agg_i[h]);
+          atomicAdd(&S.gcnt[e], agg_c[h]);
+          hkey[h] = 0u;
+          agg_m[h] = 0ull;
+          agg_i[h] = 0ull;
+          agg_c[h] = 0u;
+        }
+      }
+      lds_barrier();
+    }
+  };
   auto flush = [&]() __attribute__((always_inline)) {  // PASS 5: the LDS sums of giant `cur`
     if constexpr (PASS == 5) {
       if (agg) {
@@ -1349,8 +1398,12 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           // per group at the end (integer adds: the same totals)
           E = H.E;
           agg = E <= GA_GAGG;
+          hashed = SPX_GA_HASH && !agg;
           if (agg) {
             for (int e = tid; e < E; e += GA_BLOCK) { agg_m[e] = 0ull; agg_i[e] = 0ull; agg_c[e] = 0u; }
+            lds_barrier();
+          } else if (hashed) {
+            for (int h = tid; h < GA_HCAP; h += GA_BLOCK) { hkey[h] = 0u; agg_m[h] = 0ull; agg_i[h] = 0ull; agg_c[h] = 0u; }
             lds_barrier();
           }
         }
@@ -1409,13 +1462,35 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
             atomicAdd(&agg_m[eg], qm);
             atomicAdd(&agg_i[eg], qi);
             atomicAdd(&agg_c[eg], 1u);
-          } else {
-            atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), qm);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[eg]), qi);
-            atomicAdd(&S.gcnt[eg], 1u);
+            return;
           }
+          if constexpr (SPX_GA_HASH) {
+            if (hashed) {
+              const uint32_t want = eg + 1u;
+              uint32_t h = (eg * 2654435761u) >> (32 - 11);  // log2(GA_HCAP) = 11
+              for (int probe = 0; probe < GA_HPROBE; ++probe, h = (h + 1u) & (GA_HCAP - 1)) {
+                uint32_t k = hkey[h];
+                if (k == 0u) {
+                  const uint32_t old = atomicCAS(&hkey[h], 0u, want);
+                  k = old == 0u ? want : old;
+                }
+                if (k == want) {
+                  atomicAdd(&agg_m[h], qm);
+                  atomicAdd(&agg_i[h], qi);
+                  atomicAdd(&agg_c[h], 1u);
+                  return;
+                }
+              }
+            }
+          }
+          atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), qm);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[eg]), qi);
+          atomicAdd(&S.gcnt[eg], 1u);
         }
       });
+      if constexpr (PASS == 5 && SPX_GA_HASH) {
+        if (hashed) hflush();  // uniform: the giant's mode
+      }
     }
   }
   flush();
@@ -1534,7 +1609,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
       __syncthreads();
       if (h) continue;
     }
-    int32_t st = gap_body(v, P, S, c, out, tmp, red, votes);
+    int32_t st = gap_body<GA_UM, false>(v, P, S, c, out, tmp, red, votes);
     if (st == kNonFinite) {
       __syncthreads();
       st = gap_body_nf(v, P, S, c, out, tmp, red, votes, reinterpret_cast<uint32_t*>(stage));

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--stamps-kernel", default="bm", choices=["bm", "md", "ga"])
     ap.add_argument("--build-stamps", action="store_true")
+    ap.add_argument("--shape", default=None, help="an off-shape batch of tools/run_shape.py (skewed_config3, long_spectra_600)")
     a = ap.parse_args()
     if a.build_stamps:
         build_stamps()
@@ -53,7 +54,13 @@ def main():
     from specpride_amd import _lib, engine
     from specpride_amd.synthetic import make_clusters_torch
 
-    t = make_clusters_torch(a.clusters, seed=a.seed)
+    if a.shape:
+        sys.argv = sys.argv[:1]  # run_shape parses argv at import: only its SHAPES table is used
+        shapes = {"skewed_config3": dict(n_clusters=20000, seed=4, skewed=True, forced_large=4, large_size=5000),
+                  "long_spectra_600": dict(n_clusters=20000, seed=6, n_template=600)}
+        t = make_clusters_torch(**shapes[a.shape])
+    else:
+        t = make_clusters_torch(a.clusters, seed=a.seed)
     b = engine.DeviceBatch.from_device(t)
     which = a.which.split(",")
     res = {"clusters": b.n_clusters, "spectra": b.n_spectra, "peaks": b.n_peaks}
