@@ -429,7 +429,7 @@ def config3(args, out):
 
     _lib.profile_enable(True)
     ms = time_launches(lambda: engine.medoid(batch, out=md, check=False), 5, torch.cuda.current_stream())
-    gram_ms = kernel_ms("medoid_gram_reg_kernel")
+    gram_ms = kernel_ms("medoid_gram_kernel")
     _lib.profile_enable(False)
     sizes = np.diff(batch.host_cluster_off)
     ops = gram_ops(t, batch)

@@ -249,7 +249,7 @@ int spx_abi_version(void);
 const char *spx_last_error(void); /* thread-local text of the last failure */
 
 /* Diagnostics (bench.py's per-kernel rooflines).  spx_profile_enable(1) brackets the
- * launches of bin_mean_reg_kernel, medoid_reg_kernel, medoid_gram_reg_kernel,
+ * launches of bin_mean_reg_kernel, medoid_reg_kernel, the medoid Gram kernel ("medoid_gram_kernel"),
  * gap_average_lds_kernel, gap_average_wide_kernel and bin_mean_medoid_kernel with HIP events on the caller's
  * stream (and resets the sums); spx_profile_read syncs on them and returns the summed
  * duration and the launch count of one kernel.  Off by default: nothing recorded. */

@@ -67,7 +67,7 @@ size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 // (spx_profile_enable), the launches below are bracketed by HIP events on the
 // caller's stream; spx_profile_read syncs on them and sums.  Off by default: the
 // launch path then records nothing and never synchronises.
-constexpr const char* kProfNames[] = {"bin_mean_reg_kernel", "medoid_reg_kernel", "medoid_gram_reg_kernel",
+constexpr const char* kProfNames[] = {"bin_mean_reg_kernel", "medoid_reg_kernel", "medoid_gram_kernel",
                                       "gap_average_lds_kernel", "gap_average_wide_kernel", "bin_mean_medoid_kernel"};
 constexpr int kProfN = sizeof(kProfNames) / sizeof(kProfNames[0]);
 struct ProfAcc {
@@ -725,7 +725,7 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
   ProfScope prof_gram(2, s);
   hipLaunchKernelGGL(spx::medoid_gram_reg_kernel, dim3(2048), blk, 0, s, meta, n_def, tile_base, arena);
   prof_gram.end();
-  if (int rc = check_launch("medoid_gram_reg_kernel")) return rc;
+  if (int rc = check_launch("medoid_gram kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_leaves_kernel, dim3(4096), blk, 0, s, V, meta, n_def, unit_base, arena);
   if (int rc = check_launch("medoid_leaves_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_combine_kernel, dim3(1024), blk, 0, s, meta, n_def, chunk_base, arena, totals);
