@@ -528,20 +528,6 @@ __host__ __device__ __forceinline__ int64_t md_gr_tiles(int n) {
   return t;
 }
 
-#ifndef SPX_MD_GRAM_LDS
-#define SPX_MD_GRAM_LDS 1
-#endif
-constexpr int MG_BT = 128;         // block rows = cols
-constexpr int MG_RS = 48;          // bytes per (row, half) record
-constexpr int MG_STAGE = 2 * 2 * MG_BT * MG_RS;  // [hf][256 rows][48 B] = 24 KB
-constexpr int MG_PF = 6;           // row words in flight per thread
-
-// WG tiles of a cluster: 128-row blocks I against 128-column blocks J >= I
-__host__ __device__ __forceinline__ int64_t md_gb_tiles(int n) {
-  const int64_t T = (n + MG_BT - 1) / MG_BT;
-  return T * (T + 1) / 2;
-}
-
 constexpr int MD_GRIDX = 64;      // blocks per cluster in the grid-parallel passes
 
 __host__ __device__ __forceinline__ int64_t md_align(int64_t b) { return (b + 255) & ~int64_t(255); }
@@ -1023,497 +1009,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidM
   }
 }
 
-constexpr int MD_GRIDX = 64;      // blocks per cluster in the grid-parallel passes
-
-__host__ __device__ __forceinline__ int64_t md_align(int64_t b) { return (b + 255) & ~int64_t(255); }
-__host__ __device__ __forceinline__ int64_t md_l1_bytes() { return md_align((int64_t)MD_L1WORDS * 12); }
-__host__ __device__ __forceinline__ int64_t md_max_leaves(int64_t n) { return n / 32 + 2; }
-
-__device__ __forceinline__ unsigned long long md_key(int64_t b) {
-  return (unsigned long long)b ^ 0x8000000000000000ull;
-}
-__device__ __forceinline__ int64_t md_unkey(unsigned long long k) { return (int64_t)(k ^ 0x8000000000000000ull); }
-
-struct MedoidTables {  // views into the arena
-  const unsigned long long* l1;
-  const uint32_t* l1pre;
-  const unsigned long long* l2;
-  const uint32_t* l2pre;
-  __device__ __forceinline__ int column(int64_t rel) const {
-    const int bs = bitmap_rank(l1, l1pre, rel >> 6);
-    return (int)l2pre[bs] + __popcll(l2[bs] & ((1ull << (rel & 63)) - 1ull));
-  }
-};
-
-__device__ __forceinline__ MedoidTables md_tables(const char* arena, const MedoidMeta& M) {
-  MedoidTables T;
-  T.l1 = reinterpret_cast<const unsigned long long*>(arena + M.l1_off);
-  T.l1pre = reinterpret_cast<const uint32_t*>(arena + M.l1_off + (int64_t)MD_L1WORDS * 8);
-  T.l2 = reinterpret_cast<const unsigned long long*>(arena + M.l2_off);
-  T.l2pre = reinterpret_cast<const uint32_t*>(arena + M.l2_off + (int64_t)M.B1 * 8);
-  return T;
-}
-
-__device__ __forceinline__ int64_t md_bump(unsigned long long* bump, int64_t bytes, int64_t cap) {
-  const int64_t b = (int64_t)atomicAdd(bump, (unsigned long long)bytes);
-  return b + bytes > cap ? -1 : b;
-}
-
-// Pass 1: bin range of every deferred cluster (wave-reduced atomics on
-// order-preserving keys; lo is stored complemented so both are maxima).
-// Block x == 0 also allocates and zeroes the cluster's level-1 bitmap.
-__global__ __launch_bounds__(MD_BLOCK) void medoid_range_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
-                                                                MedoidMeta* meta, char* arena,
-                                                                unsigned long long* bump, int64_t arena_bytes) {
-  __shared__ int64_t base_sh;
-  const int tid = threadIdx.x;
-  const int32_t nd = *n_deferred;
-  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
-    MedoidMeta* M = meta + di;
-    const int64_t s0 = M->s0;
-    const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s0 + M->n];
-    if (blockIdx.x == 0) {
-      if (tid == 0) base_sh = md_bump(bump, md_l1_bytes(), arena_bytes);
-      __syncthreads();
-      const int64_t base = base_sh;
-      if (base >= 0) {
-        unsigned long long* l1 = reinterpret_cast<unsigned long long*>(arena + base);
-        for (int w = tid; w < MD_L1WORDS; w += MD_BLOCK) l1[w] = 0ull;
-      }
-      if (tid == 0) M->l1_off = base;
-      __syncthreads();
-    }
-    long long lo = 0x7fffffffffffffffll, hi = -0x7fffffffffffffffll - 1;
-    for (int64_t k = p0 + (int64_t)blockIdx.x * MD_BLOCK + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
-      const long long b = md_bin(v.mz[k], P);
-      lo = b < lo ? b : lo;
-      hi = b > hi ? b : hi;
-    }
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      const long long l2 = __shfl_xor(lo, o, kWave), h2 = __shfl_xor(hi, o, kWave);
-      lo = l2 < lo ? l2 : lo;
-      hi = h2 > hi ? h2 : hi;
-    }
-    if (lane_id() == 0 && lo <= hi) {
-      atomicMax(&M->hi_key, md_key(hi));
-      atomicMax(&M->lo_key, ~md_key(lo));
-    }
-  }
-}
-
-__device__ __forceinline__ bool md_range(const MedoidMeta& M, int64_t& blo, int& nw1) {
-  if (M.hi_key == 0ull) { blo = 0; nw1 = 0; return true; }  // no peaks at all
-  blo = md_unkey(~M.lo_key);
-  const int64_t bhi = md_unkey(M.hi_key);
-  const int64_t nblk = ((bhi - blo) >> 6) + 1;
-  const int64_t w = (nblk + 63) / 64;
-  nw1 = w > MD_L1WORDS ? -1 : (int)w;
-  return w <= MD_L1WORDS;
-}
-
-// Pass 2: level-1 occupancy, staged in LDS, merged with one atomicOr per word.
-__global__ __launch_bounds__(MD_BLOCK) void medoid_l1_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
-                                                             const MedoidMeta* meta, char* arena) {
-  __shared__ unsigned long long l1s[MD_L1WORDS];
-  const int tid = threadIdx.x;
-  const int32_t nd = *n_deferred;
-  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
-    const MedoidMeta M = meta[di];
-    int64_t blo;
-    int nw1;
-    if (M.l1_off < 0 || !md_range(M, blo, nw1) || nw1 == 0) continue;
-    const int64_t p0 = v.spec_off[M.s0], p1 = v.spec_off[M.s0 + M.n];
-    const int64_t k0 = p0 + (int64_t)blockIdx.x * MD_BLOCK;
-    if (k0 >= p1) continue;  // uniform per block: no barrier divergence
-    for (int w = tid; w < nw1; w += MD_BLOCK) l1s[w] = 0ull;
-    __syncthreads();
-    for (int64_t k = k0 + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
-      const int64_t blk = (md_bin(v.mz[k], P) - blo) >> 6;
-      atomicOr(&l1s[blk >> 6], 1ull << (blk & 63));
-    }
-    __syncthreads();
-    unsigned long long* l1 = reinterpret_cast<unsigned long long*>(arena + M.l1_off);
-    for (int w = tid; w < nw1; w += MD_BLOCK)
-      if (l1s[w]) atomicOr(&l1[w], l1s[w]);
-    __syncthreads();
-  }
-}
-
-// Plan 1 (one workgroup per cluster): level-1 prefix, allocate + zero level 2.
-__global__ __launch_bounds__(MD_BLOCK) void medoid_plan1_kernel(const int32_t* n_deferred, MedoidMeta* meta,
-                                                                char* arena, unsigned long long* bump,
-                                                                int64_t arena_bytes, int64_t* rep) {
-  __shared__ unsigned long long l1s[MD_L1WORDS];
-  __shared__ uint32_t pre[MD_L1WORDS];
-  __shared__ int tmp[MD_BLOCK / kWave + 1];
-  __shared__ int64_t base_sh;
-  const int tid = threadIdx.x;
-  const int32_t nd = *n_deferred;
-  for (int32_t di = blockIdx.x; di < nd; di += gridDim.x) {
-    MedoidMeta* M = meta + di;
-    int64_t blo;
-    int nw1;
-    const bool fits = md_range(*M, blo, nw1);
-    if (M->l1_off < 0 || !fits) {  // > 4.2M bins (-2) or arena exhausted (-3): reported, not approximated
-      if (tid == 0) rep[M->c] = fits ? -3 : -2;
-      continue;
-    }
-    const unsigned long long* l1 = reinterpret_cast<const unsigned long long*>(arena + M->l1_off);
-    for (int w = tid; w < nw1; w += MD_BLOCK) l1s[w] = l1[w];
-    __syncthreads();
-    const int B1 = bitmap_prefix<MD_BLOCK>(l1s, pre, nw1, tmp);
-    uint32_t* l1pre = reinterpret_cast<uint32_t*>(arena + M->l1_off + (int64_t)MD_L1WORDS * 8);
-    for (int w = tid; w < nw1; w += MD_BLOCK) l1pre[w] = pre[w];
-    if (tid == 0) base_sh = md_bump(bump, md_align((int64_t)B1 * 12 + 8), arena_bytes);
-    __syncthreads();
-    const int64_t base = base_sh;
-    if (base < 0) {
-      if (tid == 0) { rep[M->c] = -3; M->l1_off = -1; }
-      __syncthreads();
-      continue;
-    }
-    unsigned long long* l2 = reinterpret_cast<unsigned long long*>(arena + base);
-    for (int w = tid; w < B1; w += MD_BLOCK) l2[w] = 0ull;
-    if (tid == 0) { M->blo = blo; M->nw1 = nw1; M->B1 = B1; M->l2_off = base; }
-    __syncthreads();
-  }
-}
-
-// Pass 3: level-2 occupancy (LDS-staged when the cluster's level-2 fits).
-__global__ __launch_bounds__(MD_BLOCK) void medoid_l2_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
-                                                             const MedoidMeta* meta, char* arena) {
-  __shared__ unsigned long long l2s[MD_L2LDS];
-  const int tid = threadIdx.x;
-  const int32_t nd = *n_deferred;
-  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
-    const MedoidMeta M = meta[di];
-    if (M.l1_off < 0 || M.l2_off == 0 || M.B1 == 0) continue;
-    const int64_t p0 = v.spec_off[M.s0], p1 = v.spec_off[M.s0 + M.n];
-    const int64_t k0 = p0 + (int64_t)blockIdx.x * MD_BLOCK;
-    if (k0 >= p1) continue;
-    const MedoidTables T = md_tables(arena, M);
-    unsigned long long* l2 = reinterpret_cast<unsigned long long*>(arena + M.l2_off);
-    const bool staged = M.B1 <= MD_L2LDS;
-    if (staged) {
-      for (int w = tid; w < M.B1; w += MD_BLOCK) l2s[w] = 0ull;
-      __syncthreads();
-    }
-    for (int64_t k = k0 + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
-      const int64_t rel = md_bin(v.mz[k], P) - M.blo;
-      const int bs = bitmap_rank(T.l1, T.l1pre, rel >> 6);
-      if (staged) atomicOr(&l2s[bs], 1ull << (rel & 63));
-      else atomicOr(&l2[bs], 1ull << (rel & 63));
-    }
-    if (staged) {
-      __syncthreads();
-      for (int w = tid; w < M.B1; w += MD_BLOCK)
-        if (l2s[w]) atomicOr(&l2[w], l2s[w]);
-      __syncthreads();
-    }
-  }
-}
-
-// Plan 2 (one workgroup per cluster): level-2 prefix -> K columns; allocate
-// rows (bit-packed, KW multiple of 8 words, rows padded to Gram tiles), the
-// count matrix, numpy's leaf segmentation of [0, n) and the leaf sums.
-__global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n_deferred, MedoidMeta* meta,
-                                                                char* arena, unsigned long long* bump,
-                                                                int64_t arena_bytes, int64_t* rep) {
-  __shared__ int tmp[MD_BLOCK / kWave + 1];
-  __shared__ int64_t base_sh;
-  const int tid = threadIdx.x;
-  const int32_t nd = *n_deferred;
-  for (int32_t di = blockIdx.x; di < nd; di += gridDim.x) {
-    MedoidMeta* M = meta + di;
-    if (M->l1_off < 0) continue;
-    int K = 0;
-    if (M->B1 > 0) {
-      unsigned long long* l2 = reinterpret_cast<unsigned long long*>(arena + M->l2_off);
-      uint32_t* l2pre = reinterpret_cast<uint32_t*>(arena + M->l2_off + (int64_t)M->B1 * 8);
-      K = bitmap_prefix<MD_BLOCK>(l2, l2pre, M->B1, tmp);
-    }
-    const int n = M->n;
-    const int KW = ((K + 63) / 64 + 7) / 8 * 8 > 0 ? ((K + 63) / 64 + 7) / 8 * 8 : 8;
-    const int T = (n + MD_GT - 1) / MD_GT;
-    const int64_t maxL = md_max_leaves(n);
-    const int64_t rows_b = md_align((int64_t)T * MD_GT * KW * 8);
-    const int64_t cmat_b = md_align((int64_t)n * n * 4);
-    const int64_t leaf_b = md_align((5 * maxL + 1) * 4);        // starts, leaf nodes, program
-    const int64_t lsum_b = md_align(2 * (2 * maxL) * (int64_t)n * 8);  // node values, row and column
-    const int64_t tot_b = md_align((int64_t)n * 8);
-    const int64_t rowsT_b = rows_b;  // the word-major copy the Gram kernel reads
-    if (tid == 0) base_sh = md_bump(bump, rows_b + rowsT_b + cmat_b + leaf_b + lsum_b + tot_b, arena_bytes);
-    __syncthreads();
-    const int64_t base = base_sh;
-    if (base < 0) {
-      if (tid == 0) rep[M->c] = -3;
-      __syncthreads();
-      continue;
-    }
-    if (tid == 0) {
-      // numpy's recursion over [0, n) as a post-order program: every node gets
-      // a value slot when it completes; leaves in order, internal nodes as
-      // (left slot, right slot, out slot) with children before parents.
-      int32_t* start = reinterpret_cast<int32_t*>(arena + base + rows_b + rowsT_b + cmat_b);  // [maxL + 1]
-      int32_t* lnode = start + (maxL + 1);                                           // [maxL]
-      int32_t* prog = lnode + maxL;                                                  // [3 * maxL]
-      int nl = 0, nq = 0, nid = 0, ret = 0;
-      int64_t lo[40], len[40];
-      int st[40], lft[40];
-      int sp = 0;
-      lo[0] = 0; len[0] = n; st[0] = 0;
-      for (;;) {
-        if (st[sp] == 0 && len[sp] <= 128) {  // leaf
-          start[nl] = (int32_t)lo[sp];
-          lnode[nl++] = nid;
-          ret = nid++;
-        } else if (st[sp] == 0) {  // descend left
-          int64_t h = len[sp] / 2;
-          h -= h % 8;
-          st[sp] = 1;
-          lo[sp + 1] = lo[sp]; len[sp + 1] = h; st[sp + 1] = 0;
-          ++sp;
-          continue;
-        } else if (st[sp] == 1) {  // left done: descend right
-          int64_t h = len[sp] / 2;
-          h -= h % 8;
-          lft[sp] = ret;
-          st[sp] = 2;
-          lo[sp + 1] = lo[sp] + h; len[sp + 1] = len[sp] - h; st[sp + 1] = 0;
-          ++sp;
-          continue;
-        } else {  // both done: internal node
-          prog[3 * nq] = lft[sp]; prog[3 * nq + 1] = ret; prog[3 * nq + 2] = nid;
-          ++nq;
-          ret = nid++;
-        }
-        if (sp == 0) break;
-        --sp;
-      }
-      start[nl] = n;
-      M->KW = KW;
-      M->L = nl;
-      M->rows_off = base;
-      M->rowsT_off = base + rows_b;
-      M->cmat_off = base + rows_b + rowsT_b;
-      M->leaf_off = M->cmat_off + cmat_b;
-      M->lsum_off = M->leaf_off + leaf_b;
-      M->tot_off = M->lsum_off + lsum_b;
-      M->tiles = md_gr_tiles(n);
-      M->units = ((n + MD_BLOCK - 1) / MD_BLOCK) * nl;
-      M->ok = 1;
-    }
-    __syncthreads();
-  }
-}
-
-// Exclusive scans of Gram tiles and leaf units over the deferred clusters (one workgroup).
-__device__ __forceinline__ int64_t md_xpose_tiles(const MedoidMeta& M) {  // 64 x 64-word transpose tiles
-  return (int64_t)((M.n + MD_GT - 1) / MD_GT * MD_GT / 64) * ((M.KW + 63) / 64);
-}
-
-__global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
-                                                               int64_t* tile_base, int64_t* unit_base,
-                                                               int64_t* chunk_base, int64_t* xpose_base) {
-  __shared__ int64_t tmp[MD_BLOCK / kWave + 1];
-  const int32_t nd = *n_deferred;
-  int64_t ct = 0, cu = 0, cc = 0, cx = 0;
-  for (int32_t i0 = 0; i0 < nd; i0 += MD_BLOCK) {
-    const int32_t i = i0 + threadIdx.x;
-    const bool ok = i < nd && meta[i].ok;
-    int64_t tot;
-    const int64_t et = block_exclusive_scan<MD_BLOCK>(ok ? (int64_t)meta[i].tiles : 0, tmp, tot);
-    if (i < nd) tile_base[i] = ct + et;
-    ct += tot;
-    const int64_t eu = block_exclusive_scan<MD_BLOCK>(ok ? (int64_t)meta[i].units : 0, tmp, tot);
-    if (i < nd) unit_base[i] = cu + eu;
-    cu += tot;
-    const int64_t ec =
-        block_exclusive_scan<MD_BLOCK>(ok ? (int64_t)((meta[i].n + MD_BLOCK - 1) / MD_BLOCK) : 0, tmp, tot);
-    if (i < nd) chunk_base[i] = cc + ec;
-    cc += tot;
-    const int64_t ex = block_exclusive_scan<MD_BLOCK>(ok ? md_xpose_tiles(meta[i]) : int64_t(0), tmp, tot);
-    if (i < nd) xpose_base[i] = cx + ex;
-    cx += tot;
-  }
-  if (threadIdx.x == 0) { tile_base[nd] = ct; unit_base[nd] = cu; chunk_base[nd] = cc; xpose_base[nd] = cx; }
-}
-
-// which deferred cluster owns work item t (base[lo] <= t < base[lo + 1], skipping empties)
-__device__ __forceinline__ int md_owner(const int64_t* base, int nd, int64_t t) {
-  int lo = 0, hi = nd;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (base[mid] <= t) lo = mid; else hi = mid;
-  }
-  while (lo + 1 < nd && base[lo + 1] <= t) ++lo;
-  return lo;
-}
-
-// Bit rows, one wave per (padded) row: zero the row's words, drain the stores,
-// then OR in one bit per peak (peaks may be unsorted; duplicates are idempotent).
-__global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, MedoidParams P, const MedoidMeta* meta,
-                                                               const int32_t* n_deferred, char* arena) {
-  const int32_t nd = *n_deferred;
-  constexpr int W = MD_BLOCK / kWave;
-  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
-    const MedoidMeta M = meta[di];
-    if (!M.ok) continue;
-    const MedoidTables Tb = md_tables(arena, M);
-    unsigned long long* rows = reinterpret_cast<unsigned long long*>(arena + M.rows_off);
-    const int npad = (M.n + MD_GT - 1) / MD_GT * MD_GT;
-    for (int r = blockIdx.x * W + wave_id(); r < npad; r += gridDim.x * W) {
-      unsigned long long* row = rows + (int64_t)r * M.KW;
-      for (int w = lane_id(); w < M.KW; w += kWave) row[w] = 0ull;
-      if (r >= M.n) continue;
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): zeros land before the ORs
-      const int64_t a = v.spec_off[M.s0 + r], e = v.spec_off[M.s0 + r + 1];
-      for (int64_t k = a + lane_id(); k < e; k += kWave) {
-        const int col = Tb.column(md_bin(v.mz[k], P) - M.blo);
-        atomicOr(&row[col >> 6], 1ull << (col & 63));
-      }
-    }
-  }
-}
-
-typedef int md_i32x4 __attribute__((ext_vector_type(4)));
-typedef int md_i32x16 __attribute__((ext_vector_type(16)));
-
-// 64 bins (one u64 row word) -> 64 bytes of 0/1 in 4 x 16 B.  Byte p of dword
-// g (g < 8: low word) holds bin g + 8p -- a fixed permutation of the k axis,
-// identical for the A and B operands, so the dot products are unchanged.
-constexpr int MD_GR_PF = 4;  // words in flight per lane
-
-// Bit rows, row-major [npad][KW] -> word-major [KW][npad] (64 x 64-word tiles
-// through LDS: both sides coalesced), for the register Gram's loads.
-__global__ __launch_bounds__(MD_BLOCK) void medoid_transpose_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
-                                                                    const int64_t* xpose_base, char* arena) {
-  __shared__ unsigned long long tile[64][65];
-  const int tid = threadIdx.x, x = tid & 63, y0 = tid >> 6;
-  const int32_t nd = *n_deferred;
-  const int64_t total = xpose_base[nd];
-  for (int64_t g = blockIdx.x; g < total; g += gridDim.x) {  // every tile of every cluster, flat
-    const int o = md_owner(xpose_base, nd, g);
-    const MedoidMeta M = meta[o];
-    const int npad = (M.n + MD_GT - 1) / MD_GT * MD_GT, KW = M.KW;
-    const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(arena + M.rows_off);
-    unsigned long long* rowsT = reinterpret_cast<unsigned long long*>(arena + M.rowsT_off);
-    const int tw = (KW + 63) / 64;
-    {
-      const int t = (int)(g - xpose_base[o]);
-      const int r0 = (t / tw) * 64, w0 = (t % tw) * 64;
-      for (int y = y0; y < 64; y += MD_BLOCK / 64)
-        tile[y][x] = w0 + x < KW ? rows[(int64_t)(r0 + y) * KW + w0 + x] : 0ull;
-      __syncthreads();
-      for (int y = y0; y < 64; y += MD_BLOCK / 64)
-        if (w0 + y < KW) rowsT[(int64_t)(w0 + y) * npad + r0 + x] = tile[x][y];
-      __syncthreads();
-    }
-  }
-}
-__global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
-                                                                   const int64_t* tile_base, char* arena) {
-  const int lane = lane_id();
-  const int fr = lane & 31, fh = lane >> 5;
-  const int32_t nd = *n_deferred;
-  const int64_t total = tile_base[nd];
-  const int64_t wstride = (int64_t)gridDim.x * (MD_BLOCK / kWave);
-  for (int64_t t = (int64_t)blockIdx.x * (MD_BLOCK / kWave) + wave_id(); t < total; t += wstride) {
-    const int o = md_owner(tile_base, nd, t);
-    const MedoidMeta M = meta[o];
-    int64_t r = t - tile_base[o];
-    const int TN = (M.n + MD_WTN - 1) / MD_WTN;
-    int ti = 0;
-    while (r >= TN - md_gr_first_tj(ti)) { r -= TN - md_gr_first_tj(ti); ++ti; }
-    const int tj = md_gr_first_tj(ti) + (int)r;
-    const int KW = M.KW;
-    const int64_t npad = (int64_t)((M.n + MD_GT - 1) / MD_GT) * MD_GT;
-    const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(arena + M.rowsT_off);
-    // rows this lane loads: A blocks 0/1 (64-row tile), B blocks 0..NB-1 (zero past npad)
-    const unsigned long long* pa = rows + ti * MD_WT + fr;
-    const unsigned long long* pb = rows + (int64_t)tj * MD_WTN + fr;
-    bool bok[MD_GR_NB];
-#pragma unroll
-    for (int b = 0; b < MD_GR_NB; ++b) bok[b] = (int64_t)tj * MD_WTN + b * 32 < npad;
-
-    md_i32x16 acc[2][MD_GR_NB];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < MD_GR_NB; ++b)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[a][b][q] = 0;
-
-    constexpr int NR = 2 + MD_GR_NB;  // rows per lane
-    unsigned long long ring[MD_GR_PF][NR];
-    auto load = [&](int w, unsigned long long* dst) __attribute__((always_inline)) {
-      const int64_t wo = (int64_t)(w < KW ? w : 0) * npad;  // unconditional (clamped)
-      dst[0] = pa[wo];
-      dst[1] = pa[wo + 32];
-#pragma unroll
-      for (int b = 0; b < MD_GR_NB; ++b) dst[2 + b] = pb[wo + (bok[b] ? b * 32 : 0)];
-    };
-#pragma unroll
-    for (int q = 0; q < MD_GR_PF; ++q) load(q, ring[q]);
-    // one fragment: 16 bytes of the 32-bin half c, dwords 4h..4h+3
-    auto frag = [&](uint32_t c) __attribute__((always_inline)) {
-      md_i32x4 f;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) f[g] = (int)((c >> (4 * fh + g)) & 0x01010101u);
-      return f;
-    };
-    for (int w0 = 0; w0 < KW; w0 += MD_GR_PF) {  // KW is a multiple of 8
-#pragma unroll
-      for (int q = 0; q < MD_GR_PF; ++q) {
-        unsigned long long cur[NR];
-#pragma unroll
-        for (int k = 0; k < NR; ++k) cur[k] = ring[q][k];
-        load(w0 + q + MD_GR_PF, ring[q]);
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          md_i32x4 fa[2], fb[MD_GR_NB];
-#pragma unroll
-          for (int a = 0; a < 2; ++a) fa[a] = frag((uint32_t)(cur[a] >> (32 * hf)));
-#pragma unroll
-          for (int b = 0; b < MD_GR_NB; ++b) fb[b] = frag((uint32_t)(cur[2 + b] >> (32 * hf)));
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < MD_GR_NB; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
-        }
-      }
-    }
-    // C/D layout (32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
-    uint32_t* cmat = reinterpret_cast<uint32_t*>(arena + M.cmat_off);
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < MD_GR_NB; ++b)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int i = ti * MD_WT + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
-          const int j = tj * MD_WTN + b * 32 + fr;
-          if (i < M.n && j < M.n && i <= j) {
-            const uint32_t cnt = (uint32_t)acc[a][b][q];
-            cmat[(int64_t)i * M.n + j] = cnt;
-            cmat[(int64_t)j * M.n + i] = cnt;
-          }
-        }
-  }
-}
-
-// The Gram with the 0/1 byte expansion shared through LDS.  In the register Gram
-// every wave expands its own four rows' bits per 64-bin word (64 VALU per 8 MFMAs:
-// its MFMA pipe waits on VALU issue).  Here one workgroup owns a 128 x 128 block
-// (4 waves, 2 x 2 tiles of 64 x 64): per word, thread t expands ONE row's 64 bits
-// (A rows 0..127, B rows 128..255 of the block; 32 VALU) into LDS in the exact
-// per-lane fragment order, and each wave reads its fragments with 8 ds_read_b128
-// beside its 8 MFMAs.  Row records are 48 B (32 + 16 pad): 16 lanes reading 16
-// consecutive rows then hit 16 distinct 16-B bank slots.  Two stages, one barrier
-// per word.  Same fragment permutation of k as the register Gram (bin g + 8p in
-// byte p of dword g), same int32 accumulators: the same exact counts.
 template <class F>
 __device__ __forceinline__ void dual_leaf_at(const F& f, int lo, int m, int i, double& row, double& col) {
   if (m < 8) {

@@ -725,7 +725,7 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
   ProfScope prof_gram(2, s);
   hipLaunchKernelGGL(spx::medoid_gram_reg_kernel, dim3(2048), blk, 0, s, meta, n_def, tile_base, arena);
   prof_gram.end();
-  if (int rc = check_launch("medoid_gram kernel")) return rc;
+  if (int rc = check_launch("medoid_gram_reg_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_leaves_kernel, dim3(4096), blk, 0, s, V, meta, n_def, unit_base, arena);
   if (int rc = check_launch("medoid_leaves_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_combine_kernel, dim3(1024), blk, 0, s, meta, n_def, chunk_base, arena, totals);
