@@ -31,6 +31,15 @@
 // CLI's --pepmass / --rt choices (:106-148, :190-195).
 #include "spx_device.hpp"
 
+// The stamps build leaves the gap-average kernels unstamped unless asked
+// (-DSPX_STAMPS_GA): with stamps, the LDS kernel trips an "illegal VGPR to SGPR
+// copy" in this compiler (ROCm 7.2)
+#if defined(SPX_STAMPS) && !defined(SPX_STAMPS_GA)
+#define SPX_GA_STAMP(k) do { } while (0)
+#else
+#define SPX_GA_STAMP(k) SPX_STAMP(k)
+#endif
+
 namespace spx {
 
 struct GapParams {
@@ -662,7 +671,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     prank[wid * kWave + lane] = k.m;
     prank[(GA_NW + wid) * kWave + lane] = k.r;
   }
-  SPX_STAMP(1);
+  SPX_GA_STAMP(1);
   // f(m, it, tag) over every peak; kInten false passes it = 0 and loads none
   auto peaks_g = [&](auto inten_c, auto tagout_c, auto f) __attribute__((always_inline)) {
     constexpr bool kInten = decltype(inten_c)::value;
@@ -711,7 +720,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     imax = fmax(imax, fabs(it));
   });
   if (any(bad, 0)) return kNonFinite;
-  SPX_STAMP(2);
+  SPX_GA_STAMP(2);
 
   if (n == 1) {
     // passthrough + dynamic-range filter on the raw spectrum (:88-98)
@@ -777,7 +786,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   if constexpr (kL) D = bitmap_prefix_fixed<GA_BLOCK, GA_WMAX / GA_BLOCK>(S.bitmap, S.wprefix, tmp);
   else D = bitmap_prefix<GA_BLOCK, PrefixT, kL>(S.bitmap, S.wprefix, (int)nw, tmp);
   if (D > S.dcap) return kDeferred;
-  SPX_STAMP(3);
+  SPX_GA_STAMP(3);
   for (int d = tid; d < D; d += GA_BLOCK) {
     S.cnt[d] = 0u;
     S.gcnt[d] = 0u;
@@ -799,10 +808,10 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   });
   bar();
 
-  SPX_STAMP(4);
+  SPX_GA_STAMP(4);
   int E;
   if (const int32_t st = gap_groups<kL>(S, P, D, tmp, votes, E); st != kOk) return st;
-  SPX_STAMP(5);
+  SPX_GA_STAMP(5);
   // 5: fixed-point group sums (exact integer adds: order-independent)
   int ex_m, ex_i;
   frexp(fmax(fabs(lo), fabs(hi)) * (double)N, &ex_m);
@@ -818,7 +827,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   });
   bar();
 
-  SPX_STAMP(6);
+  SPX_GA_STAMP(6);
   return gap_emit<kL>(S, P, c, n, N, p0, E, sc_m, sc_i, out, tmp, red, votes);
 }
 
@@ -865,7 +874,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
                                                                    StripedList deferred) {
   __shared__ GapSmem L;
   const int64_t c = blockIdx.x;
-  SPX_STAMP(0);
+  SPX_GA_STAMP(0);
   GapState<uint16_t> S{L.bitmap, L.wprefix, L.cnt, L.gcnt, L.kmin, L.kmax, GA_WMAX, GA_DCAP};
   const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
   PrecLanes pl{0, 0.0, 0.0};
@@ -882,7 +891,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   }
   gap_finish<uint16_t>(v, P, c, st, out, prec_out, charge_out, rt_out, status, &pl, L.prank,
                        reinterpret_cast<double*>(L.prank), L.sel);
-  SPX_STAMP(7);
+  SPX_GA_STAMP(7);
 }
 
 // The LDS kernel's leftovers (striped list), grid-stride, one 147 KB workgroup per

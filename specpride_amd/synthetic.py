@@ -142,7 +142,10 @@ def make_clusters_torch(n_clusters: int, seed: int = 0, *, device="cuda", min_si
         block = torch.cat([jit, noise], dim=1)
         block = torch.where((block < MZ_LO) | (block >= MZ_HI), torch.full_like(block, float("inf")), block)
         block = torch.sort(block, dim=1).values
-        block = torch.round(block * 1e5) / 1e5
+        # the double nearest each 5-decimal value, as an MGF parse gives it: a true
+        # division (dividing by a Python scalar may multiply by its reciprocal on
+        # the device, which is 1 ulp off for some values)
+        block = torch.round(block * 1e5) / torch.full_like(block, 1e5)
         valid = torch.isfinite(block)
         lens_parts.append(valid.sum(dim=1))
         mz_parts.append(block[valid])
