@@ -62,6 +62,9 @@ constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10
 #ifndef SPX_GA_WUM
 #define SPX_GA_WUM 20
 #endif
+#ifndef SPX_GA_EARLY
+#define SPX_GA_EARLY 1  // wide kernel: intensities streamed during the bucket pass, bitmap zeroed under the m/z loads
+#endif
 // the wide kernel's (40 spilled 135 VGPRs even at its 256-VGPR budget)
 constexpr int GA_WUM = SPX_GA_WUM;
 constexpr int GA_WMAX = 3584;  // 229,376 buckets (2,293 Da at 0.01)
@@ -710,16 +713,43 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   auto peaks_m_tag = [&](auto f) __attribute__((always_inline)) { peaks_g(std::false_type{}, std::true_type{}, f); };
   const bool tagged = inreg;  // passes 3 and 5 take the bucket / slot from registers (uniform)
 
-  // 1: extrema and finiteness
   double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
   int bad = 0;
-  peaks([&](double m, double it, int32_t& tag) {
-    bad |= !isfinite(m) || !isfinite(it);
-    lo = fmin(lo, m);
-    hi = fmax(hi, m);
-    imax = fmax(imax, fabs(it));
-  });
-  if (any(bad, 0)) return kNonFinite;
+#if SPX_GA_EARLY
+  // The wide kernel (LDS state, m/z in registers, one workgroup per CU: its
+  // latencies are not covered by a second workgroup): the intensities are needed
+  // only for max |intensity| (pass 5's fixed-point scale) and their finiteness,
+  // so they are streamed DURING the bucket pass instead of in a pass of their
+  // own, and the bitmap is zeroed while the m/z loads land.  (In the LDS kernel,
+  // two per CU, the same order measured 16.68 -> 17.18 ms: its pass-1 loads had
+  // overlapped the m/z loads; profiles/r04_ab_gap_early.txt.)
+  const bool early = kL && !kDeferBig && inreg && n > 1 && N >= 2;  // uniform
+#else
+  const bool early = false;
+#endif
+  if (early) {
+#pragma unroll
+    for (int k = 0; k < GA_WMAX / GA_BLOCK; ++k) S.bitmap[k * GA_BLOCK + tid] = 0ull;
+    // 1a: m/z extrema and finiteness from registers
+#pragma unroll
+    for (int u = 0; u < UM; ++u) {
+      if (p0 + (int64_t)u * GA_BLOCK + tid < p1) {
+        bad |= !isfinite(rm[u]);
+        lo = fmin(lo, rm[u]);
+        hi = fmax(hi, rm[u]);
+      }
+    }
+    if (any(bad, 0)) return kNonFinite;
+  } else {
+    // 1: extrema and finiteness
+    peaks([&](double m, double it, int32_t& tag) {
+      bad |= !isfinite(m) || !isfinite(it);
+      lo = fmin(lo, m);
+      hi = fmax(hi, m);
+      imax = fmax(imax, fabs(it));
+    });
+    if (any(bad, 0)) return kNonFinite;
+  }
   SPX_GA_STAMP(2);
 
   if (n == 1) {
@@ -767,21 +797,64 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   if (nw > S.wcap) return kDeferred;
 
   // 2: occupied buckets
-  if constexpr (kL) {  // the whole LDS bitmap (the fixed-size prefix reads all of it)
+  if (early) {
+    // 1b + 2: the buckets of the register m/z, one batch of intensity loads in
+    // flight behind each batch of bucket work; the block's max |intensity| and
+    // the intensities' finiteness ride the barrier before the prefix
+    imax = 0.0;
 #pragma unroll
-    for (int k = 0; k < GA_WMAX / GA_BLOCK; ++k) S.bitmap[k * GA_BLOCK + tid] = 0ull;
+    for (int u0 = 0; u0 < UM; u0 += 8) {
+      double itb[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int64_t k = p0 + (int64_t)(u0 + q) * GA_BLOCK + tid;
+        itb[q] = (u0 + q < UM) ? v.inten[k < p1 ? k : p0] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int u = u0 + q;
+        if (u < UM && p0 + (int64_t)u * GA_BLOCK + tid < p1) {
+          const int64_t bk = floor_div_exact(rm[u], P.bucket_w, P.inv_bucket_w) - kb;
+          tags[u] = (uint32_t)bk;
+          atomicOr(&S.bitmap[bk >> 6], 1ull << (bk & 63));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int u = u0 + q;
+        if (u < UM && p0 + (int64_t)u * GA_BLOCK + tid < p1) {
+          bad |= !isfinite(itb[q]);
+          imax = fmax(imax, fabs(itb[q]));
+        }
+      }
+    }
+    imax = wave_max_dpp(imax);
+    const bool wbad = __ballot(bad) != 0ull;
+    if (lane == 0) { red[2 * GA_NW + wid] = imax; votes[GA_NW + wid] = wbad; }
+    bar();
+    int nf = 0;
+    for (int w = 0; w < GA_NW; ++w) {
+      imax = fmax(imax, red[2 * GA_NW + w]);
+      nf |= votes[GA_NW + w];
+    }
+    if (nf) return kNonFinite;
   } else {
-    for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
+    if constexpr (kL) {  // the whole LDS bitmap (the fixed-size prefix reads all of it)
+#pragma unroll
+      for (int k = 0; k < GA_WMAX / GA_BLOCK; ++k) S.bitmap[k * GA_BLOCK + tid] = 0ull;
+    } else {
+      for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
+    }
+    bar();
+    auto pass2 = [&](double m, double, int32_t& tag) __attribute__((always_inline)) {
+      const int64_t b = floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
+      tag = (int32_t)b;
+      SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
+      atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
+    };
+    peaks_m_tag(pass2);
+    bar();
   }
-  bar();
-  auto pass2 = [&](double m, double, int32_t& tag) __attribute__((always_inline)) {
-    const int64_t b = floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
-    tag = (int32_t)b;
-    SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
-    atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
-  };
-  peaks_m_tag(pass2);
-  bar();
   int D;
   if constexpr (kL) D = bitmap_prefix_fixed<GA_BLOCK, GA_WMAX / GA_BLOCK>(S.bitmap, S.wprefix, tmp);
   else D = bitmap_prefix<GA_BLOCK, PrefixT, kL>(S.bitmap, S.wprefix, (int)nw, tmp);
