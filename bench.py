@@ -42,6 +42,7 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 HBM_ACHIEVABLE_GBS = 6290.0  # measured float4 copy ceiling (MI355X_MICROARCH.md chip table)
 I8_DENSE_TOPS = 5000.0       # i8 MFMA dense peak, 2x BF16's ~2.5 PF (MI355X_MICROARCH.md MFMA table)
+FP4_DENSE_TOPS = 10000.0     # FP4 (e2m1) MFMA dense peak, 4x BF16 per clock (same table)
 
 
 def parse():
@@ -434,12 +435,17 @@ def config3(args, out):
     sizes = np.diff(batch.host_cluster_off)
     ops = gram_ops(t, batch)
     tops = ops / (gram_ms * 1e-3) / 1e12
+    bits = _lib.gram_operand_bits()
+    peak = FP4_DENSE_TOPS if bits == 4 else I8_DENSE_TOPS
     out["config3_medoid"] = {"clusters": batch.n_clusters, "spectra": batch.n_spectra, "max_n": int(sizes.max()),
                              "large_clusters": int((sizes > 64).sum()), "medoid_ms": round(ms, 3),
                              "clusters_per_s": round(batch.n_clusters / (ms * 1e-3), 1), "all_resolved": ok,
                              "roofline": {"bound": "mfma", "kernel": "medoid_gram_reg_kernel",
-                                          "achieved": round(tops, 1), "peak": I8_DENSE_TOPS, "unit": "TOP/s",
-                                          "frac": round(tops / I8_DENSE_TOPS, 4), "traffic": None,
+                                          "achieved": round(tops, 1), "peak": peak, "unit": "TOP/s",
+                                          "frac": round(tops / peak, 4), "traffic": None,
+                                          "operands": "fp4 e2m1 0/1 (v_mfma_f32_32x32x64_f8f6f4)" if bits == 4
+                                          else "i8 0/1 (v_mfma_i32_32x32x32_i8)",
+                                          "frac_of_i8_peak": round(tops / I8_DENSE_TOPS, 4),
                                           "launch_ms": round(gram_ms, 4), "algorithmic_ops": int(ops),
                                           "ops_definition": "sum over the large-path clusters of 2*n(n+1)/2*K_c, "
                                                             "K_c = distinct ceil(mz/0.1) bins of the cluster",

@@ -255,6 +255,11 @@ const char *spx_last_error(void); /* thread-local text of the last failure */
  * duration and the launch count of one kernel.  Off by default: nothing recorded. */
 int spx_profile_enable(int on);
 int spx_profile_read(const char *kernel, double *total_ms, int64_t *launches);
+/* The large-cluster medoid Gram's MFMA operand encoding of its 0/1 bin rows: 4 = FP4
+ * e2m1 (v_mfma_f32_32x32x64_f8f6f4, ~10 POPS dense), 8 = i8 (v_mfma_i32_32x32x32_i8,
+ * ~5 POPS dense); the counts are exact either way.  bench.py prices the Gram's MFMA
+ * roofline against the peak of the encoding the library was built with. */
+int spx_medoid_gram_operand_bits(void);
 
 #ifdef __cplusplus
 }

@@ -67,7 +67,8 @@ class SpxCosineParams(ctypes.Structure):
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_bin_mean_stage", "spx_gap_average_workspace_size", "spx_gap_average",
             "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_bin_mean_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
             "spx_compact_peaks", "spx_copy_h2d", "spx_copy_d2h",
-            "spx_abi_version", "spx_last_error", "spx_profile_enable", "spx_profile_read"]
+            "spx_abi_version", "spx_last_error", "spx_profile_enable", "spx_profile_read",
+            "spx_medoid_gram_operand_bits"]
 
 SPX_ABI_VERSION = 2
 _lib = None
@@ -146,7 +147,8 @@ def lib():
     L.spx_copy_d2h.argtypes = [_p, _p, _sz, _p]
     # symbols added in ABI 2's round 4 (bound when present: A/B runs load older builds)
     for name, argtypes in (("spx_bin_mean_medoid", [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _p, _p, _p, _p, _sz, _p]),
-                           ("spx_profile_enable", [_i32]), ("spx_profile_read", [ctypes.c_char_p, _p, _p])):
+                           ("spx_profile_enable", [_i32]), ("spx_profile_read", [ctypes.c_char_p, _p, _p]),
+                           ("spx_medoid_gram_operand_bits", [])):
         if hasattr(L, name):
             getattr(L, name).argtypes = argtypes
     if L.spx_abi_version() != SPX_ABI_VERSION:
@@ -165,6 +167,13 @@ def profile_read(kernel: str):
     ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
     check(lib().spx_profile_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)), "spx_profile_read")
     return ms.value, n.value
+
+
+def gram_operand_bits() -> int:
+    """4 (FP4 e2m1) or 8 (i8): the medoid Gram's MFMA operand encoding (8 for builds
+    that predate the query)."""
+    L = lib()
+    return int(L.spx_medoid_gram_operand_bits()) if hasattr(L, "spx_medoid_gram_operand_bits") else 8
 
 
 def check(rc: int, what: str) -> None:

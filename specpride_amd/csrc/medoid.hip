@@ -515,7 +515,10 @@ constexpr int MD_L1WORDS = 1024;  // level-1 bits: 65,536 blocks = 4.2M bins
 constexpr int MD_L2LDS = 4096;    // level-2 words staged in LDS (else global atomics)
 constexpr int MD_GT = 128;        // rows padded to a multiple
 constexpr int MD_WT = 64;         // register Gram: one wave's 64-row output tile
-constexpr int MD_GR_NB = 2;  // 32-column MFMA blocks per wave tile (64 x 128 measured: no faster)
+#ifndef SPX_GR_NB
+#define SPX_GR_NB 2
+#endif
+constexpr int MD_GR_NB = SPX_GR_NB;  // 32-column MFMA blocks per wave tile (64 x 128 measured: no faster)
 constexpr int MD_WTN = 32 * MD_GR_NB;  // wave tile columns
 
 // Wave tiles of a cluster: 64-row blocks ti against MD_WTN-column blocks tj that
@@ -858,16 +861,85 @@ __device__ __forceinline__ int md_owner(const int64_t* base, int nd, int64_t t) 
 
 // Bit rows, one wave per (padded) row: zero the row's words, drain the stores,
 // then OR in one bit per peak (peaks may be unsorted; duplicates are idempotent).
+#ifndef SPX_MD_FILL_LDS
+#define SPX_MD_FILL_LDS 1
+#endif
+constexpr int MD_FILL_KW = 512;  // row words a wave builds in LDS (4 KB; 32,768 columns)
+constexpr int MD_FILL_U = 4;     // 64-peak chunks of a spectrum whose loads go out together
+
 __global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, MedoidParams P, const MedoidMeta* meta,
                                                                const int32_t* n_deferred, char* arena) {
   const int32_t nd = *n_deferred;
   constexpr int W = MD_BLOCK / kWave;
+#if SPX_MD_FILL_LDS
+  // One wave per row.  A row of at most MD_FILL_KW words is built in the wave's
+  // LDS slice (no zeroing round trip through memory, no global atomics) and then
+  // written with plain coalesced stores; the peaks of up to MD_FILL_U chunks
+  // issue their m/z loads, then their level-1 and level-2 rank loads, together
+  // (three dependent round trips per 256 peaks instead of three per 64).
+  __shared__ unsigned long long lrow[W][MD_FILL_KW];
+  unsigned long long* L = lrow[wave_id()];
+#endif
   for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
     const MedoidMeta M = meta[di];
     if (!M.ok) continue;
     const MedoidTables Tb = md_tables(arena, M);
     unsigned long long* rows = reinterpret_cast<unsigned long long*>(arena + M.rows_off);
     const int npad = (M.n + MD_GT - 1) / MD_GT * MD_GT;
+#if SPX_MD_FILL_LDS
+    if (M.KW <= MD_FILL_KW) {  // uniform
+      for (int r = blockIdx.x * W + wave_id(); r < npad; r += gridDim.x * W) {
+        unsigned long long* row = rows + (int64_t)r * M.KW;
+        for (int w = lane_id(); w < M.KW; w += kWave) L[w] = 0ull;
+        if (r < M.n) {
+          const int64_t a = v.spec_off[M.s0 + r], e = v.spec_off[M.s0 + r + 1];
+          for (int64_t k0 = a; k0 < e; k0 += MD_FILL_U * kWave) {
+            double m[MD_FILL_U];
+#pragma unroll
+            for (int u = 0; u < MD_FILL_U; ++u) {
+              const int64_t k = k0 + u * kWave + lane_id();
+              m[u] = v.mz[k < e ? k : a];
+            }
+            int64_t rel[MD_FILL_U];
+            unsigned long long w1[MD_FILL_U];
+            uint32_t p1[MD_FILL_U];
+#pragma unroll
+            for (int u = 0; u < MD_FILL_U; ++u) {
+              rel[u] = md_bin(m[u], P) - M.blo;
+              const int64_t b1 = rel[u] >> 6;  // level-1 bit = the 64-bin block
+              w1[u] = Tb.l1[b1 >> 6];
+              p1[u] = Tb.l1pre[b1 >> 6];
+            }
+            unsigned long long w2[MD_FILL_U];
+            uint32_t p2[MD_FILL_U];
+#pragma unroll
+            for (int u = 0; u < MD_FILL_U; ++u) {
+              const int64_t b1 = rel[u] >> 6;
+              const int bs = (int)p1[u] + __popcll(w1[u] & ((1ull << (b1 & 63)) - 1ull));
+              w2[u] = Tb.l2[bs];
+              p2[u] = Tb.l2pre[bs];
+            }
+#pragma unroll
+            for (int u = 0; u < MD_FILL_U; ++u) {
+              const int64_t k = k0 + u * kWave + lane_id();
+              if (k < e) {
+                const int col = (int)p2[u] + __popcll(w2[u] & ((1ull << (rel[u] & 63)) - 1ull));
+                atomicOr(&L[col >> 6], 1ull << (col & 63));
+              }
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int w = lane_id(); w < M.KW; w += kWave) row[w] = L[w];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the next row's zeroing after these reads
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      continue;
+    }
+#endif
     for (int r = blockIdx.x * W + wave_id(); r < npad; r += gridDim.x * W) {
       unsigned long long* row = rows + (int64_t)r * M.KW;
       for (int w = lane_id(); w < M.KW; w += kWave) row[w] = 0ull;
@@ -888,7 +960,27 @@ typedef int md_i32x16 __attribute__((ext_vector_type(16)));
 // 64 bins (one u64 row word) -> 64 bytes of 0/1 in 4 x 16 B.  Byte p of dword
 // g (g < 8: low word) holds bin g + 8p -- a fixed permutation of the k axis,
 // identical for the A and B operands, so the dot products are unchanged.
-constexpr int MD_GR_PF = 4;  // words in flight per lane
+#ifndef SPX_GR_PF
+#define SPX_GR_PF 4
+#endif
+#ifndef SPX_GR_MINW
+#define SPX_GR_MINW 3  // 3 waves per SIMD (167 unified registers, the accumulators in VGPRs)
+#endif
+constexpr int MD_GR_PF = SPX_GR_PF;  // words in flight per lane (divides 8: KW is a multiple of 8)
+#ifndef SPX_GR_FP4
+#define SPX_GR_FP4 1
+#endif
+#ifndef SPX_GR_TR
+#define SPX_GR_TR 1  // the mirrored Gram entries written through a wave-private LDS transpose
+#endif
+// SPX_GR_FP4: the 0/1 operands as FP4 e2m1 (1.0 = nibble 0b0010) through
+// v_mfma_f32_32x32x64_f8f6f4 (the MX-scaled instruction at unit scale): one MFMA per
+// 64-bin word and (a, b) block instead of two, from half the expansion VALU (a
+// 32-bin half word -> 4 dwords of 8 nibbles, 2 ops each).  Products are 1.0 or 0,
+// the f32 accumulation of at most 2^24 of them is exact, so the counts are the
+// integer ones.  Peak: the FP4 dense rate (~10 POPS), twice the i8 one.
+typedef int md_i32x8 __attribute__((ext_vector_type(8)));
+typedef float md_f32x16 __attribute__((ext_vector_type(16)));
 
 // Bit rows, row-major [npad][KW] -> word-major [KW][npad] (64 x 64-word tiles
 // through LDS: both sides coalesced), for the register Gram's loads.
@@ -917,10 +1009,13 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_transpose_kernel(const Medoid
     }
   }
 }
-__global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
+__global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
                                                                    const int64_t* tile_base, char* arena) {
   const int lane = lane_id();
   const int fr = lane & 31, fh = lane >> 5;
+#if SPX_GR_TR
+  __shared__ uint32_t tr[MD_BLOCK / kWave][32][33];
+#endif
   const int32_t nd = *n_deferred;
   const int64_t total = tile_base[nd];
   const int64_t wstride = (int64_t)gridDim.x * (MD_BLOCK / kWave);
@@ -937,12 +1032,20 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidM
     const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(arena + M.rowsT_off);
     // rows this lane loads: A blocks 0/1 (64-row tile), B blocks 0..NB-1 (zero past npad)
     const unsigned long long* pa = rows + ti * MD_WT + fr;
+#ifdef SPX_GR_DIAG  // diagnostic only (results wrong): every wave reads the same B rows (L2-resident)
+    const unsigned long long* pb = rows + fr;
+#else
     const unsigned long long* pb = rows + (int64_t)tj * MD_WTN + fr;
+#endif
     bool bok[MD_GR_NB];
 #pragma unroll
     for (int b = 0; b < MD_GR_NB; ++b) bok[b] = (int64_t)tj * MD_WTN + b * 32 < npad;
 
+#if SPX_GR_FP4
+    md_f32x16 acc[2][MD_GR_NB];
+#else
     md_i32x16 acc[2][MD_GR_NB];
+#endif
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -961,6 +1064,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidM
     };
 #pragma unroll
     for (int q = 0; q < MD_GR_PF; ++q) load(q, ring[q]);
+#if !SPX_GR_FP4
     // one fragment: 16 bytes of the 32-bin half c, dwords 4h..4h+3
     auto frag = [&](uint32_t c) __attribute__((always_inline)) {
       md_i32x4 f;
@@ -968,6 +1072,21 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidM
       for (int g = 0; g < 4; ++g) f[g] = (int)((c >> (4 * fh + g)) & 0x01010101u);
       return f;
     };
+#endif
+#if SPX_GR_FP4
+    // lane half fh takes bins 32fh..32fh+31 of the word: dword g, nibble p = bin
+    // 32fh + g + 4p (the same k order for A and B)
+    auto frag4 = [&](uint64_t w) __attribute__((always_inline)) {
+      const uint32_t c = (uint32_t)(w >> (32 * fh));
+      md_i32x8 f;
+      f[0] = (int)((c << 1) & 0x22222222u);
+      f[1] = (int)(c & 0x22222222u);
+      f[2] = (int)((c >> 1) & 0x22222222u);
+      f[3] = (int)((c >> 2) & 0x22222222u);
+      f[4] = f[5] = f[6] = f[7] = 0;
+      return f;
+    };
+#endif
     for (int w0 = 0; w0 < KW; w0 += MD_GR_PF) {  // KW is a multiple of 8
 #pragma unroll
       for (int q = 0; q < MD_GR_PF; ++q) {
@@ -975,6 +1094,20 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidM
 #pragma unroll
         for (int k = 0; k < NR; ++k) cur[k] = ring[q][k];
         load(w0 + q + MD_GR_PF, ring[q]);
+#if SPX_GR_FP4
+        {
+          md_i32x8 fa[2], fb[MD_GR_NB];
+#pragma unroll
+          for (int a = 0; a < 2; ++a) fa[a] = frag4(cur[a]);
+#pragma unroll
+          for (int b = 0; b < MD_GR_NB; ++b) fb[b] = frag4(cur[2 + b]);
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < MD_GR_NB; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[a], fb[b], acc[a][b], 4, 4, 0, 0, 0, 0);
+        }
+#else
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
           md_i32x4 fa[2], fb[MD_GR_NB];
@@ -988,6 +1121,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidM
             for (int b = 0; b < MD_GR_NB; ++b)
               acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
         }
+#endif
       }
     }
     // C/D layout (32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
@@ -995,17 +1129,40 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_gram_reg_kernel(const MedoidM
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < MD_GR_NB; ++b)
+      for (int b = 0; b < MD_GR_NB; ++b) {
+        const int i0 = ti * MD_WT + a * 32, j0 = tj * MD_WTN + b * 32;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const int i = ti * MD_WT + a * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
-          const int j = tj * MD_WTN + b * 32 + fr;
+          const int i = i0 + (q & 3) + 8 * (q >> 2) + 4 * fh;
+          const int j = j0 + fr;
           if (i < M.n && j < M.n && i <= j) {
             const uint32_t cnt = (uint32_t)acc[a][b][q];
-            cmat[(int64_t)i * M.n + j] = cnt;
-            cmat[(int64_t)j * M.n + i] = cnt;
+            cmat[(int64_t)i * M.n + j] = cnt;  // row i: the lanes write consecutive j
+#if !SPX_GR_TR
+            cmat[(int64_t)j * M.n + i] = cnt;  // column: one line per lane
+#endif
           }
         }
+#if SPX_GR_TR
+        // the mirrored entries (j, i): through a wave-private 32 x 33 LDS tile so
+        // that the lanes write consecutive columns of each row j (the direct
+        // column store put every lane on its own cache line: 19% of the kernel)
+        uint32_t(*T)[33] = tr[wave_id()];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) T[fr][(q & 3) + 8 * (q >> 2) + 4 * fh] = (uint32_t)acc[a][b][q];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int jl = 2 * rr + fh, j = j0 + jl, i = i0 + fr;
+          if (i < M.n && j < M.n && i <= j) cmat[(int64_t)j * M.n + i] = T[jl][fr];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the next block's writes after these reads
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+      }
   }
 }
 

@@ -218,6 +218,8 @@ int spx_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
   return SPX_SUCCESS;
 }
 
+int spx_medoid_gram_operand_bits(void) { return SPX_GR_FP4 ? 4 : 8; }
+
 // ------------------------------------------------------------------ bin-mean
 // range records of the split path: every range holds >= SP_CAPW occupied bins
 // except each cluster's last, so C + P / SP_CAPW bounds them (capped; clusters past
