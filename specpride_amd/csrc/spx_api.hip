@@ -31,6 +31,11 @@
 #include "fused.hip"
 #include "transfer.hip"
 
+#ifndef SPX_GR_GRID
+#define SPX_GR_GRID 8192  // medoid_gram_reg_kernel workgroups (4 waves each, grid-stride over the flat tile list;
+                          // 2048: 3.20 ms configs[3] medoid, 8192: 3.05-3.11, 16384: 3.06-3.08)
+#endif
+
 namespace {
 
 thread_local char g_err[256] = "";
@@ -725,7 +730,7 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
   hipLaunchKernelGGL(spx::medoid_transpose_kernel, dim3(4096), blk, 0, s, meta, n_def, xpose_base, arena);
   if (int rc = check_launch("medoid_transpose_kernel")) return rc;
   ProfScope prof_gram(2, s);
-  hipLaunchKernelGGL(spx::medoid_gram_reg_kernel, dim3(2048), blk, 0, s, meta, n_def, tile_base, arena);
+  hipLaunchKernelGGL(spx::medoid_gram_reg_kernel, dim3(SPX_GR_GRID), blk, 0, s, meta, n_def, tile_base, arena);
   prof_gram.end();
   if (int rc = check_launch("medoid_gram_reg_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_leaves_kernel, dim3(4096), blk, 0, s, V, meta, n_def, unit_base, arena);
