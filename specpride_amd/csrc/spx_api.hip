@@ -31,6 +31,9 @@
 #include "fused.hip"
 #include "transfer.hip"
 
+#ifndef SPX_MD_GRIDY
+#define SPX_MD_GRIDY 32u  // deferred clusters the large path's grid-stride passes take at a time
+#endif
 #ifndef SPX_GR_GRID
 #define SPX_GR_GRID 8192  // medoid_gram_reg_kernel workgroups (4 waves each, grid-stride over the flat tile list;
                           // 2048: 3.20 ms configs[3] medoid, 8192: 3.05-3.11, 16384: 3.06-3.08)
@@ -691,7 +694,7 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024));
   // grid-stride passes: 32 deferred clusters at a time x 64 blocks fills the chip,
   // and an empty deferred list (the common case) costs a small launch
-  const dim3 grid2(spx::MD_GRIDX, std::min<unsigned>(g, 32u)), blk(spx::MD_BLOCK);
+  const dim3 grid2(spx::MD_GRIDX, std::min<unsigned>(g, SPX_MD_GRIDY)), blk(spx::MD_BLOCK);
 
   if (part != 2) {
     // n_def, bump and the striped list's counters: the first 512 B + kListCountBytes
