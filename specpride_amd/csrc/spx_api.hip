@@ -32,7 +32,7 @@
 #include "transfer.hip"
 
 #ifndef SPX_MD_GRIDY
-#define SPX_MD_GRIDY 32u  // deferred clusters the large path's grid-stride passes take at a time
+#define SPX_MD_GRIDY 128u  // deferred clusters the large path's grid-stride passes take at a time (32: configs[3] medoid 3.02 ms, 128: 2.92, 512: 2.92)
 #endif
 #ifndef SPX_GR_GRID
 #define SPX_GR_GRID 8192  // medoid_gram_reg_kernel workgroups (4 waves each, grid-stride over the flat tile list;
