@@ -1028,7 +1028,13 @@ __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
 constexpr int64_t GA_GIANT_N = 16384;
 constexpr int GA_GMAX = 256;                      // giant records per call
 constexpr int64_t GA_TILE = 2 * GA_BATCH * GA_BLOCK;  // peaks per tile
-constexpr int GA_GIANT_GRID = 1024;               // tile kernels' workgroups
+#ifndef SPX_GA_GBATCH
+#define SPX_GA_GBATCH 1  // giant passes 2-3: a batch's global reads before its atomics
+#endif
+#ifndef SPX_GA_GGRID
+#define SPX_GA_GGRID 512  // skewed configs[3] gap-average: 1024 4.21 ms, 512 3.77-3.79, 256 3.78-3.80, 4096 6.05
+#endif
+constexpr int GA_GIANT_GRID = SPX_GA_GGRID;       // tile kernels' workgroups
 constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS first (50 KB)
 // More groups than that (the skewed law's giants: 6.5k-59k, mostly noise groups of
 // one peak): an open-addressing LDS table of HCAP groups per tile (a tile of ~40
@@ -1521,6 +1527,48 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
         }
       }
       lds_barrier();  // red and votes are reused by the next tile
+    } else if (SPX_GA_GBATCH && (PASS == 2 || PASS == 3)) {
+      // passes 2-3 in batches of GA_BATCH peaks per thread: every global read a
+      // batch needs (bitmap words; ranks, then the slots' extrema) goes out before
+      // its first atomic -- an atomic in between would order each read behind it
+      for (int64_t k0 = t0 + tid; k0 < t1; k0 += GA_BATCH * GA_BLOCK) {
+        double m[GA_BATCH];
+#pragma unroll
+        for (int q = 0; q < GA_BATCH; ++q) {
+          const int64_t k = k0 + (int64_t)q * GA_BLOCK;
+          m[q] = A.v.mz[k < t1 ? k : t0];
+        }
+        int64_t b[GA_BATCH];
+#pragma unroll
+        for (int q = 0; q < GA_BATCH; ++q) b[q] = floor_div_exact(m[q], A.P.bucket_w, A.P.inv_bucket_w) - kb;
+        if constexpr (PASS == 2) {
+          unsigned long long w[GA_BATCH];
+#pragma unroll
+          for (int q = 0; q < GA_BATCH; ++q) w[q] = S.bitmap[b[q] >> 6];
+#pragma unroll
+          for (int q = 0; q < GA_BATCH; ++q) {
+            const unsigned long long bit = 1ull << (b[q] & 63);
+            if (k0 + (int64_t)q * GA_BLOCK < t1 && !(w[q] & bit)) atomicOr(&S.bitmap[b[q] >> 6], bit);
+          }
+        } else {
+          int slot[GA_BATCH];
+#pragma unroll
+          for (int q = 0; q < GA_BATCH; ++q) slot[q] = bitmap_rank(S.bitmap, S.wprefix, b[q]);
+          unsigned long long lo[GA_BATCH], hi[GA_BATCH];
+#pragma unroll
+          for (int q = 0; q < GA_BATCH; ++q) {
+            lo[q] = reinterpret_cast<const unsigned long long*>(S.kmin)[slot[q]];
+            hi[q] = reinterpret_cast<const unsigned long long*>(S.kmax)[slot[q]];
+          }
+#pragma unroll
+          for (int q = 0; q < GA_BATCH; ++q) {
+            if (k0 + (int64_t)q * GA_BLOCK >= t1) continue;
+            const unsigned long long key = f64_order_key(m[q]);
+            if (key < lo[q]) atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot[q]]), key);
+            if (key > hi[q]) atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot[q]]), key);
+          }
+        }
+      }
     } else {
       gap_peaks<PASS == 5>(A.v, t0, t1, [&](int64_t, double m, double it) {
         const int64_t b = floor_div_exact(m, A.P.bucket_w, A.P.inv_bucket_w) - kb;
