@@ -37,6 +37,9 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_MINW
 #define SPX_MD_MINW 7
 #endif
+#ifndef SPX_MD_RECIP
+#define SPX_MD_RECIP 1  // P4's quotients from per-spectrum reciprocals (exact, md_dist_r)
+#endif
 constexpr int MD_KWMAX = SPX_MD_KWMAX;  // row words (odd stride): <= 64 * MD_KWMAX occupied bins per small cluster
 
 
@@ -50,6 +53,18 @@ __device__ __forceinline__ double md_dist(uint32_t c, int64_t pi, int64_t pj) {
   return 1.0 - x;
 }
 
+// d(i,j) = 1 - c/q, q = min(p_i, p_j), with the quotient from q's reciprocal r = fl(1/q)
+// and one exact fma remainder step: equal to the IEEE quotient fl(c/q) for every
+// 0 <= c <= q <= 65,536 (all 2.1e9 pairs checked on the host), so the distances --
+// and with them the totals and representatives -- are md_dist's bit for bit.
+__device__ __forceinline__ double md_dist_r(uint32_t c, int pi, double ri, int pj, double rj) {
+  const int q = pi < pj ? pi : pj;
+  const double cd = (double)c, qd = (double)q;
+  const double r = pi < pj ? ri : rj;
+  const double y = cd * r;
+  const double x = __builtin_fma(__builtin_fma(-y, qd, cd), r, y);
+  return (pi == 0 || pj == 0) ? 1.0 : 1.0 - x;
+}
 // Both pairwise sums of thread i (row i: j >= i; column i: j <= i) in one pass
 // over j, for n <= 128 (numpy's leaf regime).  f(j) returns d(i, j) = d(j, i).
 template <class F>
@@ -371,6 +386,15 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       }
     }
   }
+#if SPX_MD_RECIP
+  // each spectrum's exact reciprocal for P4's quotients (totals is free until P5;
+  // spectra here hold at most PMAX <= 65,536 peaks, md_dist_r's checked range)
+  static_assert(PMAX <= 65536, "md_dist_r's exact range");
+  if (tid < n) {
+    const int p = L.soff[tid + 1] - L.soff[tid];
+    L.totals[tid] = p > 0 ? 1.0 / (double)p : 0.0;
+  }
+#endif
   __syncthreads();
   SPX_STAMP(4);
 
@@ -405,7 +429,12 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   for (int q = 0; q < PPT; ++q) {
     if (pij[q] >= 0) {
       const int i = pij[q] >> 8, j = pij[q] & 0xff;
+#if SPX_MD_RECIP
+      L.u.d[row_start(i) + j - i] =
+          md_dist_r(pc[q], L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
+#else
       L.u.d[row_start(i) + j - i] = md_dist(pc[q], L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
+#endif
     }
   }
   __syncthreads();
@@ -1209,18 +1238,6 @@ __device__ __forceinline__ void dual_leaf_at(const F& f, int lo, int m, int i, d
   col = cs;
 }
 
-// d(i,j) = 1 - c/q, q = min(p_i, p_j), with the quotient from q's reciprocal r = fl(1/q)
-// and one exact fma remainder step: equal to the IEEE quotient fl(c/q) for every
-// 0 <= c <= q <= 65,536 (all 2.1e9 pairs checked on the host), so the distances --
-// and with them the totals and representatives -- are md_dist's bit for bit.
-__device__ __forceinline__ double md_dist_r(uint32_t c, int pi, double ri, int pj, double rj) {
-  const int q = pi < pj ? pi : pj;
-  const double cd = (double)c, qd = (double)q;
-  const double r = pi < pj ? ri : rj;
-  const double y = cd * r;
-  const double x = __builtin_fma(__builtin_fma(-y, qd, cd), r, y);
-  return (pi == 0 || pj == 0) ? 1.0 : 1.0 - x;
-}
 #ifndef SPX_MD_LEAF_W
 #define SPX_MD_LEAF_W 1
 #endif
