@@ -701,3 +701,36 @@ def test_bin_mean_mz_representations(gpu, synth):
                 assert_bin_mean_equal(got, ref)
             except AssertionError as e:
                 raise AssertionError(f"batch {name} params {kw}: {e}") from None
+
+
+def test_medoid_large_path_row_widths(gpu):
+    """The large path's bit rows are built in LDS up to 512 row words (32,768 columns)
+    and with global atomics past that (medoid_fill_kernel); the Gram reads them as FP4
+    operands and the leaves kernel takes its quotients from exact reciprocals.  Clusters
+    of n = 65..200 spectra whose distinct 0.1-Da bins fall under (28.5k), at (32,768) and
+    over (33,000; 56.6k) the LDS row width, spectra of 1 to 9,000 peaks, an empty spectrum and identical spectra
+    (count = min size, distance exactly 0): representatives AND totals bit-exact vs
+    the C oracle."""
+    rng = np.random.default_rng(2024)
+    clusters = []
+
+    def spec(mz):
+        mz = np.sort(np.asarray(mz, np.float64))
+        return {"m/z array": mz, "intensity array": np.ones(len(mz)), "precursor mz": 500.0,
+                "precursor charge": 2}
+
+    for n, cols, kmax in ((65, 32000, 3000), (70, 32768, 9000), (80, 33000, 9000), (120, 60000, 3000),
+                          (200, 5000, 3000)):
+        grid = 0.1 * np.arange(1, cols + 1) - 0.05  # one bin per grid value: ceil(m / 0.1) = k
+        members = []
+        for j in range(n):
+            k = int(rng.integers(1, kmax)) if j % 7 else int(rng.integers(1, 40))
+            members.append(spec(rng.choice(grid, size=min(k, cols), replace=False)))
+        members[3] = spec([])                 # an empty spectrum
+        members[5] = dict(members[4])         # identical spectra
+        clusters.append(members)
+    csr = SpectraCSR.from_clusters(clusters)
+    rep, tot = engine.medoid(engine.DeviceBatch.from_host(csr), with_totals=True).to_host()
+    ref_rep, ref_tot = c_oracle.medoid(csr, with_totals=True)
+    np.testing.assert_array_equal(rep, ref_rep)
+    np.testing.assert_array_equal(tot, ref_tot)
