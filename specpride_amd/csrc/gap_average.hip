@@ -62,6 +62,9 @@ constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10
 #ifndef SPX_GA_WUM
 #define SPX_GA_WUM 20
 #endif
+#ifndef SPX_GA_HYBRID
+#define SPX_GA_HYBRID 1  // wide/global kernels: past UM * BLOCK peaks, the first UM * BLOCK stay in registers
+#endif
 #ifndef SPX_GA_EARLY
 #define SPX_GA_EARLY 1  // wide kernel: intensities streamed during the bucket pass, bitmap zeroed under the m/z loads
 #endif
@@ -657,11 +660,18 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     if (Nd > (int64_t)UM * GA_BLOCK) return kDeferred;
   }
   const bool inreg = N <= (int64_t)UM * GA_BLOCK;  // uniform
+  // hybrid (not the LDS kernel, which hands such clusters on): the first UM * BLOCK
+  // peaks are register-resident and tagged like a small cluster's, only the tail is
+  // re-read per pass (600-peak spectra: clusters of 10,800 to 30,000 peaks)
+  constexpr bool kHy = !kDeferBig && SPX_GA_HYBRID;
+  const bool hyb = kHy && !inreg;  // uniform
+  const bool regs = inreg || hyb;
+  const int64_t ptail = p0 + (int64_t)UM * GA_BLOCK;
   double rm[UM];
   uint32_t tags[UM];  // per register peak: pass 2's bucket, then pass 3's slot (for pass 5)
 #pragma unroll
   for (int q = 0; q < UM; ++q) tags[q] = 0u;
-  if (inreg) {
+  if (regs) {
 #pragma unroll
     for (int u = 0; u < UM; ++u) {
       const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
@@ -675,11 +685,12 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     prank[(GA_NW + wid) * kWave + lane] = k.r;
   }
   SPX_GA_STAMP(1);
-  // f(m, it, tag) over every peak; kInten false passes it = 0 and loads none
+  // f(m, it, tag, reg) over every peak; kInten false passes it = 0 and loads none;
+  // reg (a std::bool_constant) is true for a register peak, whose tag is live
   auto peaks_g = [&](auto inten_c, auto tagout_c, auto f) __attribute__((always_inline)) {
     constexpr bool kInten = decltype(inten_c)::value;
     constexpr bool kTagOut = decltype(tagout_c)::value;
-    if (inreg) {
+    if (regs) {
       if (N == 0) return;  // uniform: no peaks (and the batch may hold none to load)
 #pragma unroll
       for (int u0 = 0; u0 < UM; u0 += 8) {
@@ -697,21 +708,29 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
           if (u < UM) {
             const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
             int32_t tag = (int32_t)tags[u];
-            if (k < p1) f(rm[u], kInten ? itb[q] : 0.0, tag);
+            if (k < p1) f(rm[u], kInten ? itb[q] : 0.0, tag, std::true_type{});
             if constexpr (kTagOut) tags[u] = (uint32_t)tag;
           }
+        }
+      }
+      if constexpr (kHy) {
+        if (hyb) {
+          gap_peaks<kInten>(v, ptail, p1, [&](int64_t, double m, double it) {
+            int32_t tag = 0;
+            f(m, it, tag, std::false_type{});
+          });
         }
       }
     } else {
       gap_peaks<kInten>(v, p0, p1, [&](int64_t, double m, double it) {
         int32_t tag = 0;
-        f(m, it, tag);
+        f(m, it, tag, std::false_type{});
       });
     }
   };
   auto peaks = [&](auto f) __attribute__((always_inline)) { peaks_g(std::true_type{}, std::false_type{}, f); };
   auto peaks_m_tag = [&](auto f) __attribute__((always_inline)) { peaks_g(std::false_type{}, std::true_type{}, f); };
-  const bool tagged = inreg;  // passes 3 and 5 take the bucket / slot from registers (uniform)
+  // passes 3 and 5 take a register peak's bucket / slot from its tag
 
   double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
   int bad = 0;
@@ -742,7 +761,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     if (any(bad, 0)) return kNonFinite;
   } else {
     // 1: extrema and finiteness
-    peaks([&](double m, double it, int32_t& tag) {
+    peaks([&](double m, double it, int32_t& tag, auto) {
       bad |= !isfinite(m) || !isfinite(it);
       lo = fmin(lo, m);
       hi = fmax(hi, m);
@@ -846,7 +865,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       for (int w = tid; w < nw; w += GA_BLOCK) S.bitmap[w] = 0ull;
     }
     bar();
-    auto pass2 = [&](double m, double, int32_t& tag) __attribute__((always_inline)) {
+    auto pass2 = [&](double m, double, int32_t& tag, auto) __attribute__((always_inline)) {
       const int64_t b = floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
       tag = (int32_t)b;
       SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
@@ -869,8 +888,8 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   bar();
 
   // 3: per-slot count and m/z extent
-  peaks_m_tag([&](double m, double, int32_t& tag) {
-    const int64_t b = tagged ? (int64_t)tag : floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
+  peaks_m_tag([&](double m, double, int32_t& tag, auto reg_c) {
+    const int64_t b = decltype(reg_c)::value ? (int64_t)tag : floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
     const int slot = bitmap_rank(S.bitmap, S.wprefix, b);
     tag = slot;
     const uint64_t key = f64_order_key(m);
@@ -890,9 +909,10 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   frexp(fmax(fabs(lo), fabs(hi)) * (double)N, &ex_m);
   frexp(imax * (double)N, &ex_i);
   const int sc_m = 61 - ex_m, sc_i = 61 - ex_i;
-  peaks([&](double m, double it, int32_t& tag) {
-    const int slot =
-        tagged ? tag : bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
+  peaks([&](double m, double it, int32_t& tag, auto reg_c) {
+    const int slot = decltype(reg_c)::value
+                         ? tag
+                         : bitmap_rank(S.bitmap, S.wprefix, floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb);
     const uint32_t eg = S.cnt[slot];
     SPX_GUARD(slot >= 0 && slot < D && (int)eg < E, "gap eg c=%ld slot=%d eg=%u E=%d\n", (long)c, slot, eg, E)
     atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[eg]), (unsigned long long)__double2ll_rn(ldexp(m, sc_m)));
