@@ -1064,6 +1064,12 @@ constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS f
 #ifndef SPX_GA_HASH
 #define SPX_GA_HASH 1
 #endif
+#ifndef SPX_GA_HASH3
+#define SPX_GA_HASH3 1  // pass 3 too: a tile's per-slot m/z extents in an LDS table, one global min/max per (tile, slot)
+#endif
+#ifndef SPX_GA_HASH2
+#define SPX_GA_HASH2 1  // pass 2 too: a tile's bitmap words OR-ed in an LDS table, one global OR per (tile, word)
+#endif
 constexpr int GA_HCAP = 2048;
 constexpr int GA_HPROBE = 16;
 
@@ -1413,9 +1419,13 @@ template <int PASS>
 __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) {
   __shared__ double red[GA_NW * 3];
   __shared__ int votes[2 * GA_NW];
-  __shared__ unsigned long long agg_m[PASS == 5 ? GA_GAGG : 1], agg_i[PASS == 5 ? GA_GAGG : 1];
+  constexpr bool kH3 = (PASS == 3 && SPX_GA_HASH3 && SPX_GA_GBATCH) || (PASS == 2 && SPX_GA_HASH2 && SPX_GA_GBATCH);
+  // pass 2 (kH3 too): agg_m holds the hashed words' OR-ed bits
+  // pass 5: group sums (agg_m, agg_i); pass 3 (kH3): the hashed slots' min / max m/z keys
+  __shared__ unsigned long long agg_m[PASS == 5 ? GA_GAGG : (kH3 ? GA_HCAP : 1)];
+  __shared__ unsigned long long agg_i[PASS == 5 ? GA_GAGG : (kH3 && PASS == 3 ? GA_HCAP : 1)];
   __shared__ uint32_t agg_c[PASS == 5 ? GA_GAGG : 1];
-  __shared__ uint32_t hkey[PASS == 5 && SPX_GA_HASH ? GA_HCAP : 1];  // group + 1 (0: empty)
+  __shared__ uint32_t hkey[(PASS == 5 && SPX_GA_HASH) || kH3 ? GA_HCAP : 1];  // group / slot + 1 (0: empty)
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
   const int ng = min(*A.n_giant, A.gmax);
   auto peaks_of = [&](const GapGiant& H, int64_t& p0, int64_t& p1) {
@@ -1433,6 +1443,14 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
     peaks_of(H, p0, p1);
     return (p1 - p0 + GA_TILE - 1) / GA_TILE;
   };
+  if constexpr (kH3) {
+    for (int h = tid; h < GA_HCAP; h += GA_BLOCK) {
+      hkey[h] = 0u;
+      agg_m[h] = PASS == 3 ? ~0ull : 0ull;
+      if constexpr (PASS == 3) agg_i[h] = 0ull;
+    }
+    lds_barrier();
+  }
   if constexpr (PASS == 1) {
     for (int g = 0; g < ng; ++g) {
       if (!A.giants[g].ok) continue;
@@ -1561,7 +1579,30 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
         int64_t b[GA_BATCH];
 #pragma unroll
         for (int q = 0; q < GA_BATCH; ++q) b[q] = floor_div_exact(m[q], A.P.bucket_w, A.P.inv_bucket_w) - kb;
-        if constexpr (PASS == 2) {
+        if constexpr (PASS == 2 && kH3) {
+#pragma unroll
+          for (int q = 0; q < GA_BATCH; ++q) {
+            if (k0 + (int64_t)q * GA_BLOCK >= t1) continue;
+            const uint32_t wi = (uint32_t)(b[q] >> 6);
+            const unsigned long long bit = 1ull << (b[q] & 63);
+            const uint32_t want = wi + 1u;
+            uint32_t h = (wi * 2654435761u) >> (32 - 11);  // log2(GA_HCAP) = 11
+            bool done = false;
+            for (int probe = 0; probe < GA_HPROBE; ++probe, h = (h + 1u) & (GA_HCAP - 1)) {
+              uint32_t k = hkey[h];
+              if (k == 0u) {
+                const uint32_t old = atomicCAS(&hkey[h], 0u, want);
+                k = old == 0u ? want : old;
+              }
+              if (k == want) {
+                if (!(agg_m[h] & bit)) atomicOr(&agg_m[h], bit);
+                done = true;
+                break;
+              }
+            }
+            if (!done && !(S.bitmap[wi] & bit)) atomicOr(&S.bitmap[wi], bit);  // a long probe: globally
+          }
+        } else if constexpr (PASS == 2) {
           unsigned long long w[GA_BATCH];
 #pragma unroll
           for (int q = 0; q < GA_BATCH; ++q) w[q] = S.bitmap[b[q] >> 6];
@@ -1569,6 +1610,37 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           for (int q = 0; q < GA_BATCH; ++q) {
             const unsigned long long bit = 1ull << (b[q] & 63);
             if (k0 + (int64_t)q * GA_BLOCK < t1 && !(w[q] & bit)) atomicOr(&S.bitmap[b[q] >> 6], bit);
+          }
+        } else if constexpr (kH3) {
+          int slot[GA_BATCH];
+#pragma unroll
+          for (int q = 0; q < GA_BATCH; ++q) slot[q] = bitmap_rank(S.bitmap, S.wprefix, b[q]);
+#pragma unroll
+          for (int q = 0; q < GA_BATCH; ++q) {
+            if (k0 + (int64_t)q * GA_BLOCK >= t1) continue;
+            const unsigned long long key = f64_order_key(m[q]);
+            const uint32_t want = (uint32_t)slot[q] + 1u;
+            uint32_t h = ((uint32_t)slot[q] * 2654435761u) >> (32 - 11);  // log2(GA_HCAP) = 11
+            bool done = false;
+            for (int probe = 0; probe < GA_HPROBE; ++probe, h = (h + 1u) & (GA_HCAP - 1)) {
+              uint32_t k = hkey[h];
+              if (k == 0u) {
+                const uint32_t old = atomicCAS(&hkey[h], 0u, want);
+                k = old == 0u ? want : old;
+              }
+              if (k == want) {
+                atomicMin(&agg_m[h], key);
+                atomicMax(&agg_i[h], key);
+                done = true;
+                break;
+              }
+            }
+            if (!done) {  // a long probe: the slot's extent globally
+              unsigned long long* kmin = reinterpret_cast<unsigned long long*>(&S.kmin[slot[q]]);
+              unsigned long long* kmax = reinterpret_cast<unsigned long long*>(&S.kmax[slot[q]]);
+              if (key < *kmin) atomicMin(kmin, key);
+              if (key > *kmax) atomicMax(kmax, key);
+            }
           }
         } else {
           int slot[GA_BATCH];
@@ -1588,6 +1660,29 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
             if (key > hi[q]) atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot[q]]), key);
           }
         }
+      }
+      if constexpr (kH3) {  // the tile's words / slot extents to the slice (only where they change it)
+        lds_barrier();
+        for (int h = tid; h < GA_HCAP; h += GA_BLOCK) {
+          const uint32_t k = hkey[h];
+          if (k) {
+            if constexpr (PASS == 2) {
+              const unsigned long long bits = agg_m[h];
+              if ((S.bitmap[k - 1u] & bits) != bits) atomicOr(&S.bitmap[k - 1u], bits);
+              agg_m[h] = 0ull;
+            } else {
+              unsigned long long* kmin = reinterpret_cast<unsigned long long*>(&S.kmin[k - 1u]);
+              unsigned long long* kmax = reinterpret_cast<unsigned long long*>(&S.kmax[k - 1u]);
+              const unsigned long long lo = agg_m[h], hi = agg_i[h];
+              if (lo < *kmin) atomicMin(kmin, lo);
+              if (hi > *kmax) atomicMax(kmax, hi);
+              agg_m[h] = ~0ull;
+              agg_i[h] = 0ull;
+            }
+            hkey[h] = 0u;
+          }
+        }
+        lds_barrier();
       }
     } else {
       gap_peaks<PASS == 5>(A.v, t0, t1, [&](int64_t, double m, double it) {
