@@ -629,13 +629,20 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
                  align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
                  align256(sizeof(spx::MedoidMeta) * Cm) + 4 * align256(sizeof(int64_t) * (Cm + 1));
   size_t arena = 0, margin = 0;
+  int64_t wide_risk = 0;  // small clusters with more peaks than the wide kernel has bin words for
   for (int64_t c = 0; c < C; ++c) {
     const int64_t n = hco[c + 1] - hco[c];
     const int64_t p = hso[hco[c + 1]] - hso[hco[c]];
     const size_t bytes = medoid_cluster_bytes(n, p);
     if (medoid_large_by_size(n, p)) arena += bytes;
-    else if (n > 1) margin = std::max(margin, bytes);
+    else if (n > 1) {
+      margin = std::max(margin, bytes);
+      wide_risk += p > 64 * (int64_t)spx::MW_KWMAX;
+    }
   }
+  // slots for run-time deferrals: 8, or one per cluster that may overflow the wide
+  // kernel's bins, up to 256 (beyond that a re-run with `extra` takes the rest)
+  const size_t slots = (size_t)std::min<int64_t>(std::max<int64_t>(wide_risk, 8), 256);
   for (int64_t k = 0; k < n_extra; ++k) {
     const int64_t c = extra[k];
     if (c < 0 || c >= C) return 0;
@@ -644,7 +651,7 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
   // small clusters deferred at run time land in the arena too: room for a few of
   // the largest on top (a call that runs out reports SPX_REP_ARENA for them, and a
   // re-run with those clusters in `extra` has room for every one)
-  return fixed + arena + 8 * margin + (size_t(1) << 20);
+  return fixed + arena + slots * margin + (size_t(1) << 20);
 }
 
 int spx_medoid_needs_large_path(const int64_t* hco, const int64_t* hso, int64_t C) {

@@ -507,6 +507,27 @@ def test_medoid_many_runtime_deferrals(gpu):
     np.testing.assert_array_equal(tot, want_tot)
 
 
+def test_medoid_wide_bin_overflow_deferrals(gpu):
+    """small clusters (n <= 64) whose distinct bins overflow the wide
+    kernel's 6,080 are deferred at run time; the workspace query reserves a slot per
+    such cluster (up to 256), and all 40 resolve equal to the oracle, totals included."""
+    rng = np.random.default_rng(11)
+    clusters = []
+    for _c in range(40):
+        n = int(rng.integers(12, 30))
+        spectra = []
+        for _s in range(n):
+            mz = np.sort(np.round(rng.uniform(100.0, 3200.0, 420), 4))
+            spectra.append({"m/z array": mz, "intensity array": rng.uniform(1.0, 9.0, len(mz))})
+        clusters.append(spectra)
+    csr = SpectraCSR.from_clusters(clusters)
+    rep, tot = engine.medoid(engine.DeviceBatch.from_host(csr), with_totals=True).to_host()
+    want_rep, want_tot = c_oracle.medoid(csr, with_totals=True)
+    assert np.all(rep >= 0)
+    np.testing.assert_array_equal(rep, want_rep)
+    np.testing.assert_array_equal(tot, want_tot)
+
+
 def test_bin_mean_split_path(gpu):
     """Clusters past the register and wide kernels (> 128 spectra, > 4,096 distinct
     bins) through the segmented fold and -- with its arena capped -- the bin-range
