@@ -11,11 +11,16 @@ directly in HBM on every rank.
 One step = one pass of the hot path over the resident batch:
   spx_bin_mean (combine_bin_mean, binning.py:170-231, for every cluster) +
   spx_medoid  (medoid representative, most_similar_representative.py:60-111).
-Multi-GPU (torchrun, one process per GPU): every rank owns its own 385k-cluster
-shard (clusters are independent: weak scaling), and each step's results --
-representatives and the compacted consensus peaks -- are gathered to rank 0
-over RCCL inside the timed region, on a second stream that overlaps the next
-step's kernels.  value = all ranks' clusters / max-over-ranks time.
+Multi-GPU (torchrun, one process per GPU), default --scaling strong: every rank
+generates the SAME seeded configs[4] batch and keeps only the clusters of its
+size-balanced LPT bucket (shard.strong_partition: cost = peaks + n*peaks/64, the
+reference's serial loops binning.py:291 / most_similar_representative.py:60 split
+over the GPUs), so total work is fixed as N grows.  Each step's results --
+representatives (as member indices) and the compacted consensus peaks -- are
+gathered to rank 0 over RCCL inside the timed region, on a second stream that
+overlaps the next step's kernels; after the timed region rank 0 reassembles the
+last step in global cluster order and checks it.  value = the batch's clusters /
+max-over-ranks time.  --scaling weak gives every rank its own 385k-cluster batch.
 
 Extra keys (single GPU): the gap-average consensus on the same batch, the
 north-star run (1M clusters on one MI355X), the configs[3] skewed medoid, bin-mean
@@ -58,6 +63,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2000, help="clusters in the CPU-baseline sample (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tier2-chunk-mb", type=int, default=2048, help="tier-2 pipeline chunk (MB of peaks)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong (default): ONE configs[4] batch split over the ranks by size-balanced LPT "
+                         "buckets; weak: every rank its own --clusters batch")
+    ap.add_argument("--tier3-clusters", type=int, default=20000, help="tier-3 MGF size in clusters (0: skip)")
     return ap.parse_args()
 
 
@@ -135,12 +144,20 @@ def load_shape_traffic(key: str):
         return None
 
 
-def roofline(name, kernel, nbytes, ms, traffic=None):
+def roofline(name, kernel, nbytes, ms, traffic=None, kernel_ms=None):
+    """HBM roofline of one entry point: ``nbytes`` algorithmic bytes of the WHOLE batch
+    over ``ms``, the time of the launches that process all of them (the entry point's:
+    every cluster a first kernel hands on is finished inside it), so nothing deferred is
+    counted without its time.  ``kernel_ms`` = the dominant kernel's own launch time
+    (spx_profile events; the rocprofv3 kernel stats agree with it), reported beside."""
     gbs = nbytes / (ms * 1e-3) / 1e9
-    return {"bound": "hbm", "kernel": kernel, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "frac_of_achievable": round(gbs / HBM_ACHIEVABLE_GBS, 4),
-            "achievable": HBM_ACHIEVABLE_GBS, "traffic": traffic, "launch_ms": round(ms, 4),
-            "algorithmic_bytes": int(nbytes), "entry_point": name}
+    r = {"bound": "hbm", "kernel": kernel, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(gbs / HBM_PEAK_GBS, 4), "frac_of_achievable": round(gbs / HBM_ACHIEVABLE_GBS, 4),
+         "achievable": HBM_ACHIEVABLE_GBS, "traffic": traffic, "launch_ms": round(ms, 4),
+         "algorithmic_bytes": int(nbytes), "entry_point": name}
+    if kernel_ms is not None:
+        r["dominant_kernel_ms"] = round(kernel_ms, 4)
+    return r
 
 
 def time_launches(fn, reps, stream):
@@ -227,11 +244,28 @@ def cpu_baseline_parallel(n_clusters: int, seed: int):
 def headline(args, rank, world, local, out):
     import torch
 
-    from specpride_amd import engine
+    from specpride_amd import engine, shard
+    from specpride_amd.csr import SpectraCSR
     from specpride_amd.synthetic import make_clusters_torch
 
     dev = torch.device("cuda", local)
-    t = make_clusters_torch(args.clusters, seed=args.seed + 1000 * rank, device=dev)
+    strong = args.scaling == "strong"
+    parts = loads = None
+    global_co = None
+    if strong:
+        # every rank generates the SAME seeded configs[4] batch and keeps the clusters the
+        # size-balanced LPT plan gives it (shard.strong_partition, identical on every rank)
+        t = make_clusters_torch(args.clusters, seed=args.seed, device=dev)
+        if world > 1:
+            global_co = t["cluster_off"].cpu().numpy()
+            so = t["spec_off"].cpu().numpy()
+            parts, loads = shard.strong_partition(global_co, so, world, "both")
+            full, t = t, None
+            t = SpectraCSR.select_on_device(full, parts[rank], global_co, so)
+            del full, so
+            torch.cuda.empty_cache()
+    else:
+        t = make_clusters_torch(args.clusters, seed=args.seed + 1000 * rank, device=dev)
     batch = engine.DeviceBatch.from_device(t)
     torch.cuda.synchronize()
 
@@ -246,15 +280,14 @@ def headline(args, rank, world, local, out):
     kept = int(bm.count[:batch.n_clusters].sum().item())
     large = engine.medoid_needs_large_path(batch) or bool(batch._ws.get("medoid_extra"))
     stream = torch.cuda.current_stream()
+    first = batch.t["cluster_off"][:-1] if strong else None
 
     # double-buffered results when gathering (step k's are in flight during step k+1)
     bufs = [(bm, md)]
     gat = None
     if world > 1:
-        from specpride_amd.shard import StepGatherer
-
         bufs.append((engine.bin_mean(batch), engine.medoid(batch, check=False)))
-        gat = StepGatherer(batch.n_clusters, rank, world, batch.device)
+        gat = shard.StepGatherer(batch.n_clusters, rank, world, batch.device)
         total_c, total_p = gat.plan(kept)
 
     inflight = [None] * len(bufs)  # per buffer: the event of the gather reading it
@@ -269,7 +302,7 @@ def headline(args, rank, world, local, out):
         if gat is not None:
             ev = torch.cuda.Event()
             ev.record(stream)
-            inflight[i] = gat.launch(b, m.rep, ev)
+            inflight[i] = gat.launch(b, m.rep, ev, first=first)
 
     for k in range(args.warmup):
         step(k)
@@ -281,7 +314,24 @@ def headline(args, rank, world, local, out):
         gat.stream.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    value = world * batch.n_clusters * args.steps / elapsed
+    total_clusters = (args.clusters if strong else world * batch.n_clusters)
+    value = total_clusters * args.steps / elapsed
+
+    assembled = None
+    if gat is not None and strong:
+        # rank 0 reassembles the last step's gathered results in global cluster order
+        # (host-side index, after the timed region): every representative resolved and
+        # the consensus peak count equal to the sum the ranks planned
+        last = bufs[(args.warmup + args.steps - 1) % len(bufs)]
+        if rank == 0:
+            own_member = torch.where(last[1].rep[:batch.n_clusters] >= 0,
+                                     last[1].rep[:batch.n_clusters] - first, last[1].rep[:batch.n_clusters])
+            a = gat.assemble(parts, global_co, last[0], own_member)
+            assembled = {"clusters": int(len(a["rep"])), "reps_resolved": bool(np.all(a["rep"] >= 0)),
+                         "consensus_peaks": int(a["out_off"][-1]), "planned_peaks": int(total_p),
+                         "ok": bool(np.all(a["rep"] >= 0) and int(a["out_off"][-1]) == int(total_p))}
+            del a
+        barrier(world)
 
     # per-kernel timing, after the timed region: HIP events on the stream the kernels
     # are launched on -- around each whole entry point, and (spx_profile_*) around
@@ -305,28 +355,37 @@ def headline(args, rank, world, local, out):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY.md §8(d) law, generated in HBM per rank; stand-in for the ~10M-spectrum PRIDE set)",
         "config": {"workload": "configs[4]: full pipeline (bin-mean consensus + medoid representative) on a "
                                "PRIDE-scale clustered dataset of ~10M spectra, U{2..50} spectra/cluster, "
                                "~200 peaks/spectrum",
-                   "clusters_per_gpu": batch.n_clusters, "spectra_per_gpu": batch.n_spectra,
-                   "peaks_per_gpu": batch.n_peaks, "parallelism": f"cluster-sharded x{world}",
+                   "clusters": total_clusters, "clusters_this_rank": batch.n_clusters,
+                   "spectra_this_rank": batch.n_spectra, "peaks_this_rank": batch.n_peaks,
+                   "parallelism": (f"cluster-sharded x{world}, size-balanced LPT buckets of one batch "
+                                   "(cost = peaks + n*peaks/64)" if strong and world > 1
+                                   else f"cluster-sharded x{world}"),
                    "gather": ("per-step RCCL gather of reps + compacted consensus peaks to rank 0, "
                               "overlapped with the next step" if world > 1 else "none (1 GPU: results stay in HBM)"),
                    "medoid_large_path": bool(large)},
-        "roofline": roofline("spx_bin_mean", "bin_mean_reg_kernel", bm_bytes, bm_ms,
-                             load_pmc_traffic("bin_mean_reg_kernel", batch)),
-        "roofline_medoid": roofline("spx_medoid", "medoid_reg_kernel", medoid_bytes(batch), md_ms,
-                                    load_pmc_traffic("medoid_reg_kernel", batch)),
+        "roofline": roofline("spx_bin_mean", "bin_mean_reg_kernel", bm_bytes, bm_ms_ep,
+                             load_pmc_traffic("bin_mean_reg_kernel", batch), kernel_ms=bm_ms),
+        "roofline_medoid": roofline("spx_medoid", "medoid_reg_kernel", medoid_bytes(batch), md_ms_ep,
+                                    load_pmc_traffic("medoid_reg_kernel", batch), kernel_ms=md_ms),
         "kernels": {"spx_bin_mean_ms": round(bm_ms_ep, 4), "spx_medoid_ms": round(md_ms_ep, 4),
                     "bin_mean_reg_kernel_ms": round(bm_ms, 4), "medoid_reg_kernel_ms": round(md_ms, 4)},
     })
     if gat is not None:
         out["config"]["gathered_clusters_per_step"] = total_c
         out["config"]["gathered_peaks_per_step"] = total_p
+    if loads is not None:
+        out["config"]["rank_cost_share"] = [round(float(x / loads.sum()), 5) for x in loads]
+        out["config"]["cost_max_over_min"] = round(float(loads.max() / max(loads.min(), 1.0)), 5)
+        out["config"]["rank_clusters"] = [int(len(p)) for p in parts]
+    if assembled is not None:
+        out["config"]["assembled_last_step"] = assembled
     if rank == 0 and world == 1 and not args.no_extras:
         # the same step through the fused entry point (spx_bin_mean_medoid: both register
         # bodies per workgroup, then each method's leftover chain); results checked equal
@@ -355,8 +414,8 @@ def headline(args, rank, world, local, out):
         out["gap_average"] = {"clusters_per_s": round(batch.n_clusters / (ga_ms * 1e-3), 1), "launch_ms": round(ga_ms, 4),
                               "lds_kernel_ms": round(ga_k, 4), "ok_clusters": int((gst == 0).sum()),
                               "roofline": roofline("spx_gap_average", "gap_average_lds_kernel",
-                                                   consensus_bytes(batch, gkept), ga_k,
-                                                   load_pmc_traffic("gap_average_lds_kernel", batch))}
+                                                   consensus_bytes(batch, gkept), ga_ms,
+                                                   load_pmc_traffic("gap_average_lds_kernel", batch), kernel_ms=ga_k)}
         del ga
     del bm, md, bufs, batch, t
     torch.cuda.empty_cache()
@@ -408,7 +467,8 @@ def north_star(args, out):
     out["north_star_1m"]["gap_average"] = {
         "ms": round(ga_ms, 3), "clusters_per_s": round(batch.n_clusters / (ga_ms * 1e-3), 1),
         "ok_clusters": int((gst == 0).sum()), "lds_kernel_ms": round(ga_k, 3),
-        "roofline": roofline("spx_gap_average", "gap_average_lds_kernel", consensus_bytes(batch, gkept), ga_k),
+        "roofline": roofline("spx_gap_average", "gap_average_lds_kernel", consensus_bytes(batch, gkept), ga_ms,
+                             kernel_ms=ga_k),
         "hbm_gb_resident": round(torch.cuda.max_memory_allocated() / 1e9, 1)}
     del ga, batch, t
     torch.cuda.empty_cache()
@@ -608,6 +668,61 @@ def tier2(args, out):
     torch.cuda.empty_cache()
 
 
+def tier3(args, out):
+    """SURVEY.md §8(d) tier 3: each of the three CLIs MGF text -> MGF text on one
+    synthetic clustered MGF (configs law, --tier3-clusters clusters, written once
+    before the timed region by the native writer): binning.py (binning.py:250-302),
+    average_spectrum_clustering.py --encodedclusters (:168-210) and
+    most_similar_representative.py (:22-115).  Each CLI runs once on a 200-cluster
+    file first (code objects, allocator, pinned staging), then is timed on the big
+    one.  The reference's own binning CLI on the same file shape, timed in the
+    build container (the reference never reaches the GPU box), is reported beside
+    it from profiles/r02_reference_cli_container.json.  Never `value`."""
+    import contextlib
+    import io
+    import tempfile
+
+    import torch
+
+    from specpride_amd import average_spectrum_clustering as asc
+    from specpride_amd import binning
+    from specpride_amd import most_similar_representative as msr
+    from specpride_amd.synthetic import write_clustered_mgf
+
+    clis = {"binning": lambda i, o: binning.main(["--mgf_file", i, "--out", o]),
+            "average_spectrum_clustering": lambda i, o: asc.main([i, o, "--encodedclusters"]),
+            "most_similar_representative": lambda i, o: msr.main(["-i", i, "-o", o])}
+    res = {}
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        warm_in, mgf_in, mgf_out = (os.path.join(td, x) for x in ("w.mgf", "in.mgf", "out.mgf"))
+        write_clustered_mgf(warm_in, 200, args.seed + 22)
+        t0 = time.perf_counter()
+        S, P = write_clustered_mgf(mgf_in, args.tier3_clusters, args.seed + 21)
+        size = os.path.getsize(mgf_in)
+        res.update(clusters=args.tier3_clusters, spectra=S, peaks=P, mgf_bytes=int(size),
+                   input_write_s=round(time.perf_counter() - t0, 2))
+        torch.cuda.empty_cache()
+        for name, cli in clis.items():
+            with contextlib.redirect_stdout(io.StringIO()):
+                cli(warm_in, mgf_out)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                cli(mgf_in, mgf_out)
+                dt = time.perf_counter() - t0
+            res[name] = {"cli_s": round(dt, 3), "clusters_per_s": round(args.tier3_clusters / dt, 1),
+                         "mgf_in_GBs": round(size / dt / 1e9, 3), "mgf_out_bytes": int(os.path.getsize(mgf_out))}
+    try:
+        with open(os.path.join(REPO, "profiles", "r02_reference_cli_container.json")) as fh:
+            ref = json.load(fh)
+        res["reference_binning_cli"] = {"clusters_per_s": ref["clusters_per_s"], "cores": ref["cores"],
+                                        "where": ref["host"], "file": f"{ref['clusters']} clusters, "
+                                                                      f"{ref['mgf_MB']} MB MGF"}
+        res["binning_vs_reference_cli"] = round(res["binning"]["clusters_per_s"] / ref["clusters_per_s"], 1)
+    except (OSError, ValueError, KeyError):
+        pass
+    out["tier3_mgf_to_mgf"] = res
+
+
 def main():
     args = parse()
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
@@ -622,6 +737,8 @@ def main():
         medoid_shapes(args, out)
         gap_average_shapes(args, out)
         tier2(args, out)
+        if args.tier3_clusters > 0:
+            tier3(args, out)
         if args.ns_clusters > 0:
             north_star(args, out)
     if rank == 0 and want_cpu:

@@ -167,6 +167,37 @@ class SpectraCSR:
         g = lambda k: d[k].detach().cpu().numpy()  # noqa: E731
         return cls(g("cluster_off"), g("spec_off"), g("mz"), g("inten"), g("prec_mz"), g("charge"), g("rt"))
 
+    @staticmethod
+    def select_on_device(d: dict, clusters, host_cluster_off=None, host_spec_off=None) -> dict:
+        """A new DEVICE batch (the dict layout of :meth:`to_device`) holding only
+        ``clusters`` (in the given order) of the device batch ``d``: offsets are
+        rebuilt on the host from the (optionally passed) host offsets, the peaks and
+        per-spectrum fields are gathered in HBM.  This is how a rank keeps its share
+        of a batch every rank generated identically (bench.py strong scaling)."""
+        import torch
+
+        clusters = np.asarray(clusters, np.int64)
+        co = d["cluster_off"].cpu().numpy() if host_cluster_off is None else np.asarray(host_cluster_off, np.int64)
+        so = d["spec_off"].cpu().numpy() if host_spec_off is None else np.asarray(host_spec_off, np.int64)
+        sizes = co[clusters + 1] - co[clusters]
+        cluster_off = np.zeros(len(clusters) + 1, np.int64)
+        np.cumsum(sizes, out=cluster_off[1:])
+        spectra = concat_ranges(co[clusters], sizes)
+        lens = so[spectra + 1] - so[spectra]
+        spec_off = np.zeros(len(spectra) + 1, np.int64)
+        np.cumsum(lens, out=spec_off[1:])
+        dev = d["mz"].device
+        idx = torch.from_numpy(concat_ranges(so[spectra], lens)).to(dev)
+        sidx = torch.from_numpy(spectra).to(dev)
+        out = {k: d[k].index_select(0, sidx) for k in ("prec_mz", "charge", "rt")}
+        out["mz"] = d["mz"].index_select(0, idx)
+        out["inten"] = d["inten"].index_select(0, idx)
+        del idx
+        out["cluster_off"] = torch.from_numpy(cluster_off).to(dev)
+        out["spec_off"] = torch.from_numpy(spec_off).to(dev)
+        out.update(n_clusters=len(clusters), n_spectra=len(spectra), n_peaks=int(spec_off[-1]))
+        return out
+
     @classmethod
     def select_from_device(cls, d: dict, clusters) -> "SpectraCSR":
         """Host copy of only ``clusters`` (in the given order) of a device batch:

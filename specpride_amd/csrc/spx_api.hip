@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -347,10 +348,10 @@ struct BinMeanHead {
   void* ctx;
 };
 
-int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
-                  spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* workspace,
-                  size_t workspace_bytes, void* stream, int stage, const BinMeanHead* head) {
-  if (stage < 0 || stage > 2) return fail(SPX_EINVAL, "spx_bin_mean_stage: stage must be 0, 1 or 2");
+// argument and workspace checks of spx_bin_mean (also run up front by the fused entry point)
+int bin_mean_validate(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
+                      const spx_peaks_out* out, const double* prec_out, const int32_t* charge_out,
+                      const int32_t* status, const void* workspace, size_t workspace_bytes) {
   if (!csr_ok(csr) || !params || !info || !out || !out->count || !prec_out || !charge_out || !status)
     return fail(SPX_EINVAL, "spx_bin_mean: null argument");
   if (!(params->binsize > 0) || !(params->maximum > params->minimum))
@@ -358,6 +359,15 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
   if (csr->n_peaks && (!out->mz || !out->inten)) return fail(SPX_EINVAL, "spx_bin_mean: null output arrays");
   const size_t need = spx_bin_mean_workspace_size(csr, params, info);
   if (!workspace || workspace_bytes < need) return fail(SPX_ENOSPACE, "spx_bin_mean: workspace too small");
+  return SPX_SUCCESS;
+}
+
+int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
+                  spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* workspace,
+                  size_t workspace_bytes, void* stream, int stage, const BinMeanHead* head) {
+  if (stage < 0 || stage > 2) return fail(SPX_EINVAL, "spx_bin_mean_stage: stage must be 0, 1 or 2");
+  if (int rc = bin_mean_validate(csr, params, info, out, prec_out, charge_out, status, workspace, workspace_bytes))
+    return rc;
   const int64_t C = csr->n_clusters;
   if (C == 0) return SPX_SUCCESS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -629,7 +639,9 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
                  align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
                  align256(sizeof(spx::MedoidMeta) * Cm) + 4 * align256(sizeof(int64_t) * (Cm + 1));
   size_t arena = 0, margin = 0;
-  int64_t wide_risk = 0;  // small clusters with more peaks than the wide kernel has bin words for
+  // small clusters with more peaks than the wide kernel has bin words for: the only
+  // ones a run can defer into the arena (their arena bytes)
+  std::vector<size_t> risk;
   for (int64_t c = 0; c < C; ++c) {
     const int64_t n = hco[c + 1] - hco[c];
     const int64_t p = hso[hco[c + 1]] - hso[hco[c]];
@@ -637,21 +649,25 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
     if (medoid_large_by_size(n, p)) arena += bytes;
     else if (n > 1) {
       margin = std::max(margin, bytes);
-      wide_risk += p > 64 * (int64_t)spx::MW_KWMAX;
+      if (p > 64 * (int64_t)spx::MW_KWMAX) risk.push_back(bytes);
     }
   }
-  // slots for run-time deferrals: 8, or one per cluster that may overflow the wide
-  // kernel's bins, up to 256 (beyond that a re-run with `extra` takes the rest)
-  const size_t slots = (size_t)std::min<int64_t>(std::max<int64_t>(wide_risk, 8), 256);
   for (int64_t k = 0; k < n_extra; ++k) {
     const int64_t c = extra[k];
     if (c < 0 || c >= C) return 0;
     arena += medoid_cluster_bytes(hco[c + 1] - hco[c], hso[hco[c + 1]] - hso[hco[c]]);
   }
-  // small clusters deferred at run time land in the arena too: room for a few of
-  // the largest on top (a call that runs out reports SPX_REP_ARENA for them, and a
-  // re-run with those clusters in `extra` has room for every one)
-  return fixed + arena + slots * margin + (size_t(1) << 20);
+  // Room for run-time deferrals on top: the arena bytes of the 256 largest at-risk
+  // clusters (all of them when fewer), and never less than 8 slots of the largest
+  // small cluster.  A call that still runs out reports SPX_REP_ARENA for the rest, and
+  // a re-run with those clusters in `extra` has room for every one.
+  const size_t slots = std::min<size_t>(risk.size(), 256);
+  if (slots < risk.size())
+    std::nth_element(risk.begin(), risk.begin() + (ptrdiff_t)slots, risk.end(), std::greater<size_t>());
+  size_t reserve = 0;
+  for (size_t k = 0; k < slots; ++k) reserve += risk[k];
+  reserve = std::max(reserve, 8 * margin);
+  return fixed + arena + reserve + (size_t(1) << 20);
 }
 
 int spx_medoid_needs_large_path(const int64_t* hco, const int64_t* hso, int64_t C) {
@@ -672,15 +688,22 @@ struct MedoidHead {
 // part 0: the whole call; 1: checks, workspace carving and the memset only (the
 // caller launches the head kernel: spx_bin_mean_medoid); 2: everything after the
 // register kernel (the wide kernel and the large path), on the same workspace.
-int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep, double* totals, void* workspace,
-                size_t workspace_bytes, void* stream, int part, MedoidHead* head) {
+// argument checks of spx_medoid (also run up front by the fused entry point)
+int medoid_validate(const spx_csr* csr, const spx_medoid_params* params, const int64_t* rep,
+                    const void* workspace) {
   if (!csr_ok(csr) || !params || !rep) return fail(SPX_EINVAL, "spx_medoid: null argument");
   if (!(params->tolerance > 0)) return fail(SPX_EINVAL, "spx_medoid: tolerance must be > 0");
+  if (csr->n_clusters > 0 && !workspace) return fail(SPX_ENOSPACE, "spx_medoid: no workspace");
+  return SPX_SUCCESS;
+}
+
+int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep, double* totals, void* workspace,
+                size_t workspace_bytes, void* stream, int part, MedoidHead* head) {
+  if (int rc = medoid_validate(csr, params, rep, workspace)) return rc;
   const int64_t C = csr->n_clusters;
   if (C == 0) return SPX_SUCCESS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
-  if (!workspace) return fail(SPX_ENOSPACE, "spx_medoid: no workspace");
   int32_t* n_def = w.take<int32_t>(1);
   unsigned long long* bump = w.take<unsigned long long>(1);
   spx::StripedList wide;  // the register kernel's leftovers for the wide kernel (striped appends)
@@ -781,6 +804,11 @@ int spx_bin_mean_medoid(const spx_csr* csr, const spx_bin_params* bin_params, co
                         size_t bin_workspace_bytes, const spx_medoid_params* medoid_params, int64_t* rep,
                         double* totals, void* medoid_workspace, size_t medoid_workspace_bytes, void* stream) {
   if (!csr_ok(csr)) return fail(SPX_EINVAL, "spx_bin_mean_medoid: null argument");
+  // both methods' checks before anything is enqueued (and before the empty-batch return)
+  if (int rc = bin_mean_validate(csr, bin_params, info, out, prec_out, charge_out, status, bin_workspace,
+                                 bin_workspace_bytes))
+    return rc;
+  if (int rc = medoid_validate(csr, medoid_params, rep, medoid_workspace)) return rc;
   if (csr->n_clusters == 0) return SPX_SUCCESS;
   MedoidHead H{};
   if (int rc = medoid_impl(csr, medoid_params, rep, totals, medoid_workspace, medoid_workspace_bytes, stream, 1, &H))

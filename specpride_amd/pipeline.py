@@ -176,6 +176,7 @@ class HostPipeline:
                "out_int": np.empty(max(csr.n_peaks, 1)), "status": np.empty(C, np.int32),
                "prec": np.empty(C), "charge": np.empty(C, np.int32), "rep": np.empty(C, np.int64)}
         kept = [0]
+        redo = []  # chunks whose medoid deferred clusters at run time
         tm = {"h2d_host_s": 0.0, "readback_s": 0.0, "kernel_ms": 0.0, "chunks": len(chunks)}
         kev = []
 
@@ -218,14 +219,25 @@ class HostPipeline:
                     rep = slot.md.rep[:Cc].cpu().numpy()
                 res["rep"][c0:c1] = np.where(rep >= 0, rep + co[c0], rep)
                 kept[0] = k0 + n
-                # the medoid's run-time deferrals (REP_DEFERRED / REP_ARENA) are resolved
-                # by the checked call, once, outside the overlapped loop
+                # the medoid's run-time deferrals (REP_DEFERRED / REP_ARENA): the chunk is
+                # re-run by the checked call after the overlapped loop (redo), so the
+                # copy and compute streams never drain here
                 if np.any((rep == engine.REP_DEFERRED) | (rep == engine.REP_ARENA)):
-                    torch.cuda.synchronize(self.device)
-                    md = engine.medoid(batch, out=slot.md, check=True)
-                    r2 = md.rep[:Cc].cpu().numpy()
-                    res["rep"][c0:c1] = np.where(r2 >= 0, r2 + co[c0], r2)
+                    redo.append(i)
             tm["readback_s"] += time.perf_counter() - t0
+
+        def resolve(i):
+            """Chunk i again, after the loop: H2D into slot 0, the checked medoid."""
+            slot = self.slots[0]
+            ev = self._h2d(slot, csr, *chunks[i])
+            ev.synchronize()
+            batch = self._batch(slot, csr)
+            _, md = self._outputs(slot, batch)
+            c0, c1 = slot.chunk
+            with torch.cuda.device(self.device):
+                md = engine.medoid(batch, out=md, check=True)  # the current stream, synchronised reads
+                r2 = md.rep[:c1 - c0].cpu().numpy()
+            res["rep"][c0:c1] = np.where(r2 >= 0, r2 + co[c0], r2)
 
         in_ev = [None] * len(chunks)
         batches = [None] * len(chunks)
@@ -247,6 +259,11 @@ class HostPipeline:
         if chunks:
             readback(len(chunks) - 1, batches[-1])
         torch.cuda.synchronize(self.device)
+        tm["redo_chunks"] = len(redo)
+        for i in redo:
+            t0 = time.perf_counter()
+            resolve(i)
+            tm["readback_s"] += time.perf_counter() - t0
         tm["kernel_ms"] = sum(a.elapsed_time(b) for a, b in kev)
         self.timing = tm
         res["out_mz"] = res["out_mz"][:kept[0]]

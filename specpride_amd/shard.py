@@ -190,11 +190,16 @@ class StepGatherer:
         self.send_peaks = int(kept_peaks)
         return sum(x[0] for x in self.recv_sizes), sum(x[1] for x in self.recv_sizes)
 
-    def launch(self, bm, rep, done_event=None):
+    def launch(self, bm, rep, done_event=None, first=None):
         """Enqueue the gather of one step's results (consensus ``bm`` with
         ``.count`` and ``.compact``, representatives ``rep``) after
         ``done_event``; returns an event that completes when this rank's part of
-        the gather has (None on CPU, where the call blocks until it has)."""
+        the gather has (None on CPU, where the call blocks until it has).
+
+        With ``first`` (the rank's local ``cluster_off[:-1]``) the representatives
+        travel as member indices within their cluster (``rep - first``; failure
+        codes < 0 pass through), which rank 0 maps to global spectrum indices in
+        :meth:`assemble`; without it, as the rank's local spectrum indices."""
         import contextlib
 
         import torch
@@ -204,6 +209,9 @@ class StepGatherer:
         with ctx:
             if self.cuda and done_event is not None:
                 self.stream.wait_event(done_event)
+            if first is not None:
+                r = rep[:self.n]
+                rep = torch.where(r >= 0, r - first[:self.n], r)
             if self.rank == 0:
                 ops = []
                 for r in range(1, self.world):
@@ -231,6 +239,66 @@ class StepGatherer:
             ev = torch.cuda.Event()
             ev.record(self.stream)
         return ev
+
+    def assemble(self, parts: list, cluster_off: np.ndarray, own_bm, own_member) -> dict:
+        """Rank 0, after a step's gather has completed: the whole batch's results in
+        GLOBAL cluster order from rank 0's own (``own_bm``, ``own_member``) and the
+        peers' received buffers (sent with ``first=``).  ``parts[r]`` = the ascending
+        global cluster ids of rank r (:func:`plan_costs`), ``cluster_off`` = the global
+        spectrum offsets.  Returns host arrays: ``out_off``, ``out_mz``, ``out_int``
+        (the compacted consensus peaks), ``count``, ``rep`` (global spectrum index, or
+        the failure code).  A host-side index: not part of the timed device pass."""
+        if self.rank != 0:
+            raise RuntimeError("assemble() runs on rank 0")
+        cluster_off = np.asarray(cluster_off, np.int64)
+        C = len(cluster_off) - 1
+        count = np.zeros(C, np.int64)
+        member = np.full(C, -1, np.int64)
+        pieces = {}
+        for r, ids in enumerate(parts):
+            ids = np.asarray(ids, np.int64)
+            n = len(ids)
+            if r == 0:
+                cnt = own_bm.count[:n].to("cpu").numpy()
+                _, mz, it = own_bm.compact(total=int(cnt.sum()))
+                mem = own_member[:n].to("cpu").numpy()
+            else:
+                c_r, p_r = self.recv_sizes[r]
+                if c_r != n:
+                    raise ValueError(f"rank {r} sent {c_r} clusters, the plan gives it {n}")
+                b = self.recv[r]
+                cnt = b[0][:n].cpu().numpy()
+                mem = b[1][:n].cpu().numpy()
+                mz, it = b[2][:p_r], b[3][:p_r]
+            count[ids] = cnt
+            member[ids] = mem
+            pieces[r] = (ids, cnt, mz.cpu().numpy(), it.cpu().numpy())
+        out_off = np.zeros(C + 1, np.int64)
+        np.cumsum(count, out=out_off[1:])
+        out_mz = np.empty(int(out_off[-1]), np.float64)
+        out_int = np.empty_like(out_mz)
+        for ids, cnt, mz, it in pieces.values():
+            dst = concat_ranges(out_off[ids], cnt)
+            out_mz[dst] = mz[:len(dst)]
+            out_int[dst] = it[:len(dst)]
+        rep = np.where(member >= 0, cluster_off[:-1] + member, member)
+        return dict(out_off=out_off, out_mz=out_mz, out_int=out_int, count=count, rep=rep)
+
+
+def strong_partition(cluster_off, spec_off, world: int, method: str = "both"):
+    """bench.py's strong-scaling split of ONE batch (the same on every rank: each
+    rank computes it from the offsets of the batch it generated identically):
+    size-balanced LPT buckets (:func:`plan_costs`) over the per-cluster cost of
+    ``method`` -- "both" = Σpeaks (bin-mean) + n·Σpeaks/64 (medoid).  Returns
+    ``(parts, loads)``: rank -> ascending global cluster ids, and each rank's cost."""
+    co = np.asarray(cluster_off, np.int64)
+    so = np.asarray(spec_off, np.int64)
+    sizes = np.diff(co)
+    peaks = so[co[1:]] - so[co[:-1]]
+    cost = costs_from_sizes(sizes, peaks, method)
+    parts = plan_costs(cost, world)
+    loads = np.array([float(cost[p].sum()) for p in parts])
+    return parts, loads
 
 
 # ------------------------------------------------------------ default compute

@@ -178,3 +178,25 @@ def make_clusters_torch(n_clusters: int, seed: int = 0, *, device="cuda", min_si
     rt = torch.round(3600.0 * torch.rand(S, generator=g, device=device, dtype=f64) * 100.0) / 100.0
     return dict(cluster_off=cluster_off, spec_off=spec_off, mz=mz, inten=inten, prec_mz=prec,
                 charge=charge.contiguous(), rt=rt, n_clusters=C, n_spectra=S, n_peaks=P)
+
+
+def write_clustered_mgf(path: str, n_clusters: int, seed: int = 0, device="cuda") -> tuple:
+    """Write a clustered MGF of this law (the reference's title convention,
+    file_formats.md: ``TITLE=cluster-<c>;mzspec:PXDSYN:synthetic:scan:<s>``, PEPMASS,
+    CHARGE, RTINSECONDS, repr floats) with the native batched writer; the batch is
+    generated by :func:`make_clusters_torch` on ``device``.  Returns (spectra, peaks).
+    The tier-3 benchmarks' input (bench.py, tools/bench_tiers.py)."""
+    import torch
+
+    from . import engine, mgf_native
+
+    t = make_clusters_torch(n_clusters, seed=seed, device=device)
+    h = {k: engine.to_host_array(t[k]) for k in ("cluster_off", "spec_off", "mz", "inten", "prec_mz", "charge", "rt")}
+    del t
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+    owner = np.repeat(np.arange(n_clusters), np.diff(h["cluster_off"]))
+    titles = [f"cluster-{c};mzspec:PXDSYN:synthetic:scan:{s}" for s, c in enumerate(owner.tolist())]
+    mgf_native.write_records(path, mgf_native.STYLE_MEDOID, titles, h["spec_off"], h["mz"], h["inten"],
+                             h["prec_mz"], h["charge"], h["rt"])
+    return int(len(owner)), int(h["spec_off"][-1])

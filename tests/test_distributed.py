@@ -173,3 +173,71 @@ def test_step_gatherer_gloo(world):
     assert all(ok for ok, _ in got.values())
     want_c = sum(5 + 3 * r for r in range(world))
     assert all(tot[0] == want_c for _, tot in got.values())
+
+
+# ------------------------------------------- bench.py's strong-scaling partition
+class _OracleConsensus:
+    """An oracle bin-mean result with the two members StepGatherer/assemble use:
+    ``count`` and ``compact(stream=, total=)`` (dense already)."""
+
+    def __init__(self, r):
+        self.count = torch.from_numpy(np.diff(r["out_off"]))
+        self._off = torch.from_numpy(r["out_off"])
+        self._mz, self._int = torch.from_numpy(r["out_mz"]), torch.from_numpy(r["out_int"])
+
+    def compact(self, stream=None, total=None):
+        assert total is None or total == int(self._off[-1])
+        return self._off, self._mz, self._int
+
+
+def _strong_worker(rank, world, port, q):
+    from oracle import c_oracle
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # every rank builds the same batch and keeps its LPT bucket, as bench.py does
+        csr = make_clusters_np(61, seed=23)
+        parts, loads = shard.strong_partition(csr.cluster_off, csr.spec_off, world, "both")
+        sub = csr.select(parts[rank])
+        bm = _OracleConsensus(c_oracle.bin_mean(sub))
+        rep = torch.from_numpy(c_oracle.medoid(sub))
+        first = torch.from_numpy(sub.cluster_off[:-1])
+        gat = shard.StepGatherer(sub.n_clusters, rank, world, "cpu")
+        gat.plan(int(bm.count.sum()))
+        for _ in range(2):  # two steps through the same receive buffers
+            assert gat.launch(bm, rep, first=first) is None
+        if rank == 0:
+            own_member = torch.where(rep >= 0, rep - first, rep)
+            q.put((gat.assemble(parts, csr.cluster_off, bm, own_member), loads.tolist(),
+                   [len(p) for p in parts]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strong_partition_gather_equals_world1(world):
+    """bench.py --scaling strong at world 2/3 under gloo: the size-balanced LPT split
+    of ONE batch (shard.strong_partition), per-rank compute on the rank's clusters,
+    the per-step gather with member-index representatives, and rank 0's reassembly
+    in global order (StepGatherer.assemble) give exactly the world-1 results."""
+    from oracle import c_oracle
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_strong_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, loads, sizes = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    csr = make_clusters_np(61, seed=23)
+    ref = c_oracle.bin_mean(csr)
+    for k in ("out_off", "out_mz", "out_int"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    np.testing.assert_array_equal(got["rep"], c_oracle.medoid(csr))
+    assert sum(sizes) == csr.n_clusters and min(sizes) > 0
+    cost = shard.costs_from_sizes(csr.cluster_sizes(), csr.cluster_peaks(), "both")
+    assert max(loads) <= sum(loads) / world + cost.max()  # the LPT bound

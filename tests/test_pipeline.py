@@ -42,3 +42,37 @@ def test_pipeline_equals_engine_and_oracle(gpu, chunk_bytes):
         np.testing.assert_array_equal(r["rep"], c_oracle.medoid(csr))
     one = engine.bin_mean(engine.DeviceBatch.from_host(csr)).to_host()
     np.testing.assert_array_equal(r["out_mz"], one["out_mz"])
+
+
+def _with_wide_overflow(csr, n_spec=40, n_peaks=700, seed=9):
+    """csr + one small cluster (n <= 64, <= 32,768 peaks) whose ~16k distinct
+    0.1-Da bins overflow the medoid wide kernel's 6,080: deferred at RUN time."""
+    from specpride_amd.csr import SpectraCSR
+
+    rng = np.random.default_rng(seed)
+    mz = np.sort(np.round(rng.uniform(100.0, 2000.0, (n_spec, n_peaks)), 5), axis=1).ravel()
+    inten = np.round(rng.uniform(1.0, 1000.0, mz.size), 2)
+    so = np.concatenate([csr.spec_off, csr.spec_off[-1] + n_peaks * np.arange(1, n_spec + 1)])
+    co = np.concatenate([csr.cluster_off, [csr.cluster_off[-1] + n_spec]])
+    S = n_spec
+    return SpectraCSR(co, so, np.concatenate([csr.mz, mz]), np.concatenate([csr.inten, inten]),
+                      np.concatenate([csr.prec_mz, np.full(S, 500.0)]), np.concatenate([csr.charge, np.full(S, 2)]),
+                      np.concatenate([csr.rt, np.zeros(S)]))
+
+
+@pytest.mark.gpu
+def test_pipeline_runtime_medoid_deferral_resolved_after_loop(gpu):
+    """A chunk whose medoid defers a cluster at run time (large path off in that
+    chunk) is re-run by the checked call after the overlapped loop; results equal
+    the oracle's (no device-wide sync inside the loop)."""
+    from oracle import c_oracle
+    from specpride_amd.pipeline import HostPipeline
+
+    csr = _with_wide_overflow(make_clusters_np(400, seed=31))
+    pipe = HostPipeline(chunk_bytes=16 * 60_000)
+    r = pipe.run(csr)
+    assert pipe.timing["chunks"] >= 3 and pipe.timing["redo_chunks"] == 1
+    np.testing.assert_array_equal(r["rep"], c_oracle.medoid(csr))
+    ref = c_oracle.bin_mean(csr)
+    for k in ("status", "out_off", "out_mz", "out_int"):
+        np.testing.assert_array_equal(r[k], ref[k], err_msg=k)

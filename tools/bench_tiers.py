@@ -77,24 +77,8 @@ def main():
         out["tier2_per_method"] = per
     # ---------------------------------------------------------------- tier 3
     from specpride_amd import average_spectrum_clustering as asc
-    from specpride_amd import mgf_native
     from specpride_amd import most_similar_representative as msr
-    from specpride_amd.synthetic import make_clusters_torch
-
-    def write_mgf(path, n_clusters, seed):
-        """A clustered MGF (file_formats.md:5-57) of the configs law, written by the
-        native writer: TITLE=cluster-<c>;mzspec:PXDSYN:synthetic:scan:<s>, PEPMASS,
-        CHARGE, RTINSECONDS, repr floats."""
-        t = make_clusters_torch(n_clusters, seed=seed)
-        h = {k: engine.to_host_array(t[k]) for k in ("cluster_off", "spec_off", "mz", "inten", "prec_mz", "charge",
-                                                      "rt")}
-        del t
-        torch.cuda.empty_cache()
-        owner = np.repeat(np.arange(n_clusters), np.diff(h["cluster_off"]))
-        titles = [f"cluster-{c};mzspec:PXDSYN:synthetic:scan:{s}" for s, c in enumerate(owner.tolist())]
-        mgf_native.write_records(path, mgf_native.STYLE_MEDOID, titles, h["spec_off"], h["mz"], h["inten"],
-                                 h["prec_mz"], h["charge"], h["rt"])
-        return int(len(owner)), int(h["spec_off"][-1])
+    from specpride_amd.synthetic import write_clustered_mgf as write_mgf
 
     clis = {"binning": lambda i, o: binning.main(["--mgf_file", i, "--out", o]),
             "average_spectrum_clustering": lambda i, o: asc.main([i, o, "--encodedclusters"]),
