@@ -24,7 +24,7 @@ namespace spx {
 #endif
 
 union FusedSmem {
-  BinRegSmem b;
+  BinHeadSmem b;
   MedoidRegSmem<MD_BLOCK, MR_UMAX, MD_KWMAX> m;
 };
 static_assert(BM_BLOCK == MD_BLOCK, "one workgroup shape for both bodies");
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(BM_BLOCK, SPX_FU_MINW) void bin_mean_medoid_kernel(
   const int64_t c = blockIdx.x;
   // bin-mean first: its phase A streams the cluster's m/z, which the medoid's
   // first pass then re-reads from cache
-  const int32_t st = bin_mean_reg_path(v, PB, L.b, c, out, prec_out, charge_out);
+  const int32_t st = bin_mean_head_path(v, PB, L.b, c, out, prec_out, charge_out);
   if (threadIdx.x == 0) {  // bin_mean_reg_kernel's hand-off, verbatim
     if (st != kNotHere) status[c] = st;
     if (st == kNotHere || st == kDeferred) striped_push(bm_rest, (int32_t)c);

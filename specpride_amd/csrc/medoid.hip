@@ -37,6 +37,9 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_MINW
 #define SPX_MD_MINW 7
 #endif
+#ifndef SPX_MD_MFMA
+#define SPX_MD_MFMA 1  // P4's pair counts on the matrix cores (FP4 Gram tiles), not AND + popcount
+#endif
 #ifndef SPX_MD_RECIP
 #define SPX_MD_RECIP 1  // P4's quotients from per-spectrum reciprocals (exact, md_dist_r)
 #endif
@@ -116,6 +119,23 @@ __device__ __forceinline__ int spectrum_of(const int32_t* soff, int n, int32_t k
     if (soff[mid] <= k) lo = mid; else hi = mid;
   }
   return lo;
+}
+
+typedef int md_i32x8 __attribute__((ext_vector_type(8)));
+typedef float md_f32x16 __attribute__((ext_vector_type(16)));
+
+// One 32-bin half of a 64-bin row word as an FP4 e2m1 MFMA operand (1.0 = nibble
+// 0b0010): lane half fh takes bins 32fh..32fh+31, dword g nibble p = bin 32fh + g + 4p
+// (the same k order for A and B, so the dot products are the bit-AND popcounts).
+__device__ __forceinline__ md_i32x8 md_frag4(uint64_t w, int fh) {
+  const uint32_t c = (uint32_t)(w >> (32 * fh));
+  md_i32x8 f;
+  f[0] = (int)((c << 1) & 0x22222222u);
+  f[1] = (int)(c & 0x22222222u);
+  f[2] = (int)((c >> 1) & 0x22222222u);
+  f[3] = (int)((c >> 2) & 0x22222222u);
+  f[4] = f[5] = f[6] = f[7] = 0;
+  return f;
 }
 
 // --------------------------------------------------------- small clusters
@@ -398,12 +418,61 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   __syncthreads();
   SPX_STAMP(4);
 
+  auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
+#if SPX_MD_MFMA
+  // P4 on the matrix cores: c_ij = |B_i ∩ B_j| = the Gram of the 0/1 rows, one
+  // 32 x 32 tile per wave -- (0,0) for n <= 32; (0,0), (0,1), (1,1) for n <= 64 --
+  // one v_mfma_f32_32x32x64_f8f6f4 per 64-bin row word (FP4 0/1 operands at unit
+  // scale: the f32 sums of <= 2^24 ones are the integer counts), then
+  // d_ij = 1 - c_ij / min(p_i, p_j) into the packed upper triangle
+  {
+    const int fr = lane & 31, fh = lane >> 5;
+    const int ntile = n > 32 ? 3 : 1;
+    const bool work = wid < ntile;  // wave-uniform
+    const int ta = wid == 2 ? 1 : 0, tb = wid == 0 ? 0 : 1;
+    md_f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+    if (work) {
+      const int ra = ta * 32 + fr, rb = tb * 32 + fr;
+      const unsigned long long* pa = L.u.a.rows + (ra < n ? ra : 0) * KW;
+      const unsigned long long* pb = L.u.a.rows + (rb < n ? rb : 0) * KW;
+      const unsigned long long ma = ra < n ? ~0ull : 0ull, mb = rb < n ? ~0ull : 0ull;
+      unsigned long long wa = pa[0] & ma, wb = pb[0] & mb;  // one word ahead
+      for (int w = 0; w < KW; ++w) {
+        const int wn = w + 1 < KW ? w + 1 : w;
+        const unsigned long long na = pa[wn] & ma, nb = pb[wn] & mb;
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(md_frag4(wa, fh), md_frag4(wb, fh), acc, 4, 4, 0, 0,
+                                                              0, 0);
+        wa = na;
+        wb = nb;
+      }
+    }
+    __syncthreads();  // rows dead: the distance matrix takes their place
+    if (work) {
+      // C/D layout (32x32): col = lane & 31, row = (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5)
+      const int j = tb * 32 + fr;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = ta * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
+        if (i <= j && j < n) {
+          const uint32_t cnt = (uint32_t)acc[q];
+#if SPX_MD_RECIP
+          L.u.d[row_start(i) + j - i] =
+              md_dist_r(cnt, L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
+#else
+          L.u.d[row_start(i) + j - i] = md_dist(cnt, L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
+#endif
+        }
+      }
+    }
+  }
+#else
   // P4: every pair i <= j of the row-major upper triangle (row i starts at
   // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
   // registers until the rows are dead
   constexpr int PPT = (MD_NMAX * (MD_NMAX + 1) / 2 + BLOCK - 1) / BLOCK;  // pairs per thread (9)
   const int NP = n * (n + 1) / 2;
-  auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
   uint32_t pc[PPT];
   int pij[PPT];
 #pragma unroll
@@ -437,6 +506,7 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
 #endif
     }
   }
+#endif
   __syncthreads();
   // D(a, b) of the reference's dense matrix: the upper triangle incl. the
   // diagonal, zeros below (most_similar_representative.py:91-93)
@@ -1008,8 +1078,6 @@ constexpr int MD_GR_PF = SPX_GR_PF;  // words in flight per lane (divides 8: KW 
 // 32-bin half word -> 4 dwords of 8 nibbles, 2 ops each).  Products are 1.0 or 0,
 // the f32 accumulation of at most 2^24 of them is exact, so the counts are the
 // integer ones.  Peak: the FP4 dense rate (~10 POPS), twice the i8 one.
-typedef int md_i32x8 __attribute__((ext_vector_type(8)));
-typedef float md_f32x16 __attribute__((ext_vector_type(16)));
 
 // Bit rows, row-major [npad][KW] -> word-major [KW][npad] (64 x 64-word tiles
 // through LDS: both sides coalesced), for the register Gram's loads.

@@ -121,19 +121,25 @@ def main():
         s = buf.view(-1, 8).cpu().numpy().astype(np.float64)
         sizes = np.diff(b.host_cluster_off)
         ph = {}
-        last = 5 if a.stamps_kernel == "bm" else 7
-        for k in range(1, last + 1):
-            ok = (s[:, k] > 0) & (s[:, k - 1] > 0)
+        last = 6 if a.stamps_kernel == "bm" else 7
+        # phases between consecutive stamps that the build records (a path may skip an index)
+        present = [k for k in range(last + 1) if (s[:, k] > 0).any()]
+        last = present[-1]
+        ph = {}
+        for k0, k1 in zip(present[:-1], present[1:]):
+            ok = (s[:, k1] > 0) & (s[:, k0] > 0)
             if ok.any():
-                ph[f"p{k - 1}->p{k}"] = round(float(np.mean(s[ok, k] - s[ok, k - 1])), 1)
+                ph[f"p{k0}->p{k1}"] = round(float(np.mean(s[ok, k1] - s[ok, k0])), 1)
         ok = (s[:, last] > 0) & (s[:, 0] > 0)
         ph["lifetime"] = round(float(np.mean(s[ok, last] - s[ok, 0])), 1)
         bands = {}
         for lo, hi in ((2, 10), (11, 25), (26, 40), (41, 50)):
-            m = ok & (sizes >= lo) & (sizes <= hi) & (s[:, last - 1] > 0)
+            m = ok & (sizes >= lo) & (sizes <= hi)
+            for k in present:
+                m &= s[:, k] > 0
             if m.any():
-                bands[f"n{lo}-{hi}"] = {f"p{k - 1}->p{k}": round(float(np.mean(s[m, k] - s[m, k - 1])), 1)
-                                        for k in range(1, last + 1)}
+                bands[f"n{lo}-{hi}"] = {f"p{k0}->p{k1}": round(float(np.mean(s[m, k1] - s[m, k0])), 1)
+                                        for k0, k1 in zip(present[:-1], present[1:])}
         span = (s[ok, last].max() - s[ok, 0].min())
         res["stamps"] = {"phases_cycles": ph, "by_size": bands, "span_cycles": span,
                          "cycles_per_cluster_per_cu": round(span * 256 / ok.sum(), 1)}
