@@ -1240,7 +1240,7 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
 #endif
           }
         }
-#if SPX_GR_TR
+#if SPX_GR_TR && !defined(SPX_DG_NOMIRROR)  // (diagnostic build: no mirrored entries, totals wrong by design)
         // the mirrored entries (j, i): through a wave-private 32 x 33 LDS tile so
         // that the lanes write consecutive columns of each row j (the direct
         // column store put every lane on its own cache line: 19% of the kernel)

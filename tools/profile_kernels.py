@@ -94,6 +94,22 @@ def main():
         md = engine.medoid(b)
         res["medoid_ms"] = timed(lambda: engine.medoid(b, out=md, check=False))
         res["medoid_digest"] = digest(md.rep)
+    if "cc" in which:  # the step as two concurrent streams: bin-mean on this one, medoid on a second
+        cbm, cmd = engine.bin_mean(b), engine.medoid(b)
+        s2 = torch.cuda.Stream()
+
+        def both():
+            ev = torch.cuda.Event()
+            ev.record(st)
+            s2.wait_event(ev)
+            engine.bin_mean(b, out=cbm)
+            engine.medoid(b, out=cmd, check=False, stream=s2)
+            ev2 = torch.cuda.Event()
+            ev2.record(s2)
+            st.wait_event(ev2)
+        res["concurrent_ms"] = timed(both)
+        off, mz, it = cbm.compact()
+        res["concurrent_digests"] = [digest(off, mz, it, cbm.status, cbm.prec, cbm.charge), digest(cmd.rep)]
     if "fu" in which:  # the fused step (spx_bin_mean_medoid): digests must equal bm's and md's
         fbm, fmd = engine.bin_mean_medoid(b)
         res["fused_ms"] = timed(lambda: engine.bin_mean_medoid(b, out_bm=fbm, out_md=fmd, check=False))
