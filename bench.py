@@ -269,15 +269,24 @@ def headline(args, rank, world, local, out):
     batch = engine.DeviceBatch.from_device(t)
     torch.cuda.synchronize()
 
-    # checked once, before timing: every cluster resolved by the launches the step makes
-    bm = engine.bin_mean(batch)
-    md = engine.medoid(batch, check=True)
+    # checked once, before timing: every cluster resolved by the launch the step makes, and
+    # the fused pass (spx_bin_mean_medoid: each cluster's bin-mean and medoid register
+    # bodies in one workgroup, then each method's leftover chain) equal to the two
+    # separate entry points, consensus peaks and representatives bit for bit
+    bm_sep = engine.bin_mean(batch)
+    md_sep = engine.medoid(batch, check=True)
+    bm, md = engine.bin_mean_medoid(batch, check=True)
     torch.cuda.synchronize()
     st = bm.status.cpu().numpy()[:batch.n_clusters]
     rep = md.rep.cpu().numpy()[:batch.n_clusters]
     if np.any(st != 0) or np.any(rep < 0):
         raise RuntimeError(f"unexpected statuses: bin-mean {np.unique(st)}, medoid min rep {rep.min()}")
     kept = int(bm.count[:batch.n_clusters].sum().item())
+    C = batch.n_clusters
+    same = (torch.equal(bm.count[:C], bm_sep.count[:C]) and torch.equal(md.rep[:C], md_sep.rep[:C]) and
+            all(torch.equal(a, b) for a, b in zip(bm.compact()[1:], bm_sep.compact()[1:])))
+    if not same:
+        raise RuntimeError("spx_bin_mean_medoid differs from spx_bin_mean + spx_medoid")
     large = engine.medoid_needs_large_path(batch) or bool(batch._ws.get("medoid_extra"))
     stream = torch.cuda.current_stream()
     first = batch.t["cluster_off"][:-1] if strong else None
@@ -286,7 +295,7 @@ def headline(args, rank, world, local, out):
     bufs = [(bm, md)]
     gat = None
     if world > 1:
-        bufs.append((engine.bin_mean(batch), engine.medoid(batch, check=False)))
+        bufs.append(engine.bin_mean_medoid(batch, check=False))
         gat = shard.StepGatherer(batch.n_clusters, rank, world, batch.device)
         total_c, total_p = gat.plan(kept)
 
@@ -297,8 +306,7 @@ def headline(args, rank, world, local, out):
         b, m = bufs[i]
         if inflight[i] is not None:
             stream.wait_event(inflight[i])  # this buffer's previous gather (step k-2) is done
-        engine.bin_mean(batch, out=b)
-        engine.medoid(batch, out=m, check=False)
+        engine.bin_mean_medoid(batch, out_bm=b, out_md=m, check=False)
         if gat is not None:
             ev = torch.cuda.Event()
             ev.record(stream)
@@ -340,8 +348,10 @@ def headline(args, rank, world, local, out):
 
     reps = max(3, args.steps)
     _lib.profile_enable(True)
-    bm_ms_ep = time_launches(lambda: engine.bin_mean(batch, out=bm), reps, stream)
-    md_ms_ep = time_launches(lambda: engine.medoid(batch, out=md, check=False), reps, stream)
+    bm_ms_ep = time_launches(lambda: engine.bin_mean(batch, out=bm_sep), reps, stream)
+    md_ms_ep = time_launches(lambda: engine.medoid(batch, out=md_sep, check=False), reps, stream)
+    fu_ms_ep = time_launches(lambda: engine.bin_mean_medoid(batch, out_bm=bm, out_md=md, check=False), reps, stream)
+    fu_k = kernel_ms("bin_mean_medoid_kernel")
     bm_ms = kernel_ms("bin_mean_reg_kernel")
     md_ms = kernel_ms("medoid_reg_kernel")
     _lib.profile_enable(False)
@@ -386,22 +396,18 @@ def headline(args, rank, world, local, out):
         out["config"]["rank_clusters"] = [int(len(p)) for p in parts]
     if assembled is not None:
         out["config"]["assembled_last_step"] = assembled
+    out["config"]["step"] = ("spx_bin_mean_medoid: one fused pass per cluster (bin-mean + medoid register bodies "
+                             "in one workgroup, then each method's leftover kernels); checked bit-identical to "
+                             "spx_bin_mean + spx_medoid before timing")
+    out["kernels"]["spx_bin_mean_medoid_ms"] = round(fu_ms_ep, 4)
+    out["kernels"]["bin_mean_medoid_kernel_ms"] = round(fu_k, 4)
     if rank == 0 and world == 1 and not args.no_extras:
-        # the same step through the fused entry point (spx_bin_mean_medoid: both register
-        # bodies per workgroup, then each method's leftover chain); results checked equal
-        fbm, fmd = engine.bin_mean_medoid(batch)
-        torch.cuda.synchronize()
-        same = bool(torch.equal(fbm.count[:batch.n_clusters], bm.count[:batch.n_clusters]) and
-                    torch.equal(fmd.rep[:batch.n_clusters], md.rep[:batch.n_clusters]))
-        _lib.profile_enable(True)
-        fu_ms = time_launches(lambda: engine.bin_mean_medoid(batch, out_bm=fbm, out_md=fmd, check=False), reps, stream)
-        fu_k = kernel_ms("bin_mean_medoid_kernel")
-        _lib.profile_enable(False)
-        out["fused_step"] = {"entry_point": "spx_bin_mean_medoid", "ms": round(fu_ms, 4),
-                             "clusters_per_s": round(batch.n_clusters / (fu_ms * 1e-3), 1),
-                             "fused_kernel_ms": round(fu_k, 4), "separate_ms": round(bm_ms_ep + md_ms_ep, 4),
-                             "results_equal_separate": same}
-        del fbm, fmd
+        # the same step through the two separate entry points (the two CLIs' calls)
+        sep_ms = time_launches(lambda: (engine.bin_mean(batch, out=bm_sep),
+                                        engine.medoid(batch, out=md_sep, check=False)), reps, stream)
+        out["separate_step"] = {"entry_points": "spx_bin_mean + spx_medoid", "ms": round(sep_ms, 4),
+                                "clusters_per_s": round(batch.n_clusters / (sep_ms * 1e-3), 1),
+                                "fused_ms_per_step": round(elapsed / args.steps * 1e3, 4)}
         # gap-average consensus on the same resident batch (average_spectrum_clustering.py:26-148)
         ga = engine.gap_average(batch)
         torch.cuda.synchronize()
@@ -417,7 +423,7 @@ def headline(args, rank, world, local, out):
                                                    consensus_bytes(batch, gkept), ga_ms,
                                                    load_pmc_traffic("gap_average_lds_kernel", batch), kernel_ms=ga_k)}
         del ga
-    del bm, md, bufs, batch, t
+    del bm, md, bm_sep, md_sep, bufs, batch, t
     torch.cuda.empty_cache()
 
 

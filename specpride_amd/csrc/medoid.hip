@@ -40,6 +40,9 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_MFMA
 #define SPX_MD_MFMA 1  // P4's pair counts on the matrix cores (FP4 Gram tiles), not AND + popcount
 #endif
+#ifndef SPX_MD_MFMA_NMIN
+#define SPX_MD_MFMA_NMIN 32  // ... for clusters of more spectra than this
+#endif
 #ifndef SPX_MD_RECIP
 #define SPX_MD_RECIP 1  // P4's quotients from per-spectrum reciprocals (exact, md_dist_r)
 #endif
@@ -419,7 +422,15 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   SPX_STAMP(4);
 
   auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
-#if SPX_MD_MFMA
+  // the matrix cores for the register kernel's P4; the wide kernel (up to 95 row words,
+  // 128 VGPRs) keeps the AND + popcount pairs: there the sequential MFMA chain measured
+  // slower (600-peak spectra, medoid_shapes: 1.12 -> 1.37 ms)
+  // and only for clusters of more than SPX_MD_MFMA_NMIN spectra: below, one wave holds
+  // the one 32 x 32 tile and its epilogue while the pairs spread over the whole workgroup
+  // (stamps, configs[4]: P4 n 41-50 14.4k -> 11.7k cycles, n 11-25 5.7k -> 8.7k)
+  bool mfma_p4 = false;
+  if constexpr (SPX_MD_MFMA && BLOCK == MD_BLOCK) mfma_p4 = n > SPX_MD_MFMA_NMIN;  // uniform
+  if (mfma_p4) {
   // P4 on the matrix cores: c_ij = |B_i ∩ B_j| = the Gram of the 0/1 rows, one
   // 32 x 32 tile per wave -- (0,0) for n <= 32; (0,0), (0,1), (1,1) for n <= 64 --
   // one v_mfma_f32_32x32x64_f8f6f4 per 64-bin row word (FP4 0/1 operands at unit
@@ -467,46 +478,46 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       }
     }
   }
-#else
-  // P4: every pair i <= j of the row-major upper triangle (row i starts at
-  // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
-  // registers until the rows are dead
-  constexpr int PPT = (MD_NMAX * (MD_NMAX + 1) / 2 + BLOCK - 1) / BLOCK;  // pairs per thread (9)
-  const int NP = n * (n + 1) / 2;
-  uint32_t pc[PPT];
-  int pij[PPT];
+  } else {
+    // P4: every pair i <= j of the row-major upper triangle (row i starts at
+    // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
+    // registers until the rows are dead
+    constexpr int PPT = (MD_NMAX * (MD_NMAX + 1) / 2 + BLOCK - 1) / BLOCK;  // pairs per thread (9)
+    const int NP = n * (n + 1) / 2;
+    uint32_t pc[PPT];
+    int pij[PPT];
 #pragma unroll
-  for (int q = 0; q < PPT; ++q) {
-    const int p = tid + q * BLOCK;
-    pc[q] = 0u;
-    pij[q] = -1;
-    if (p < NP) {
-      const float b2 = 2.0f * n + 1.0f;
-      int i = (int)((b2 - sqrtf(b2 * b2 - 8.0f * (float)p)) * 0.5f);
-      i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
-      while (i > 0 && row_start(i) > p) --i;
-      while (i + 1 < n && row_start(i + 1) <= p) ++i;
-      const int j = i + (p - row_start(i));
-      uint32_t cnt = 0;
-      for (int w = 0; w < KW; ++w) cnt += (uint32_t)__popcll(L.u.a.rows[i * KW + w] & L.u.a.rows[j * KW + w]);
-      pc[q] = cnt;
-      pij[q] = i << 8 | j;
+    for (int q = 0; q < PPT; ++q) {
+      const int p = tid + q * BLOCK;
+      pc[q] = 0u;
+      pij[q] = -1;
+      if (p < NP) {
+        const float b2 = 2.0f * n + 1.0f;
+        int i = (int)((b2 - sqrtf(b2 * b2 - 8.0f * (float)p)) * 0.5f);
+        i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+        while (i > 0 && row_start(i) > p) --i;
+        while (i + 1 < n && row_start(i + 1) <= p) ++i;
+        const int j = i + (p - row_start(i));
+        uint32_t cnt = 0;
+        for (int w = 0; w < KW; ++w) cnt += (uint32_t)__popcll(L.u.a.rows[i * KW + w] & L.u.a.rows[j * KW + w]);
+        pc[q] = cnt;
+        pij[q] = i << 8 | j;
+      }
     }
-  }
-  __syncthreads();  // rows dead: the distance matrix takes their place
+    __syncthreads();  // rows dead: the distance matrix takes their place
 #pragma unroll
-  for (int q = 0; q < PPT; ++q) {
-    if (pij[q] >= 0) {
-      const int i = pij[q] >> 8, j = pij[q] & 0xff;
+    for (int q = 0; q < PPT; ++q) {
+      if (pij[q] >= 0) {
+        const int i = pij[q] >> 8, j = pij[q] & 0xff;
 #if SPX_MD_RECIP
-      L.u.d[row_start(i) + j - i] =
-          md_dist_r(pc[q], L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
+        L.u.d[row_start(i) + j - i] =
+            md_dist_r(pc[q], L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
 #else
-      L.u.d[row_start(i) + j - i] = md_dist(pc[q], L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
+        L.u.d[row_start(i) + j - i] = md_dist(pc[q], L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
 #endif
+      }
     }
   }
-#endif
   __syncthreads();
   // D(a, b) of the reference's dense matrix: the upper triangle incl. the
   // diagonal, zeros below (most_similar_representative.py:91-93)
