@@ -296,7 +296,8 @@ def headline(args, rank, world, local, out):
     gat = None
     if world > 1:
         bufs.append(engine.bin_mean_medoid(batch, check=False))
-        gat = shard.StepGatherer(batch.n_clusters, rank, world, batch.device)
+        gat = shard.StepGatherer(batch.n_clusters, rank, world, batch.device,
+                                 wire_max_count=max(1, int(batch.info.max_cluster_spectra)))
         total_c, total_p = gat.plan(kept)
 
     inflight = [None] * len(bufs)  # per buffer: the event of the gather reading it
@@ -322,6 +323,8 @@ def headline(args, rank, world, local, out):
         gat.stream.synchronize()
     barrier(world)
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    if gat is not None and gat.check() != 0:
+        raise RuntimeError(f"rank {rank}: {gat.check()} consensus peaks the gather wire format could not carry")
     total_clusters = (args.clusters if strong else world * batch.n_clusters)
     value = total_clusters * args.steps / elapsed
 
@@ -390,6 +393,9 @@ def headline(args, rank, world, local, out):
     if gat is not None:
         out["config"]["gathered_clusters_per_step"] = total_c
         out["config"]["gathered_peaks_per_step"] = total_p
+        out["config"]["gather_wire"] = (f"f32 bin sums + {gat.wire}-byte counts, rebuilt to f64 on rank 0 "
+                                        "(csrc/wire.hip)" if gat.wire else "f64 peaks")
+        out["config"]["rank0_inbound_bytes_per_step"] = gat.wire_bytes_per_step() if rank == 0 else None
     if loads is not None:
         out["config"]["rank_cost_share"] = [round(float(x / loads.sum()), 5) for x in loads]
         out["config"]["cost_max_over_min"] = round(float(loads.max() / max(loads.min(), 1.0)), 5)

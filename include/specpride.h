@@ -20,6 +20,7 @@
  *   spx_best_score   <- src/best_spectrum.py:67-100  get_best_representative
  *                       (called per cluster from best_spectrum():170-174)
  *   spx_compact_peaks   (packing helper for the shims' output writers)
+ *   spx_wire_pack / spx_wire_unpack  (9-byte consensus peaks for the multi-GPU gather to rank 0)
  *   spx_copy_h2d / spx_copy_d2h  (host transfers of pageable batches: the reference
  *                       holds its spectra in host memory, binning.py:122-167)
  *
@@ -234,6 +235,18 @@ int spx_best_score(const spx_csr *csr, const double *score, const int64_t *rank,
  * for k < count[c]; out_off is the exclusive prefix sum of count (device array [C+1]). */
 int spx_compact_peaks(const spx_csr *csr, const spx_peaks_out *src, const int64_t *out_off,
                       double *dst_mz, double *dst_inten, void *stream);
+
+/* Wire format of the multi-GPU gather (csrc/wire.hip; shard.StepGatherer): bin-mean
+ * consensus peaks (mz, inten)[n] (dense, device) -> mi[2n] (f32 bin sums M, I) and
+ * count[n] (count_bytes = 1 or 2 bytes each, max_count <= 255 or <= 65,535: at least the
+ * batch's largest cluster size), 9 or 10 bytes a peak instead of 16; spx_wire_unpack
+ * rebuilds the doubles bit for bit (mz = M == 0 ? NaN : f64(M)/c, inten = f64(I)/c,
+ * binning.py:211-218).  A peak no count <= max_count rebuilds exactly (not a bin-mean
+ * output) is sent as NaN and counted in *n_fail (device int32, zeroed by the caller). */
+int spx_wire_pack(const double *mz, const double *inten, int64_t n, int32_t max_count, float *mi, void *count,
+                  int32_t count_bytes, int32_t *n_fail, void *stream);
+int spx_wire_unpack(const float *mi, const void *count, int32_t count_bytes, int64_t n, double *mz, double *inten,
+                    void *stream);
 
 /* Host <-> device copies of batches in PAGEABLE host memory (SURVEY.md §8(d) tier 2).
  * The bytes are staged through a process-wide pool of pinned buffers by several host

@@ -66,7 +66,7 @@ class SpxCosineParams(ctypes.Structure):
 # every symbol include/specpride.h declares (checked by tests/test_host.py)
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_bin_mean_stage", "spx_gap_average_workspace_size", "spx_gap_average",
             "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_bin_mean_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
-            "spx_compact_peaks", "spx_copy_h2d", "spx_copy_d2h",
+            "spx_compact_peaks", "spx_wire_pack", "spx_wire_unpack", "spx_copy_h2d", "spx_copy_d2h",
             "spx_abi_version", "spx_last_error", "spx_profile_enable", "spx_profile_read",
             "spx_medoid_gram_operand_bits"]
 
@@ -138,6 +138,8 @@ def lib():
     L.spx_medoid_needs_large_path.argtypes = [_p, _p, _i64]
     L.spx_medoid.argtypes = [_p, _p, _p, _p, _p, _sz, _p]
     L.spx_compact_peaks.argtypes = [_p, _p, _p, _p, _p, _p]
+    L.spx_wire_pack.argtypes = [_p, _p, _i64, _i32, _p, _p, _i32, _p, _p]
+    L.spx_wire_unpack.argtypes = [_p, _p, _i32, _i64, _p, _p, _p]
     L.spx_xcorr_distance.argtypes = [_p, _p, _p, _i64, _p, _p]
     L.spx_binned_cosine_workspace_size.restype = _sz
     L.spx_binned_cosine_workspace_size.argtypes = [_i64, _i64]

@@ -31,6 +31,7 @@
 #include "medoid.hip"
 #include "fused.hip"
 #include "transfer.hip"
+#include "wire.hip"
 
 #ifndef SPX_MD_GRIDY
 #define SPX_MD_GRIDY 128u  // deferred clusters the large path's grid-stride passes take at a time (32: configs[3] medoid 3.02 ms, 128: 2.92, 512: 2.92)
@@ -919,6 +920,45 @@ extern "C" int spx_compact_peaks(const spx_csr* csr, const spx_peaks_out* src, c
   hipLaunchKernelGGL(spx::compact_kernel, dim3(g), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), view(csr),
                      src->mz, src->inten, src->count, out_off, dst_mz, dst_inten);
   return check_launch("compact_kernel");
+}
+
+// ------------------------------------------------------------ gather wire format
+namespace {
+unsigned wire_grid(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192)); }
+}  // namespace
+
+extern "C" int spx_wire_pack(const double* mz, const double* inten, int64_t n, int32_t max_count, float* mi,
+                             void* count, int32_t count_bytes, int32_t* n_fail, void* stream) {
+  if (n < 0 || (n > 0 && (!mz || !inten || !mi || !count || !n_fail)))
+    return fail(SPX_EINVAL, "spx_wire_pack: null argument");
+  if (!(count_bytes == 1 || count_bytes == 2) || max_count < 1 || max_count > (count_bytes == 1 ? 255 : 65535))
+    return fail(SPX_EINVAL, "spx_wire_pack: count_bytes must be 1 (max_count <= 255) or 2 (<= 65535)");
+  if (n == 0) return SPX_SUCCESS;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  float2* o = reinterpret_cast<float2*>(mi);
+  if (count_bytes == 1)
+    hipLaunchKernelGGL(spx::wire_pack_kernel<uint8_t>, dim3(wire_grid(n)), dim3(256), 0, s, mz, inten, n,
+                       (uint32_t)max_count, o, static_cast<uint8_t*>(count), n_fail);
+  else
+    hipLaunchKernelGGL(spx::wire_pack_kernel<uint16_t>, dim3(wire_grid(n)), dim3(256), 0, s, mz, inten, n,
+                       (uint32_t)max_count, o, static_cast<uint16_t*>(count), n_fail);
+  return check_launch("wire_pack_kernel");
+}
+
+extern "C" int spx_wire_unpack(const float* mi, const void* count, int32_t count_bytes, int64_t n, double* mz,
+                               double* inten, void* stream) {
+  if (n < 0 || (n > 0 && (!mz || !inten || !mi || !count))) return fail(SPX_EINVAL, "spx_wire_unpack: null argument");
+  if (!(count_bytes == 1 || count_bytes == 2)) return fail(SPX_EINVAL, "spx_wire_unpack: count_bytes must be 1 or 2");
+  if (n == 0) return SPX_SUCCESS;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float2* v = reinterpret_cast<const float2*>(mi);
+  if (count_bytes == 1)
+    hipLaunchKernelGGL(spx::wire_unpack_kernel<uint8_t>, dim3(wire_grid(n)), dim3(256), 0, s, v,
+                       static_cast<const uint8_t*>(count), n, mz, inten);
+  else
+    hipLaunchKernelGGL(spx::wire_unpack_kernel<uint16_t>, dim3(wire_grid(n)), dim3(256), 0, s, v,
+                       static_cast<const uint16_t*>(count), n, mz, inten);
+  return check_launch("wire_unpack_kernel");
 }
 
 // ------------------------------------------------------------ host transfers

@@ -513,6 +513,52 @@ def bin_mean_medoid(batch: DeviceBatch, minimum=100.0, maximum=2000.0, binsize=0
     return out_bm, out_md
 
 
+def wire_count_bytes(max_count: int) -> int:
+    """Bytes per peak count of the gather wire format for clusters of <= max_count
+    spectra: 1 (<= 255) or 2 (<= 65,535); 0 = the compact format does not apply."""
+    return 1 if max_count <= 255 else (2 if max_count <= 65535 else 0)
+
+
+def wire_pack(mz, inten, max_count: int, stream=None, mi=None, cnt=None, n_fail=None):
+    """spx_wire_pack: dense bin-mean consensus peaks (f64 device tensors) -> the gather's
+    wire format, (mi float32 [2n] = the f32 bin sums M, I; cnt uint8/int16 [n];
+    n_fail int32 [1], peaks no count <= max_count rebuilds).  Enqueued on ``stream``;
+    the buffers may be passed in (reused across steps)."""
+    import torch
+
+    n = int(mz.numel())
+    cb = wire_count_bytes(max_count)
+    if cb == 0:
+        raise ValueError("wire_pack: clusters past 65,535 spectra need the f64 format")
+    dev = mz.device
+    if mi is None or mi.numel() < 2 * n:
+        mi = torch.empty(max(2 * n, 2), dtype=torch.float32, device=dev)
+    if cnt is None or cnt.numel() < n:
+        cnt = torch.empty(max(n, 1), dtype=torch.uint8 if cb == 1 else torch.int16, device=dev)
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    if n_fail is None:
+        n_fail = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.check(_lib.lib().spx_wire_pack(_ptr(mz), _ptr(inten), n, int(max_count), _ptr(mi), _ptr(cnt), cb,
+                                        _ptr(n_fail), _stream_handle(st)), "spx_wire_pack")
+    return mi[:2 * n], cnt[:n], n_fail
+
+
+def wire_unpack(mi, cnt, mz=None, inten=None, stream=None):
+    """spx_wire_unpack: the wire format back to the f64 consensus peaks, bit for bit."""
+    import torch
+
+    n = int(cnt.numel())
+    dev = cnt.device
+    if mz is None:
+        mz = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    if inten is None:
+        inten = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    _lib.check(_lib.lib().spx_wire_unpack(_ptr(mi), _ptr(cnt), cnt.element_size(), n, _ptr(mz), _ptr(inten),
+                                          _stream_handle(st)), "spx_wire_unpack")
+    return mz[:n], inten[:n]
+
+
 def xcorr_distance(batch: DeviceBatch, pairs, tolerance=0.1, stream=None):
     """1 - xcorr prescore (most_similar_representative.py:13-19) for (global
     spectrum index) pairs; returns a device f64 tensor."""

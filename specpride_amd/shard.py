@@ -162,11 +162,22 @@ class StepGatherer:
     peer's shard into buffers of its own, kept in :attr:`recv` (reordering into
     global cluster order is a host-side index, not part of the device pass).  The
     per-rank cluster and kept-peak counts are exchanged once (:meth:`plan`).
-    On a CPU group (``gloo``, the test suite) the stream and events are skipped
-    and the P2P ops are the same."""
 
-    def __init__(self, n_clusters: int, rank: int, world: int, device, group=None):
+    On a GPU group, with ``wire_max_count`` (the largest cluster size, <= 65,535), the
+    peaks travel in the wire format of ``csrc/wire.hip``: the f32 bin sums and a 1- or
+    2-byte count, 9-10 bytes a peak instead of 16, and rank 0 rebuilds the f64 peaks
+    bit for bit on its gather stream (engine.wire_pack / wire_unpack); counts and
+    representatives travel as int32.  The link into rank 0 is what bounds a
+    strong-scaled step, so that is 1.6-1.8x less time on it.  :meth:`check` reads
+    the senders' pack-failure counters (0 for bin-mean output) after a run.
+    On a CPU group (``gloo``, the test suite) the stream and events are skipped,
+    the peaks travel as f64 and the P2P ops are the same."""
+
+    def __init__(self, n_clusters: int, rank: int, world: int, device, group=None, wire_max_count=None,
+                 wire_ops=None):
         import torch
+
+        from . import engine
 
         self.rank, self.world, self.n, self.group = rank, world, int(n_clusters), group
         self.dev = torch.device(device)
@@ -175,6 +186,14 @@ class StepGatherer:
         self.recv = {}
         self.recv_sizes = None
         self.send_peaks = 0
+        # (pack, unpack) with engine.wire_pack / wire_unpack's signatures: the HIP kernels
+        # on a GPU group; a CPU test passes a model of them to drive the same protocol
+        self.wire_ops = wire_ops or ((engine.wire_pack, engine.wire_unpack) if self.cuda else None)
+        cb = engine.wire_count_bytes(int(wire_max_count)) if wire_max_count else 0
+        self.wire = cb if self.wire_ops else 0  # bytes per peak count on the wire; 0 = f64 peaks
+        self._wire_bufs = {}  # reused per step: the sender's pack outputs, rank 0's wire receive buffers
+        self.n_fail = torch.zeros(1, dtype=torch.int32, device=self.dev) if self.wire else None
+        self.wire_max = int(wire_max_count) if self.wire else 0
 
     def plan(self, kept_peaks: int):
         """Exchange the (fixed) per-rank cluster and kept-peak counts once, so
@@ -183,12 +202,29 @@ class StepGatherer:
         import torch
         import torch.distributed as dist
 
-        sizes = torch.tensor([self.n, int(kept_peaks)], dtype=torch.int64, device=self.dev)
+        sizes = torch.tensor([self.n, int(kept_peaks), self.wire_max], dtype=torch.int64, device=self.dev)
         allsz = [torch.empty_like(sizes) for _ in range(self.world)]
         dist.all_gather(allsz, sizes, group=self.group)
-        self.recv_sizes = [tuple(int(v) for v in t.cpu()) for t in allsz]
+        got = [tuple(int(v) for v in t.cpu()) for t in allsz]
+        self.recv_sizes = [g[:2] for g in got]
         self.send_peaks = int(kept_peaks)
+        if self.wire:  # one count width for every rank: the largest cluster anywhere
+            from . import engine
+
+            self.wire_max = max(g[2] for g in got)
+            self.wire = engine.wire_count_bytes(self.wire_max) if min(g[2] for g in got) > 0 else 0
         return sum(x[0] for x in self.recv_sizes), sum(x[1] for x in self.recv_sizes)
+
+    def wire_bytes_per_step(self) -> int:
+        """Bytes rank 0 receives per step (all peers)."""
+        per_peak = 8 + self.wire if self.wire else 16
+        per_cluster = 8 if self.wire else 16
+        return sum(c * per_cluster + p * per_peak for c, p in self.recv_sizes[1:])
+
+    def check(self) -> int:
+        """Pack failures of this rank's sends so far (synchronises; 0 unless the peaks
+        were not bin-mean output)."""
+        return int(self.n_fail.item()) if self.wire else 0
 
     def launch(self, bm, rep, done_event=None, first=None):
         """Enqueue the gather of one step's results (consensus ``bm`` with
@@ -205,35 +241,64 @@ class StepGatherer:
         import torch
         import torch.distributed as dist
 
+        from . import engine
+
         ctx = torch.cuda.stream(self.stream) if self.cuda else contextlib.nullcontext()
+        idt = torch.int32 if self.wire else torch.int64
         with ctx:
             if self.cuda and done_event is not None:
                 self.stream.wait_event(done_event)
-            if first is not None:
-                r = rep[:self.n]
-                rep = torch.where(r >= 0, r - first[:self.n], r)
             if self.rank == 0:
                 ops = []
                 for r in range(1, self.world):
                     c_r, p_r = self.recv_sizes[r]
                     bufs = self.recv.get(r)
                     if bufs is None:
-                        bufs = (torch.empty(max(c_r, 1), dtype=torch.int64, device=self.dev),
-                                torch.empty(max(c_r, 1), dtype=torch.int64, device=self.dev),
+                        bufs = (torch.empty(max(c_r, 1), dtype=idt, device=self.dev),
+                                torch.empty(max(c_r, 1), dtype=idt, device=self.dev),
                                 torch.empty(max(p_r, 1), dtype=torch.float64, device=self.dev),
                                 torch.empty(max(p_r, 1), dtype=torch.float64, device=self.dev))
                         self.recv[r] = bufs
-                    ops += [dist.P2POp(dist.irecv, b, r, group=self.group) for b in bufs]
+                    if self.wire:
+                        wb = self._wire_bufs.get(r)
+                        if wb is None:
+                            wb = (torch.empty(max(2 * p_r, 2), dtype=torch.float32, device=self.dev),
+                                  torch.empty(max(p_r, 1), dtype=torch.uint8 if self.wire == 1 else torch.int16,
+                                              device=self.dev))
+                            self._wire_bufs[r] = wb
+                        ops += [dist.P2POp(dist.irecv, b, r, group=self.group) for b in (bufs[0], bufs[1]) + wb]
+                    else:
+                        ops += [dist.P2POp(dist.irecv, b, r, group=self.group) for b in bufs]
             else:
+                if first is not None:
+                    r0 = rep[:self.n]
+                    rep = torch.where(r0 >= 0, r0 - first[:self.n], r0)
                 # device-side compaction of this rank's consensus peaks (count known: no sync)
                 _, dmz, dint = bm.compact(stream=self.stream, total=self.send_peaks)
                 one = lambda x: x if x.numel() else torch.zeros(1, dtype=x.dtype, device=x.device)  # noqa: E731
-                ops = [dist.P2POp(dist.isend, one(bm.count[:self.n].contiguous()), 0, group=self.group),
-                       dist.P2POp(dist.isend, one(rep[:self.n].contiguous()), 0, group=self.group),
-                       dist.P2POp(dist.isend, one(dmz), 0, group=self.group),
-                       dist.P2POp(dist.isend, one(dint), 0, group=self.group)]
+                cnt = bm.count[:self.n].to(idt).contiguous()
+                rr = rep[:self.n].to(idt).contiguous()
+                if self.wire:
+                    wb = self._wire_bufs.get("send")
+                    mi, wc, _ = self.wire_ops[0](dmz, dint, self.wire_max, stream=self.stream,
+                                                 mi=wb[0] if wb else None, cnt=wb[1] if wb else None,
+                                                 n_fail=self.n_fail)
+                    self._wire_bufs["send"] = (mi, wc)
+                    payload = (cnt, rr, mi, wc)
+                else:
+                    payload = (cnt, rr, dmz, dint)
+                if self.wire and payload[2].numel() == 0:  # no peaks: rank 0 posts 2 floats, 1 count
+                    payload = payload[:2] + (torch.zeros(2, dtype=torch.float32, device=self.dev), payload[3])
+                ops = [dist.P2POp(dist.isend, one(x), 0, group=self.group) for x in payload]
             for q in (dist.batch_isend_irecv(ops) if ops else []):
                 q.wait()
+            if self.rank == 0 and self.wire:
+                for r in range(1, self.world):  # rank 0's rebuild of the f64 peaks, on the gather stream
+                    p_r = self.recv_sizes[r][1]
+                    if p_r:
+                        mi, wc = self._wire_bufs[r]
+                        b = self.recv[r]
+                        self.wire_ops[1](mi[:2 * p_r], wc[:p_r], b[2], b[3], stream=self.stream)
             if not self.cuda:
                 return None
             ev = torch.cuda.Event()

@@ -190,7 +190,7 @@ class _OracleConsensus:
         return self._off, self._mz, self._int
 
 
-def _strong_worker(rank, world, port, q):
+def _strong_worker(rank, world, port, q, wire=False):
     from oracle import c_oracle
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -203,33 +203,44 @@ def _strong_worker(rank, world, port, q):
         bm = _OracleConsensus(c_oracle.bin_mean(sub))
         rep = torch.from_numpy(c_oracle.medoid(sub))
         first = torch.from_numpy(sub.cluster_off[:-1])
-        gat = shard.StepGatherer(sub.n_clusters, rank, world, "cpu")
+        if wire:  # the GPU path's wire format, with the numpy model of the kernels
+            import wire_model
+
+            gat = shard.StepGatherer(sub.n_clusters, rank, world, "cpu", wire_ops=wire_model.torch_ops(),
+                                     wire_max_count=int(sub.cluster_sizes().max()))
+        else:
+            gat = shard.StepGatherer(sub.n_clusters, rank, world, "cpu")
         gat.plan(int(bm.count.sum()))
         for _ in range(2):  # two steps through the same receive buffers
             assert gat.launch(bm, rep, first=first) is None
         if rank == 0:
             own_member = torch.where(rep >= 0, rep - first, rep)
             q.put((gat.assemble(parts, csr.cluster_off, bm, own_member), loads.tolist(),
-                   [len(p) for p in parts]))
+                   [len(p) for p in parts], gat.wire, gat.check()))
+        else:
+            assert gat.check() == 0
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_strong_partition_gather_equals_world1(world):
+@pytest.mark.parametrize("world,wire", [(2, False), (3, False), (2, True), (3, True)])
+def test_strong_partition_gather_equals_world1(world, wire):
     """bench.py --scaling strong at world 2/3 under gloo: the size-balanced LPT split
     of ONE batch (shard.strong_partition), per-rank compute on the rank's clusters,
     the per-step gather with member-index representatives, and rank 0's reassembly
-    in global order (StepGatherer.assemble) give exactly the world-1 results."""
+    in global order (StepGatherer.assemble) give exactly the world-1 results -- with the
+    peaks as f64 (CPU groups) and in the GPU path's 9-byte wire format (f32 bin sums +
+    counts, csrc/wire.hip; its numpy model here), rebuilt bit for bit on rank 0."""
     from oracle import c_oracle
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_strong_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_strong_worker, args=(r, world, port, q, wire)) for r in range(world)]
     for p in procs:
         p.start()
-    got, loads, sizes = q.get(timeout=240)
+    got, loads, sizes, wbytes, n_fail = q.get(timeout=240)
+    assert wbytes == (1 if wire else 0) and n_fail == 0
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -755,3 +755,55 @@ def test_medoid_large_path_row_widths(gpu):
     ref_rep, ref_tot = c_oracle.medoid(csr, with_totals=True)
     np.testing.assert_array_equal(rep, ref_rep)
     np.testing.assert_array_equal(tot, ref_tot)
+
+
+# ------------------------------------------------------- gather wire format
+def _wire_roundtrip(mz, it, max_count):
+    import torch
+
+    dev = torch.device("cuda:0")
+    dmz = torch.as_tensor(np.ascontiguousarray(mz), device=dev)
+    dit = torch.as_tensor(np.ascontiguousarray(it), device=dev)
+    mi, cnt, n_fail = engine.wire_pack(dmz, dit, max_count)
+    rmz, rit = engine.wire_unpack(mi, cnt)
+    torch.cuda.synchronize()
+    return rmz.cpu().numpy(), rit.cpu().numpy(), cnt.cpu().numpy(), int(n_fail.item())
+
+
+def test_gather_wire_format_rebuilds_bin_mean_bits(gpu):
+    """spx_wire_pack / spx_wire_unpack (the multi-GPU gather's 9-10 byte peaks) on
+    bin-mean consensus peaks: every peak rebuilt bit for bit -- a NaN m/z of a zero m/z
+    sum (binning.py:216; minimum below 0 and peaks at m/z 0), infinite intensity sums,
+    1-byte counts (clusters <= 255) and 2-byte counts (a 300-spectrum cluster) -- and a
+    value that no bin-mean produces reported in n_fail."""
+    base = make_clusters_np(200, seed=61)
+    rng = np.random.default_rng(3)
+    extra = []
+    for n, lo in ((4, -1.0), (300, 100.0)):  # zero-m/z bins; a cluster past 255 spectra
+        cl = []
+        tmpl = np.sort(np.round(rng.uniform(100.0, 900.0, 60), 5))  # every bin reaches the quorum
+        for s in range(n):
+            mzv = np.round(tmpl + rng.normal(0.0, 0.002, 60), 5) if s % 2 else tmpl.copy()
+            mzv = np.sort(mzv)
+            if lo < 0:
+                mzv = np.concatenate([[0.0, 0.0], mzv])
+            itv = np.round(rng.uniform(1.0, 500.0, len(mzv)), 2)
+            if s == 1 and lo < 0:
+                itv[1] = np.inf  # the zero-m/z bin's contribution: an infinite intensity sum
+            cl.append({"m/z array": mzv, "intensity array": itv, "precursor mz": 500.0, "precursor charge": 2})
+        extra.append(cl)
+    ex = SpectraCSR.from_clusters(extra)
+    for csr, kw in ((base, {}), (ex, dict(minimum=-1.0))):
+        ref = c_oracle.bin_mean(csr, **kw)
+        got = _bin_mean(csr, **kw)
+        assert_bin_mean_equal(got, ref)
+        mz, it = got["out_mz"], got["out_int"]
+        cmax = int(csr.cluster_sizes().max())
+        rmz, rit, cnt, n_fail = _wire_roundtrip(mz, it, cmax)
+        assert n_fail == 0
+        assert cnt.dtype == (np.uint8 if cmax <= 255 else np.int16)
+        np.testing.assert_array_equal(rmz.view(np.int64), mz.view(np.int64))
+        np.testing.assert_array_equal(rit.view(np.int64), it.view(np.int64))
+    assert np.isnan(got["out_mz"]).any() and np.isinf(got["out_int"]).any()
+    _, _, _, n_fail = _wire_roundtrip(np.array([np.pi, 100.25]), np.array([np.e, 3.5]), 50)
+    assert n_fail == 1

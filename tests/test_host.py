@@ -222,3 +222,26 @@ def test_native_decimal_parse_matches_python_float(tmp_path):
     assert np.array_equal(flat["inten"].view(np.int64), it.view(np.int64))
     prec = np.array([s["precursor mz"] for s in ref])
     assert np.array_equal(flat["prec_mz"].view(np.int64), prec.view(np.int64))
+
+
+def test_gather_wire_format_model_rebuilds_bin_mean_bits():
+    """The gather's wire format (csrc/wire.hip): every bin-mean consensus peak of the
+    oracle -- mean = f64(f32 sum) / count, binning.py:198-218 -- is carried by f32
+    sums and a count <= the cluster size, and rebuilt bit for bit (incl. the NaN m/z of
+    a zero m/z sum, :216); the GPU kernels are checked against the same property in
+    tests/test_gpu_parity.py."""
+    import wire_model
+    from oracle import c_oracle
+
+    csr = make_clusters_np(400, seed=19)
+    r = c_oracle.bin_mean(csr)
+    mz, it = r["out_mz"], r["out_int"]
+    cmax = int(csr.cluster_sizes().max())
+    M, I, C = wire_model.pack(mz, it, cmax)
+    assert np.all(C > 0) and C.max() <= cmax
+    mz2, it2 = wire_model.unpack(M, I, C)
+    np.testing.assert_array_equal(mz2.view(np.int64)[~np.isnan(mz)], mz.view(np.int64)[~np.isnan(mz)])
+    np.testing.assert_array_equal(it2.view(np.int64), it.view(np.int64))
+    # a value that is no f64 quotient of an f32 sum by a small count is not carried
+    M, I, C = wire_model.pack(np.array([np.pi]), np.array([np.e]), 50)
+    assert C[0] == 0
