@@ -266,7 +266,9 @@ class StepGatherer:
                                   torch.empty(max(p_r, 1), dtype=torch.uint8 if self.wire == 1 else torch.int16,
                                               device=self.dev))
                             self._wire_bufs[r] = wb
-                        ops += [dist.P2POp(dist.irecv, b, r, group=self.group) for b in (bufs[0], bufs[1]) + wb]
+                        # (2-byte counts travel as bytes: RCCL/NCCL has no 16-bit integer type)
+                        ops += [dist.P2POp(dist.irecv, b, r, group=self.group)
+                                for b in (bufs[0], bufs[1], wb[0], wb[1].view(torch.uint8))]
                     else:
                         ops += [dist.P2POp(dist.irecv, b, r, group=self.group) for b in bufs]
             else:
@@ -284,11 +286,12 @@ class StepGatherer:
                                                  mi=wb[0] if wb else None, cnt=wb[1] if wb else None,
                                                  n_fail=self.n_fail)
                     self._wire_bufs["send"] = (mi, wc)
-                    payload = (cnt, rr, mi, wc)
+                    payload = (cnt, rr, mi, wc.view(torch.uint8))
                 else:
                     payload = (cnt, rr, dmz, dint)
                 if self.wire and payload[2].numel() == 0:  # no peaks: rank 0 posts 2 floats, 1 count
-                    payload = payload[:2] + (torch.zeros(2, dtype=torch.float32, device=self.dev), payload[3])
+                    payload = payload[:2] + (torch.zeros(2, dtype=torch.float32, device=self.dev),
+                                             torch.zeros(self.wire, dtype=torch.uint8, device=self.dev))
                 ops = [dist.P2POp(dist.isend, one(x), 0, group=self.group) for x in payload]
             for q in (dist.batch_isend_irecv(ops) if ops else []):
                 q.wait()
