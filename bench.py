@@ -443,19 +443,16 @@ def north_star(args, out):
 
     t = make_clusters_torch(args.ns_clusters, seed=args.seed + 7)
     batch = engine.DeviceBatch.from_device(t)
-    bm = engine.bin_mean(batch)
-    md = engine.medoid(batch, check=True)
+    bm, md = engine.bin_mean_medoid(batch, check=True)  # the headline's step (fused pass)
     torch.cuda.synchronize()
     ok = bool(np.all(bm.status.cpu().numpy()[:batch.n_clusters] == 0) and
               np.all(md.rep.cpu().numpy()[:batch.n_clusters] >= 0))
     steps = max(3, args.steps // 2)
-    engine.bin_mean(batch, out=bm)
-    engine.medoid(batch, out=md, check=False)
+    engine.bin_mean_medoid(batch, out_bm=bm, out_md=md, check=False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        engine.bin_mean(batch, out=bm)
-        engine.medoid(batch, out=md, check=False)
+        engine.bin_mean_medoid(batch, out_bm=bm, out_md=md, check=False)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out["north_star_1m"] = {"clusters": batch.n_clusters, "spectra": batch.n_spectra, "peaks": batch.n_peaks,
