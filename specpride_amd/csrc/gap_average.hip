@@ -65,6 +65,9 @@ constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10
 #ifndef SPX_GA_HYBRID
 #define SPX_GA_HYBRID 1  // wide/global kernels: past UM * BLOCK peaks, the first UM * BLOCK stay in registers
 #endif
+#ifndef SPX_GA_P3INT
+#define SPX_GA_P3INT 0  // the LDS kernel reads the intensities in pass 3 instead of pass 1
+#endif
 #ifndef SPX_GA_EARLY
 #define SPX_GA_EARLY 1  // wide kernel: intensities streamed during the bucket pass, bitmap zeroed under the m/z loads
 #endif
@@ -746,10 +749,30 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 #else
   const bool early = false;
 #endif
+#if SPX_GA_P3INT
+  // The LDS kernel (every peak register-resident): the intensities are read in pass 3,
+  // not pass 1 -- pass 5's second read then follows the first by one step (the gaps),
+  // not by passes 2-4, and finds them in L2 instead of the fabric
+  const bool late = kDeferBig && kL && inreg && n > 1 && N >= 2;  // uniform
+#else
+  const bool late = false;
+#endif
   if (early) {
 #pragma unroll
     for (int k = 0; k < GA_WMAX / GA_BLOCK; ++k) S.bitmap[k * GA_BLOCK + tid] = 0ull;
     // 1a: m/z extrema and finiteness from registers
+#pragma unroll
+    for (int u = 0; u < UM; ++u) {
+      if (p0 + (int64_t)u * GA_BLOCK + tid < p1) {
+        bad |= !isfinite(rm[u]);
+        lo = fmin(lo, rm[u]);
+        hi = fmax(hi, rm[u]);
+      }
+    }
+    if (any(bad, 0)) return kNonFinite;
+  } else if (late) {
+    // 1 (SPX_GA_P3INT): the m/z extrema and finiteness from registers only; the
+    // intensities' max and finiteness come with pass 3 (below)
 #pragma unroll
     for (int u = 0; u < UM; ++u) {
       if (p0 + (int64_t)u * GA_BLOCK + tid < p1) {
@@ -888,7 +911,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   bar();
 
   // 3: per-slot count and m/z extent
-  peaks_m_tag([&](double m, double, int32_t& tag, auto reg_c) {
+  auto pass3 = [&](double m, double it, int32_t& tag, auto reg_c) __attribute__((always_inline)) {
     const int64_t b = decltype(reg_c)::value ? (int64_t)tag : floor_div_exact(m, P.bucket_w, P.inv_bucket_w) - kb;
     const int slot = bitmap_rank(S.bitmap, S.wprefix, b);
     tag = slot;
@@ -897,8 +920,28 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     atomicAdd(&S.cnt[slot], 1u);
     atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)key);
     atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)key);
-  });
-  bar();
+    if (late) {
+      bad |= !isfinite(it);
+      imax = fmax(imax, fabs(it));
+    }
+  };
+  if (late) {
+    peaks_g(std::true_type{}, std::true_type{}, pass3);
+    // the block's max |intensity| (pass 5's scale) and the intensities' finiteness
+    imax = wave_max_dpp(imax);
+    const bool wbad = __ballot(bad) != 0ull;
+    if (lane == 0) { red[2 * GA_NW + wid] = imax; votes[GA_NW + wid] = wbad; }
+    bar();
+    int nf = 0;
+    for (int w = 0; w < GA_NW; ++w) {
+      imax = fmax(imax, red[2 * GA_NW + w]);
+      nf |= votes[GA_NW + w];
+    }
+    if (nf) return kNonFinite;
+  } else {
+    peaks_m_tag(pass3);
+    bar();
+  }
 
   SPX_GA_STAMP(4);
   int E;
