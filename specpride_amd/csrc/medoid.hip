@@ -43,6 +43,9 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_MFMA_NMIN
 #define SPX_MD_MFMA_NMIN 32  // ... for clusters of more spectra than this
 #endif
+#ifndef SPX_MD_P5L
+#define SPX_MD_P5L 1  // P5 with one lane per spectrum (rows on wave 0, columns on wave 1)
+#endif
 #ifndef SPX_MD_RECIP
 #define SPX_MD_RECIP 1  // P4's quotients from per-spectrum reciprocals (exact, md_dist_r)
 #endif
@@ -219,6 +222,10 @@ struct MedoidRegSmem {
       uint8_t spre[UMAX * BLOCK / 64];              // spectra started before word w
     } a;                                         // P0..P4a
     double d[MR_TRI];                            // P4b..P5: d(i, j), j >= i, row-major packed
+    struct {
+      double d[MR_TRI];
+      double col[MD_NMAX];                       // P5 (SPX_MD_P5L): column sums, past d
+    } t;
   } u;
   int32_t soff[MD_NMAX + 1];
   double totals[MD_NMAX];
@@ -524,6 +531,46 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   auto dval = [&](int a, int b) -> double { return b >= a ? L.u.d[row_start(a) + b - a] : 0.0; };
 
   SPX_STAMP(5);
+#if SPX_MD_P5L
+  // P5: totals, one lane per spectrum (n <= 64): wave 0 sums row i, wave 1 column i, each
+  // with numpy's leaf order -- 8 strided accumulators over j < lim = n - n % 8 (in order),
+  // combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the sequential tail; n < 8 is all
+  // tail.  D's zeros (below the diagonal) are skipped: adding +0.0 to a sum of d >= 0
+  // changes nothing.  (16 lanes per spectrum and 4 rounds of 16 spectra measured slower.)
+  const bool colside = wid == 1;
+  const int i5 = lane;
+  const bool valid5 = i5 < n;
+  double sum = 0.0;
+  if (tid < 2 * kWave) {  // waves 0 and 1
+    const int i = i5;
+    const bool valid = valid5;
+    const int lim = n >= 8 ? n - n % 8 : 0;
+    auto term = [&](int j) -> double {
+      const bool use = valid && (colside ? j <= i : j >= i);
+      return use ? (colside ? L.u.d[row_start(j) + i - j] : L.u.d[row_start(i) + j - i]) : 0.0;
+    };
+    double r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = 0.0;
+    for (int j0 = 0; j0 < lim; j0 += 8) {  // uniform
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = term(j0 + k);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] += v[k];
+    }
+    sum = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int j = lim; j < n; ++j) sum += term(j);  // the sequential tail
+    sum = 0.0 + sum;
+    if (colside && valid) L.u.t.col[i] = sum;
+  }
+  lds_barrier();  // every wave
+  if (wid == 0 && valid5) {
+    const double t = (sum + L.u.t.col[i5]) / (double)n;  // (row + col) / n
+    L.totals[i5] = t;
+    if (totals_out) totals_out[s0 + i5] = t;
+  }
+#else
   // P5: totals, 16 lanes per spectrum (8 row accumulators, 8 column ones)
   const int k = lane & 7;
   const bool colside = (lane & 8) != 0;
@@ -554,6 +601,7 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       if (totals_out) totals_out[s0 + i] = t;
     }
   }
+#endif
   __syncthreads();
   SPX_STAMP(6);
   // P6: first index of the minimum (:103-110)
