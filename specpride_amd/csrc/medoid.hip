@@ -49,6 +49,9 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_RECIP
 #define SPX_MD_RECIP 1  // P4's quotients from per-spectrum reciprocals (exact, md_dist_r)
 #endif
+#ifndef SPX_MD_P1B
+#define SPX_MD_P1B 1  // P1 bins a batch of 8 branch-free; the rare exact divide once per batch
+#endif
 constexpr int MD_KWMAX = SPX_MD_KWMAX;  // row words (odd stride): <= 64 * MD_KWMAX occupied bins per small cluster
 
 
@@ -318,7 +321,47 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
           mb[bt & 1][q] = mzc[r < np ? r : 0];
         }
       }
-      if (bt > 0) {  // bin batch bt - 1
+      if (bt > 0 && SPX_MD_P1B) {  // bin batch bt - 1
+        const int pb = bt - 1;
+        uint32_t* const bits32 = reinterpret_cast<uint32_t*>(L.u.a.bits);
+        uint32_t slow = 0u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int u = pb * 8 + q;
+          const int r = u * BLOCK + tid;
+          uint32_t b = 0u;
+          if (r < np) {
+            bool sure;
+            const uint32_t bf = (uint32_t)ceil_div_fast(mb[pb & 1][q], P.inv_tol, sure);
+            const bool in = bf < kBins;
+            outside |= (int)(sure & !in);
+            slow |= (uint32_t)!sure << q;
+            const bool ok = sure & in;
+            b = ok ? bf : 0u;
+            // no bin yet: 0 ORed into a word of the lane's own (same-address LDS
+            // atomics serialise); 32-bit halves of the occupancy words likewise
+            atomicOr(bits32 + (ok ? b >> 5 : (uint32_t)lane), ok ? 1u << (b & 31) : 0u);
+          }
+          if (u & 1) bins[u >> 1] |= b << 16;
+          else bins[u >> 1] = b;
+        }
+        if (__builtin_expect(slow != 0u, 0)) {  // ~1 peak in 10^7: the correctly rounded divide (md_bin)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            if ((slow >> q) & 1u) {
+              const int u = pb * 8 + q;
+              const int64_t bb = md_bin(mb[pb & 1][q], P);
+              if (bb < 0 || bb >= (int64_t)kBins) {
+                outside = 1;
+              } else {
+                const uint32_t b = (uint32_t)bb;
+                atomicOr(bits32 + (b >> 5), 1u << (b & 31));
+                bins[u >> 1] |= b << (16 * (u & 1));
+              }
+            }
+          }
+        }
+      } else if (bt > 0) {
         const int pb = bt - 1;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {

@@ -370,6 +370,16 @@ __device__ __forceinline__ int64_t ceil_div_exact(double x, double w, double inv
   return (int64_t)ceil(x / w);
 }
 
+// ceil_div_exact's fast half alone, for loops that batch the rare division:
+// the answer when *sure, else the caller divides (ceil_div_exact).
+__device__ __forceinline__ int32_t ceil_div_fast(double x, double inv_w, bool& sure) {
+  const double q = x * inv_w;
+  const double t = ceil(q);
+  const double f = t - q;
+  sure = fabs(q) < kDivFastLimit && f > kDivBand && f < 1.0 - kDivBand;
+  return __double2int_rz(t);  // saturating conversion: no UB where !sure
+}
+
 // f64 <-> order-preserving u64 (for LDS atomic min/max on doubles)
 __device__ __forceinline__ uint64_t f64_order_key(double x) {
   uint64_t u = __double_as_longlong(x);
