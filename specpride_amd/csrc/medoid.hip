@@ -324,39 +324,42 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       if (bt > 0 && SPX_MD_P1B) {  // bin batch bt - 1
         const int pb = bt - 1;
         uint32_t* const bits32 = reinterpret_cast<uint32_t*>(L.u.a.bits);
-        uint32_t slow = 0u;
+        uint32_t bad = 0u;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int u = pb * 8 + q;
           const int r = u * BLOCK + tid;
           uint32_t b = 0u;
           if (r < np) {
-            bool sure;
-            const uint32_t bf = (uint32_t)ceil_div_fast(mb[pb & 1][q], P.inv_tol, sure);
-            const bool in = bf < kBins;
-            outside |= (int)(sure & !in);
-            slow |= (uint32_t)!sure << q;
-            const bool ok = sure & in;
-            b = ok ? bf : 0u;
+            // the reciprocal product's ceil, when it is certain and inside the
+            // bitmap (|q| >= 2^24 saturates out of it); anything else -- a quotient
+            // near an integer, NaN, a bin outside [0, kBins) -- is settled below
+            const double qt = mb[pb & 1][q] * P.inv_tol;
+            const double t = ceil(qt);
+            const double f = t - qt;
+            const uint32_t bf = (uint32_t)__double2int_rz(t);
+            const bool ok = (f > kDivBand) & (f < 1.0 - kDivBand) & (bf < kBins);
+            bad |= (uint32_t)!ok << q;
             // no bin yet: 0 ORed into a word of the lane's own (same-address LDS
             // atomics serialise); 32-bit halves of the occupancy words likewise
-            atomicOr(bits32 + (ok ? b >> 5 : (uint32_t)lane), ok ? 1u << (b & 31) : 0u);
+            b = ok ? bf : (uint32_t)lane << 5;
+            atomicOr(bits32 + (b >> 5), ok ? 1u << (b & 31) : 0u);
           }
           if (u & 1) bins[u >> 1] |= b << 16;
           else bins[u >> 1] = b;
         }
-        if (__builtin_expect(slow != 0u, 0)) {  // ~1 peak in 10^7: the correctly rounded divide (md_bin)
+        if (__builtin_expect(bad != 0u, 0)) {  // ~1 peak in 10^7: md_bin's exact divide decides
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            if ((slow >> q) & 1u) {
+            if ((bad >> q) & 1u) {
               const int u = pb * 8 + q;
               const int64_t bb = md_bin(mb[pb & 1][q], P);
               if (bb < 0 || bb >= (int64_t)kBins) {
                 outside = 1;
               } else {
-                const uint32_t b = (uint32_t)bb;
+                const uint32_t b = (uint32_t)bb, s = 16 * (u & 1);
                 atomicOr(bits32 + (b >> 5), 1u << (b & 31));
-                bins[u >> 1] |= b << (16 * (u & 1));
+                bins[u >> 1] = (bins[u >> 1] & ~(0xFFFFu << s)) | (b << s);
               }
             }
           }
