@@ -458,7 +458,7 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
         const int sp = has_empty ? spectrum_of(L.soff, n, r) : spw + __popcll(sw & upto);
         // 32-bit halves: consecutive peaks of a spectrum share a row word, and
         // same-address LDS atomics serialise -- half as many per address
-        atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[sp * KW]) + (col >> 5), 1u << (col & 31));
+        atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[__mul24(sp, KW)]) + (col >> 5), 1u << (col & 31));
       }
     }
   }
