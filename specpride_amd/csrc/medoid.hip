@@ -49,6 +49,9 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_RECIP
 #define SPX_MD_RECIP 1  // P4's quotients from per-spectrum reciprocals (exact, md_dist_r)
 #endif
+#ifndef SPX_MD_P6W
+#define SPX_MD_P6W 1  // P6's argmin in wave 0 right after P5 (totals in registers)
+#endif
 #ifndef SPX_MD_P1B
 #define SPX_MD_P1B 1  // P1 bins a batch of 8 branch-free; the rare exact divide once per batch
 #endif
@@ -615,6 +618,9 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
     const double t = (sum + L.u.t.col[i5]) / (double)n;  // (row + col) / n
     L.totals[i5] = t;
     if (totals_out) totals_out[s0 + i5] = t;
+#if SPX_MD_P6W
+    sum = t;  // wave 0 keeps lane i's total for P6
+#endif
   }
 #else
   // P5: totals, 16 lanes per spectrum (8 row accumulators, 8 column ones)
@@ -648,11 +654,18 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
     }
   }
 #endif
+#if SPX_MD_P5L && SPX_MD_P6W
+  // P6 straight from wave 0's registers (lane i holds total i): no barrier, no LDS
+  SPX_STAMP(6);
+  if (wid == 0) {
+    double t = valid5 ? sum : __longlong_as_double(0x7ff0000000000000ll);
+#else
   __syncthreads();
   SPX_STAMP(6);
   // P6: first index of the minimum (:103-110)
   if (tid < kWave) {
     double t = tid < n ? L.totals[tid] : __longlong_as_double(0x7ff0000000000000ll);
+#endif
     int idx = tid < n ? tid : 0x7fffffff;
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
