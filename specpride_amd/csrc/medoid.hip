@@ -49,6 +49,12 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_RECIP
 #define SPX_MD_RECIP 1  // P4's quotients from per-spectrum reciprocals (exact, md_dist_r)
 #endif
+#ifndef SPX_MD_R32
+#define SPX_MD_R32 1  // column ranks from 32-bit occupancy words with u16 prefixes
+#endif
+#ifndef SPX_MD_MBC
+#define SPX_MD_MBC 1  // P3's spectrum index from spectrum-end bits by v_mbcnt
+#endif
 #ifndef SPX_MD_P6W
 #define SPX_MD_P6W 1  // P6's argmin in wave 0 right after P5 (totals in registers)
 #endif
@@ -224,8 +230,8 @@ struct MedoidRegSmem {
       unsigned long long bits[MR_WMAX];
       uint32_t pre[MR_WMAX];
       unsigned long long rows[MD_NMAX * KWMAX];
-      unsigned long long sbits[UMAX * BLOCK / 64];  // bit r: peak r starts spectrum >= 1
-      uint8_t spre[UMAX * BLOCK / 64];              // spectra started before word w
+      unsigned long long sbits[UMAX * BLOCK / 64];  // bit r: peak r starts spectrum >= 1 (SPX_MD_MBC: ends a spectrum)
+      uint8_t spre[UMAX * BLOCK / 64];              // spectra started (ended) before word w
     } a;                                         // P0..P4a
     double d[MR_TRI];                            // P4b..P5: d(i, j), j >= i, row-major packed
     struct {
@@ -287,7 +293,13 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   }
   for (int j = 1 + tid; j < n; j += BLOCK) {
     const int r = L.soff[j];
+#if SPX_MD_MBC
+    // end bits: peak r - 1 closes spectrum j - 1 (r >= 1 unless spectrum 0 is
+    // empty, and then the binary search decides)
+    if (r >= 1 && r < np) atomicOr(&L.u.a.sbits[(r - 1) >> 6], 1ull << ((r - 1) & 63));
+#else
     if (r < np) atomicOr(&L.u.a.sbits[r >> 6], 1ull << (r & 63));
+#endif
   }
   __syncthreads();
   const bool has_empty = L.red[1] != 0;
@@ -412,6 +424,25 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   {
     // all MR_WMAX records (P0 cleared them), RPT
     // contiguous per thread, read unconditionally: the reads pipeline
+#if SPX_MD_R32
+    // per 32-bit word: a u16 prefix (K <= 32,768) in the same 2 KB
+    constexpr int RPT = 2 * MR_WMAX / BLOCK;
+    const int w0 = tid * RPT;
+    const uint32_t* const bits32 = reinterpret_cast<const uint32_t*>(L.u.a.bits);
+    uint16_t* const pre16 = reinterpret_cast<uint16_t*>(L.u.a.pre);
+    uint32_t b[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) b[k] = bits32[w0 + k];
+    int local = 0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) local += __popc(b[k]);
+    int base = block_exclusive_scan<BLOCK, int, true>(local, L.tmp, K);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      pre16[w0 + k] = (uint16_t)base;
+      base += __popc(b[k]);
+    }
+#else
     constexpr int RPT = MR_WMAX / BLOCK;
     const int w0 = tid * RPT;
     unsigned long long b[RPT];
@@ -426,6 +457,7 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       L.u.a.pre[w0 + k] = (uint32_t)base;
       base += __popcll(b[k]);
     }
+#endif
   }
   // row stride KW is odd: lanes reading rows j, j+1, ... at one word hit
   // different LDS banks (an even stride of u64s would fold them together)
@@ -455,10 +487,25 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       const int spw = __builtin_amdgcn_readlane(my_sp, u);
       if (r < np) {
         const uint32_t b = (bins[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+#if SPX_MD_R32
+        // rank in a 32-bit word: its u16 prefix + the popcount of the bits below b
+        const uint32_t w32 = b >> 5;
+        const int col = (int)reinterpret_cast<const uint16_t*>(L.u.a.pre)[w32] +
+                        __popc(__builtin_amdgcn_ubfe(reinterpret_cast<const uint32_t*>(L.u.a.bits)[w32], 0u, b & 31u));
+#else
         const int col = (int)L.u.a.pre[b >> 6] + __popcll(L.u.a.bits[b >> 6] & ((1ull << (b & 63)) - 1ull));
+#endif
         // empty spectra share a start bit: then the binary search
         const unsigned long long sw = ((unsigned long long)swhi << 32) | swlo;
+#if SPX_MD_MBC
+        // spectra closed before peak r: the word's prefix + its end bits below this
+        // lane (peak r is bit `lane` of its word) -- two v_mbcnt
+        (void)sw;
+        const int sp = has_empty ? spectrum_of(L.soff, n, r)
+                                 : (int)__builtin_amdgcn_mbcnt_hi(swhi, __builtin_amdgcn_mbcnt_lo(swlo, (uint32_t)spw));
+#else
         const int sp = has_empty ? spectrum_of(L.soff, n, r) : spw + __popcll(sw & upto);
+#endif
         // 32-bit halves: consecutive peaks of a spectrum share a row word, and
         // same-address LDS atomics serialise -- half as many per address
         atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[__mul24(sp, KW)]) + (col >> 5), 1u << (col & 31));
