@@ -55,6 +55,9 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_MBC
 #define SPX_MD_MBC 1  // P3's spectrum index from spectrum-end bits by v_mbcnt
 #endif
+#ifndef SPX_MD_SWZ
+#define SPX_MD_SWZ 1  // P3's row words swizzled per bit position (no same-word LDS atomics)
+#endif
 #ifndef SPX_MD_P6W
 #define SPX_MD_P6W 1  // P6's argmin in wave 0 right after P5 (totals in registers)
 #endif
@@ -478,6 +481,10 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   }
   __syncthreads();
   const unsigned long long upto = (2ull << lane) - 1ull;  // bits 0..lane
+#if SPX_MD_SWZ
+  const uint32_t swz_nw = 2u * (uint32_t)KW;  // 32-bit words per row
+  const uint32_t swz_m = swz_nw >= 32u ? 31u : (1u << (31 - __clz((int)swz_nw))) - 1u;  // 2^k - 1 < swz_nw
+#endif
 #pragma unroll
   for (int u = 0; u < UMAX; ++u) {
     if (u * BLOCK < np) {  // uniform
@@ -508,7 +515,19 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
 #endif
         // 32-bit halves: consecutive peaks of a spectrum share a row word, and
         // same-address LDS atomics serialise -- half as many per address
+#ifdef SPX_DG_P3LANE  // diagnostic (wrong results): each lane ORs into a word of its own -- no conflicts
+        atomicOr(reinterpret_cast<uint32_t*>(L.u.a.rows) + (tid & 255) + ((__mul24(sp, KW) + (col >> 5)) & 0), 1u << (col & 31));
+#elif SPX_MD_SWZ
+        // word (col/32 + (col & m)) mod NW32: a bijection per bit position, so P4's
+        // row-AND popcounts and Gram sums are unchanged, while neighbouring columns of a
+        // spectrum -- consecutive lanes -- land in different words (a shared word
+        // serialises the LDS atomic: ~6 lanes per word unswizzled)
+        uint32_t wq = (uint32_t)(col >> 5) + ((uint32_t)col & swz_m);
+        wq = min(wq, wq - swz_nw);
+        atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[__mul24(sp, KW)]) + wq, 1u << (col & 31));
+#else
         atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[__mul24(sp, KW)]) + (col >> 5), 1u << (col & 31));
+#endif
       }
     }
   }
