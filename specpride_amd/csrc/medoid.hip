@@ -1013,6 +1013,10 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
                                                                 int64_t arena_bytes, int64_t* rep) {
   __shared__ int tmp[MD_BLOCK / kWave + 1];
   __shared__ int64_t base_sh;
+  // the post-order walk's stack in LDS: as private arrays it is dynamically indexed
+  // scratch, a memory round trip per access (this kernel took ~110 us for n = 5,000)
+  __shared__ int64_t lo[40], len[40];
+  __shared__ int st[40], lft[40];
   const int tid = threadIdx.x;
   const int32_t nd = *n_deferred;
   for (int32_t di = blockIdx.x; di < nd; di += gridDim.x) {
@@ -1050,8 +1054,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
       int32_t* lnode = start + (maxL + 1);                                           // [maxL]
       int32_t* prog = lnode + maxL;                                                  // [3 * maxL]
       int nl = 0, nq = 0, nid = 0, ret = 0;
-      int64_t lo[40], len[40];
-      int st[40], lft[40];
       int sp = 0;
       lo[0] = 0; len[0] = n; st[0] = 0;
       for (;;) {
@@ -1493,6 +1495,9 @@ __device__ __forceinline__ void dual_leaf_at(const F& f, int lo, int m, int i, d
 #ifndef SPX_MD_LEAF_W
 #define SPX_MD_LEAF_W 1
 #endif
+#ifndef SPX_MD_COMB_STACK
+#define SPX_MD_COMB_STACK 1  // combine: the pairwise tree as an LDS stack machine (no memory round trips)
+#endif
 constexpr int MD_LEAF_MAX = 128;  // a numpy pairwise leaf holds at most 128 terms
 
 // Leaf sums, grid-stride over (cluster, leaf, 256-wide chunk of i): thread i
@@ -1575,6 +1580,19 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_leaves_kernel(CsrView v, cons
 __global__ __launch_bounds__(MD_BLOCK) void medoid_combine_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
                                                                   const int64_t* chunk_base, char* arena,
                                                                   double* totals_out) {
+#if SPX_MD_COMB_STACK
+  // The node ids are the post-order (plan2 numbers leaves and internal nodes as they
+  // complete), so the tree is evaluated as a stack machine over ids 0..2L-2: a leaf
+  // pushes its two sums (read from memory, independent loads), an internal node pops
+  // right and left and pushes left + right -- the same additions in the same order.
+  // The stack lives in LDS (uniform depth, one slot per thread): no dependent
+  // round trip through memory per node (one per node took ~80 us for n = 5,000).
+  // depth <= log2(n / 128) + 2: 14 for n < 2^20 (the n x n count matrix alone bounds
+  // n to ~2^18 in 288 GB); larger n keep the memory walk
+  constexpr int kDepth = 16;
+  __shared__ double stk[kDepth][2][MD_BLOCK];
+  const int tid = threadIdx.x;
+#endif
   const int32_t nd = *n_deferred;
   const int64_t total = chunk_base[nd];
   for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {
@@ -1587,6 +1605,30 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_combine_kernel(const MedoidMe
                           md_max_leaves(n);
     double* row = reinterpret_cast<double*>(arena + M.lsum_off) + i;
     double* col = row + (int64_t)(2 * M.L - 1) * n;
+#if SPX_MD_COMB_STACK
+    if (n < (1 << 20)) {  // uniform
+    (void)prog;
+    const int32_t* lnode = reinterpret_cast<const int32_t*>(arena + M.leaf_off) + (md_max_leaves(n) + 1);
+    int sp = 0, kl = 0;
+    for (int id = 0; id <= 2 * M.L - 2; ++id) {  // uniform
+      if (kl < M.L && lnode[kl] == id) {
+        stk[sp][0][tid] = row[(int64_t)id * n];
+        stk[sp][1][tid] = col[(int64_t)id * n];
+        ++sp;
+        ++kl;
+      } else {
+        --sp;
+        stk[sp - 1][0][tid] = stk[sp - 1][0][tid] + stk[sp][0][tid];
+        stk[sp - 1][1][tid] = stk[sp - 1][1][tid] + stk[sp][1][tid];
+      }
+    }
+    const double t = ((0.0 + stk[0][0][tid]) + (0.0 + stk[0][1][tid])) / (double)n;
+    reinterpret_cast<double*>(arena + M.tot_off)[i] = t;
+    if (totals_out) totals_out[M.s0 + i] = t;
+    continue;
+    }
+#endif
+    {
     for (int q = 0; q < M.L - 1; ++q) {
       const int64_t l = prog[3 * q], r = prog[3 * q + 1], out = prog[3 * q + 2];
       row[out * n] = row[l * n] + row[r * n];
@@ -1596,6 +1638,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_combine_kernel(const MedoidMe
     const double t = ((0.0 + row[root * n]) + (0.0 + col[root * n])) / (double)n;
     reinterpret_cast<double*>(arena + M.tot_off)[i] = t;
     if (totals_out) totals_out[M.s0 + i] = t;
+    }
   }
 }
 
