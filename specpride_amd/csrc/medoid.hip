@@ -55,6 +55,9 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_MBC
 #define SPX_MD_MBC 1  // P3's spectrum index from spectrum-end bits by v_mbcnt
 #endif
+#ifndef SPX_MD_L1RUNS
+#define SPX_MD_L1RUNS 1  // level-1 pass: one LDS atomic per run of lanes sharing a word
+#endif
 #ifndef SPX_MD_SWZ
 #define SPX_MD_SWZ 1  // P3's row words swizzled per bit position (no same-word LDS atomics)
 #endif
@@ -164,6 +167,7 @@ __device__ __forceinline__ md_i32x8 md_frag4(uint64_t w, int fh) {
 struct MedoidMeta {
   unsigned long long lo_key, hi_key;  // bin range, order-preserving keys (atomicMax; 0 = none)
   int64_t c, s0, blo;
+  int64_t p0, np;  // the cluster's peaks (medoid_units_kernel)
   int64_t l1_off, l2_off, rows_off, rowsT_off, cmat_off, leaf_off, lsum_off, tot_off;  // arena byte offsets
   int32_t n, nw1, B1, KW, L, tiles, units, ok;
 };
@@ -850,20 +854,107 @@ __device__ __forceinline__ int64_t md_bump(unsigned long long* bump, int64_t byt
   return b + bytes > cap ? -1 : b;
 }
 
+// which deferred cluster owns work item t (base[lo] <= t < base[lo + 1], skipping empties)
+__device__ __forceinline__ int md_owner(const int64_t* base, int nd, int64_t t) {
+  int lo = 0, hi = nd;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (base[mid] <= t) lo = mid; else hi = mid;
+  }
+  while (lo + 1 < nd && base[lo + 1] <= t) ++lo;
+  return lo;
+}
+
+// Units of the three peak passes (range, level 1, level 2): per deferred cluster its
+// peak range and ceil(peaks / MD_PU) units of MD_PU peaks (one at least: unit 0 also
+// allocates the level-1 bitmap), exclusive-scanned into pk_base (one workgroup).  A
+// flat grid over units keeps every block on one unit of 64 peaks per thread, where a
+// fixed 64 blocks per cluster gave the 442 clusters of configs[3] ~4 peaks per thread
+// per cluster and a dependent meta -> offsets -> m/z chain for each.
+constexpr int MD_PU = 16384;
+
+__global__ __launch_bounds__(MD_BLOCK) void medoid_units_kernel(CsrView v, MedoidMeta* meta, const int32_t* n_deferred,
+                                                                int64_t* pk_base) {
+  __shared__ int64_t tmp[MD_BLOCK / kWave + 1];
+  const int32_t nd = *n_deferred;
+  int64_t cu = 0;
+  for (int32_t i0 = 0; i0 < nd; i0 += MD_BLOCK) {  // uniform
+    const int32_t i = i0 + (int32_t)threadIdx.x;
+    int64_t units = 0;
+    if (i < nd) {
+      const int64_t s0 = meta[i].s0;
+      const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s0 + meta[i].n];
+      meta[i].p0 = p0;
+      meta[i].np = p1 - p0;
+      units = p1 > p0 ? (p1 - p0 + MD_PU - 1) / MD_PU : 1;
+    }
+    int64_t tot;
+    const int64_t e = block_exclusive_scan<MD_BLOCK>(units, tmp, tot);
+    if (i < nd) pk_base[i] = cu + e;
+    cu += tot;
+  }
+  if (threadIdx.x == 0) pk_base[nd] = cu;
+}
+
+// a unit's peaks [k0, k1) and its cluster
+__device__ __forceinline__ int md_unit(const int64_t* pk_base, int nd, const MedoidMeta* meta, int64_t u, int64_t& r,
+                                       int64_t& k0, int64_t& k1) {
+  const int o = md_owner(pk_base, nd, u);
+  r = u - pk_base[o];
+  const int64_t p0 = meta[o].p0, p1 = p0 + meta[o].np;
+  k0 = p0 + r * MD_PU;
+  k1 = k0 + MD_PU < p1 ? k0 + MD_PU : p1;
+  return o;
+}
+
+// f(k, m) for every peak k of [k0, k1): thread tid takes k0 + tid + j * MD_BLOCK,
+// eight m/z loads in flight at a time
+template <class F>
+__device__ __forceinline__ void md_unit_peaks(const CsrView& v, int64_t k0, int64_t k1, const F& f) {
+  for (int64_t kb = k0 + threadIdx.x; kb < k1; kb += 8 * MD_BLOCK) {
+    double m[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int64_t k = kb + (int64_t)q * MD_BLOCK;
+      m[q] = k < k1 ? v.mz[k] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (kb + (int64_t)q * MD_BLOCK < k1) f(m[q]);
+  }
+}
+
+// f(m, active) for every lane on every round of [k0, k1) (uniform: the whole wave
+// calls f, lanes past k1 with active = false), eight m/z loads in flight at a time
+template <class F>
+__device__ __forceinline__ void md_unit_peaks_all(const CsrView& v, int64_t k0, int64_t k1, const F& f) {
+  for (int64_t kb = k0; kb < k1; kb += 8 * MD_BLOCK) {  // uniform
+    double m[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int64_t k = kb + (int64_t)q * MD_BLOCK + threadIdx.x;
+      m[q] = k < k1 ? v.mz[k] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f(m[q], kb + (int64_t)q * MD_BLOCK + threadIdx.x < k1);
+  }
+}
+
 // Pass 1: bin range of every deferred cluster (wave-reduced atomics on
 // order-preserving keys; lo is stored complemented so both are maxima).
-// Block x == 0 also allocates and zeroes the cluster's level-1 bitmap.
+// Unit 0 of a cluster also allocates and zeroes its level-1 bitmap.
 __global__ __launch_bounds__(MD_BLOCK) void medoid_range_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
-                                                                MedoidMeta* meta, char* arena,
+                                                                MedoidMeta* meta, const int64_t* pk_base, char* arena,
                                                                 unsigned long long* bump, int64_t arena_bytes) {
   __shared__ int64_t base_sh;
   const int tid = threadIdx.x;
   const int32_t nd = *n_deferred;
-  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
-    MedoidMeta* M = meta + di;
-    const int64_t s0 = M->s0;
-    const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s0 + M->n];
-    if (blockIdx.x == 0) {
+  const int64_t total = pk_base[nd];
+  for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {  // uniform
+    int64_t r, k0, k1;
+    const int o = md_unit(pk_base, nd, meta, u, r, k0, k1);
+    MedoidMeta* M = meta + o;
+    if (r == 0) {
       if (tid == 0) base_sh = md_bump(bump, md_l1_bytes(), arena_bytes);
       __syncthreads();
       const int64_t base = base_sh;
@@ -875,14 +966,14 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_range_kernel(CsrView v, Medoi
       __syncthreads();
     }
     long long lo = 0x7fffffffffffffffll, hi = -0x7fffffffffffffffll - 1;
-    for (int64_t k = p0 + (int64_t)blockIdx.x * MD_BLOCK + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
-      const long long b = md_bin(v.mz[k], P);
+    md_unit_peaks(v, k0, k1, [&](double m) {
+      const long long b = md_bin(m, P);
       lo = b < lo ? b : lo;
       hi = b > hi ? b : hi;
-    }
+    });
 #pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      const long long l2 = __shfl_xor(lo, o, kWave), h2 = __shfl_xor(hi, o, kWave);
+    for (int o2 = kWave / 2; o2 > 0; o2 >>= 1) {
+      const long long l2 = __shfl_xor(lo, o2, kWave), h2 = __shfl_xor(hi, o2, kWave);
       lo = l2 < lo ? l2 : lo;
       hi = h2 > hi ? h2 : hi;
     }
@@ -905,24 +996,37 @@ __device__ __forceinline__ bool md_range(const MedoidMeta& M, int64_t& blo, int&
 
 // Pass 2: level-1 occupancy, staged in LDS, merged with one atomicOr per word.
 __global__ __launch_bounds__(MD_BLOCK) void medoid_l1_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
-                                                             const MedoidMeta* meta, char* arena) {
+                                                             const MedoidMeta* meta, const int64_t* pk_base,
+                                                             char* arena) {
   __shared__ unsigned long long l1s[MD_L1WORDS];
   const int tid = threadIdx.x;
   const int32_t nd = *n_deferred;
-  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
-    const MedoidMeta M = meta[di];
+  const int64_t total = pk_base[nd];
+  for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {  // uniform
+    int64_t r, k0, k1;
+    const MedoidMeta M = meta[md_unit(pk_base, nd, meta, u, r, k0, k1)];
     int64_t blo;
     int nw1;
-    if (M.l1_off < 0 || !md_range(M, blo, nw1) || nw1 == 0) continue;
-    const int64_t p0 = v.spec_off[M.s0], p1 = v.spec_off[M.s0 + M.n];
-    const int64_t k0 = p0 + (int64_t)blockIdx.x * MD_BLOCK;
-    if (k0 >= p1) continue;  // uniform per block: no barrier divergence
+    if (M.l1_off < 0 || !md_range(M, blo, nw1) || nw1 == 0 || k0 >= k1) continue;
     for (int w = tid; w < nw1; w += MD_BLOCK) l1s[w] = 0ull;
     __syncthreads();
-    for (int64_t k = k0 + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
-      const int64_t blk = (md_bin(v.mz[k], P) - blo) >> 6;
+#if SPX_MD_L1RUNS
+    // neighbouring peaks fall in the same 64-bin block or the next: ~40 lanes of a
+    // wave OR into one level-1 word, so each run of lanes with one 32-bit word
+    // ORs its bits together first and its last lane issues the atomic
+    uint32_t* const l1s32 = reinterpret_cast<uint32_t*>(l1s);
+    md_unit_peaks_all(v, k0, k1, [&](double m, bool act) {
+      const int64_t blk = act ? (md_bin(m, P) - blo) >> 6 : 0;
+      const uint32_t key = act ? (uint32_t)(blk >> 5) : 0xFFFFFFFEu;
+      uint32_t val = act ? 1u << (blk & 31) : 0u;
+      if (wave_or_runs(key, val) && act) atomicOr(&l1s32[key], val);
+    });
+#else
+    md_unit_peaks(v, k0, k1, [&](double m) {
+      const int64_t blk = (md_bin(m, P) - blo) >> 6;
       atomicOr(&l1s[blk >> 6], 1ull << (blk & 63));
-    }
+    });
+#endif
     __syncthreads();
     unsigned long long* l1 = reinterpret_cast<unsigned long long*>(arena + M.l1_off);
     for (int w = tid; w < nw1; w += MD_BLOCK)
@@ -973,16 +1077,16 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan1_kernel(const int32_t* n
 
 // Pass 3: level-2 occupancy (LDS-staged when the cluster's level-2 fits).
 __global__ __launch_bounds__(MD_BLOCK) void medoid_l2_kernel(CsrView v, MedoidParams P, const int32_t* n_deferred,
-                                                             const MedoidMeta* meta, char* arena) {
+                                                             const MedoidMeta* meta, const int64_t* pk_base,
+                                                             char* arena) {
   __shared__ unsigned long long l2s[MD_L2LDS];
   const int tid = threadIdx.x;
   const int32_t nd = *n_deferred;
-  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
-    const MedoidMeta M = meta[di];
-    if (M.l1_off < 0 || M.l2_off == 0 || M.B1 == 0) continue;
-    const int64_t p0 = v.spec_off[M.s0], p1 = v.spec_off[M.s0 + M.n];
-    const int64_t k0 = p0 + (int64_t)blockIdx.x * MD_BLOCK;
-    if (k0 >= p1) continue;
+  const int64_t total = pk_base[nd];
+  for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {  // uniform
+    int64_t r, k0, k1;
+    const MedoidMeta M = meta[md_unit(pk_base, nd, meta, u, r, k0, k1)];
+    if (M.l1_off < 0 || M.l2_off == 0 || M.B1 == 0 || k0 >= k1) continue;
     const MedoidTables T = md_tables(arena, M);
     unsigned long long* l2 = reinterpret_cast<unsigned long long*>(arena + M.l2_off);
     const bool staged = M.B1 <= MD_L2LDS;
@@ -990,12 +1094,12 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_l2_kernel(CsrView v, MedoidPa
       for (int w = tid; w < M.B1; w += MD_BLOCK) l2s[w] = 0ull;
       __syncthreads();
     }
-    for (int64_t k = k0 + tid; k < p1; k += (int64_t)gridDim.x * MD_BLOCK) {
-      const int64_t rel = md_bin(v.mz[k], P) - M.blo;
+    md_unit_peaks(v, k0, k1, [&](double m) {
+      const int64_t rel = md_bin(m, P) - M.blo;
       const int bs = bitmap_rank(T.l1, T.l1pre, rel >> 6);
       if (staged) atomicOr(&l2s[bs], 1ull << (rel & 63));
       else atomicOr(&l2[bs], 1ull << (rel & 63));
-    }
+    });
     if (staged) {
       __syncthreads();
       for (int w = tid; w < M.B1; w += MD_BLOCK)
@@ -1133,16 +1237,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta*
   if (threadIdx.x == 0) { tile_base[nd] = ct; unit_base[nd] = cu; chunk_base[nd] = cc; xpose_base[nd] = cx; }
 }
 
-// which deferred cluster owns work item t (base[lo] <= t < base[lo + 1], skipping empties)
-__device__ __forceinline__ int md_owner(const int64_t* base, int nd, int64_t t) {
-  int lo = 0, hi = nd;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (base[mid] <= t) lo = mid; else hi = mid;
-  }
-  while (lo + 1 < nd && base[lo + 1] <= t) ++lo;
-  return lo;
-}
 
 // Bit rows, one wave per (padded) row: zero the row's words, drain the stores,
 // then OR in one bit per peak (peaks may be unsorted; duplicates are idempotent).

@@ -638,7 +638,7 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
   size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(spx::kListCountBytes) +
                  align256(sizeof(int32_t) * Cm) +
                  align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
-                 align256(sizeof(spx::MedoidMeta) * Cm) + 4 * align256(sizeof(int64_t) * (Cm + 1));
+                 align256(sizeof(spx::MedoidMeta) * Cm) + 5 * align256(sizeof(int64_t) * (Cm + 1));
   size_t arena = 0, margin = 0;
   // small clusters with more peaks than the wide kernel has bin words for: the only
   // ones a run can defer into the arena (their arena bytes)
@@ -717,6 +717,7 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
   int64_t* unit_base = w.take<int64_t>((size_t)C + 1);
   int64_t* chunk_base = w.take<int64_t>((size_t)C + 1);
   int64_t* xpose_base = w.take<int64_t>((size_t)C + 1);
+  int64_t* pk_base = w.take<int64_t>((size_t)C + 1);
   if (w.used >= workspace_bytes) return fail(SPX_ENOSPACE, "spx_medoid: workspace too small");
   char* arena = w.base + w.used;
   const int64_t arena_bytes = (int64_t)(workspace_bytes - w.used);
@@ -746,13 +747,18 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
                      dim3(spx::MW_BLOCK), 0, s, V, P, rep, totals, wide, def, n_def, meta);
   if (int rc = check_launch("medoid_wide_kernel")) return rc;
   if (!params->large_path) return SPX_SUCCESS;  // deferred clusters keep rep = SPX_REP_DEFERRED
-  hipLaunchKernelGGL(spx::medoid_range_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena, bump, arena_bytes);
+  hipLaunchKernelGGL(spx::medoid_units_kernel, dim3(1), blk, 0, s, V, meta, n_def, pk_base);
+  if (int rc = check_launch("medoid_units_kernel")) return rc;
+  // the peak passes: a flat grid over MD_PU-peak units of every deferred cluster
+  const dim3 gridu(2048);
+  hipLaunchKernelGGL(spx::medoid_range_kernel, gridu, blk, 0, s, V, P, n_def, meta, pk_base, arena, bump,
+                     arena_bytes);
   if (int rc = check_launch("medoid_range_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_l1_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena);
+  hipLaunchKernelGGL(spx::medoid_l1_kernel, gridu, blk, 0, s, V, P, n_def, meta, pk_base, arena);
   if (int rc = check_launch("medoid_l1_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_plan1_kernel, dim3(g), blk, 0, s, n_def, meta, arena, bump, arena_bytes, rep);
   if (int rc = check_launch("medoid_plan1_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_l2_kernel, grid2, blk, 0, s, V, P, n_def, meta, arena);
+  hipLaunchKernelGGL(spx::medoid_l2_kernel, gridu, blk, 0, s, V, P, n_def, meta, pk_base, arena);
   if (int rc = check_launch("medoid_l2_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_plan2_kernel, dim3(g), blk, 0, s, n_def, meta, arena, bump, arena_bytes, rep);
   if (int rc = check_launch("medoid_plan2_kernel")) return rc;

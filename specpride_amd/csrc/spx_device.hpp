@@ -127,6 +127,27 @@ __device__ __forceinline__ T wave_scan_dpp(T x, T ident, Op op) {
   return x;
 }
 
+// OR of `val` over each run of consecutive lanes holding the same `key` (a segmented
+// Hillis-Steele scan on the DPP steps of wave_scan_dpp); true on the lane that ends
+// its run, which then holds the OR of the run.  Lanes of one key that are not
+// contiguous end runs of their own (each a correct partial OR).  Keys must differ
+// from 0xFFFFFFFF; call with the whole wave active.  This turns a wave's LDS atomic
+// ORs into one word from many lanes (which serialise) into one atomic per run.
+__device__ __forceinline__ bool wave_or_runs(uint32_t key, uint32_t& val) {
+  auto step = [&](auto ctrl_c, auto mask_c) __attribute__((always_inline)) {
+    constexpr int C = decltype(ctrl_c)::value, M = decltype(mask_c)::value;
+    const uint32_t k2 = dpp_u32<C, M>(0xFFFFFFFFu, key), v2 = dpp_u32<C, M>(0u, val);
+    if (k2 == key) val |= v2;
+  };
+  step(std::integral_constant<int, 0x111>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x112>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x114>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x118>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xA>{});
+  step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xC>{});
+  return (uint32_t)wave_next((int32_t)key, -1) != key;
+}
+
 // Inclusive wave scan: DPP for 32-bit integers (kDpp), else ds_bpermute shuffles.
 // The register bin-mean kernel measured 1% faster with the shuffle form (its
 // LDS round trips overlap the surrounding VALU work), the others 2-3% faster
