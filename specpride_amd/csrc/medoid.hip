@@ -1589,6 +1589,67 @@ __device__ __forceinline__ void dual_leaf_at(const F& f, int lo, int m, int i, d
 #ifndef SPX_MD_LEAF_W
 #define SPX_MD_LEAF_W 1
 #endif
+#ifndef SPX_MD_LEAF_B
+#define SPX_MD_LEAF_B 1  // leaves: count loads issued 16 at a time, ahead of the distances
+#endif
+
+// dual_leaf_at over column i of the count matrix (colp = cmat + i, row stride n) with
+// the loads separated from the arithmetic: 16 counts in flight per lane, then the
+// distances g(j, c) in j order.  Same sums: the 8 accumulators start at +0.0 instead
+// of the first term, which is exact for the distances' values (+0.0 <= d, or NaN).
+template <class G>
+__device__ __forceinline__ void dual_leaf_cols(const uint32_t* colp, int64_t n, const G& g, int lo, int m, int i,
+                                               double& row, double& col) {
+  auto acc = [&](int jj, uint32_t c, double& r, double& cc) __attribute__((always_inline)) {
+    const double d = g(jj, c);
+    r += jj >= i ? d : 0.0;
+    cc += jj <= i ? d : 0.0;
+  };
+  if (m < 8) {
+    double r = 0.0, cc = 0.0;
+    uint32_t cv[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) cv[q] = q < m ? colp[(int64_t)(lo + q) * n] : 0u;
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+      if (q < m) acc(lo + q, cv[q], r, cc);
+    row = r;
+    col = cc;
+    return;
+  }
+  double r[8], cc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = cc[k] = 0.0;
+  const int lim = m - (m % 8);
+  int j = 0;
+  for (; j + 16 <= lim; j += 16) {  // uniform
+    uint32_t cv[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) cv[q] = colp[(int64_t)(lo + j + q) * n];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc(lo + j + q, cv[q], r[q & 7], cc[q & 7]);
+  }
+  if (j < lim) {  // one round of 8 left
+    uint32_t cv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cv[q] = colp[(int64_t)(lo + j + q) * n];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc(lo + j + q, cv[q], r[q], cc[q]);
+    j += 8;
+  }
+  double rs = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  double cs = ((cc[0] + cc[1]) + (cc[2] + cc[3])) + ((cc[4] + cc[5]) + (cc[6] + cc[7]));
+  {  // the sequential tail (< 8 terms)
+    uint32_t cv[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) cv[q] = j + q < m ? colp[(int64_t)(lo + j + q) * n] : 0u;
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+      if (j + q < m) acc(lo + j + q, cv[q], rs, cs);
+  }
+  row = rs;
+  col = cs;
+}
 #ifndef SPX_MD_COMB_STACK
 #define SPX_MD_COMB_STACK 1  // combine: the pairwise tree as an LDS stack machine (no memory round trips)
 #endif
@@ -1601,7 +1662,10 @@ constexpr int MD_LEAF_MAX = 128;  // a numpy pairwise leaf holds at most 128 ter
 // operations complete in order), and the j loop reads them back as broadcasts:
 // one division per spectrum and lane instead of one per (i, j).  Clusters whose
 // spectra reach 65,536 peaks keep the division.
-__global__ __launch_bounds__(MD_BLOCK) void medoid_leaves_kernel(CsrView v, const MedoidMeta* meta,
+#ifndef SPX_MD_LEAF_MINW
+#define SPX_MD_LEAF_MINW 5  // 86 VGPRs, no spills: 5 waves/SIMD (301 vs 318 us on configs[3] at 4)
+#endif
+__global__ __launch_bounds__(MD_BLOCK, SPX_MD_LEAF_MINW) void medoid_leaves_kernel(CsrView v, const MedoidMeta* meta,
                                                                  const int32_t* n_deferred, const int64_t* unit_base,
                                                                  char* arena) {
 #if SPX_MD_LEAF_W
@@ -1646,8 +1710,13 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_leaves_kernel(CsrView v, cons
         if (i >= n) continue;
         const int pi = (int)pi64;
         const double ri = pi > 0 ? 1.0 / (double)pi : 0.0;
+#if SPX_MD_LEAF_B
+        dual_leaf_cols(cmat + i, n, [&](int j, uint32_t c) { return md_dist_r(c, pi, ri, Pp[j - lo], R[j - lo]); }, lo,
+                       m, i, row, col);
+#else
         dual_leaf_at([&](int j) { return md_dist_r(cmat[(int64_t)j * n + i], pi, ri, Pp[j - lo], R[j - lo]); }, lo,
                      m, i, row, col);
+#endif
       } else {
         if (i >= n) continue;
         dual_leaf_at([&](int j) { return md_dist(cmat[(int64_t)j * n + i], pi64, so[j + 1] - so[j]); }, lo, m, i,
