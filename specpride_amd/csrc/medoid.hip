@@ -1117,10 +1117,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
                                                                 int64_t arena_bytes, int64_t* rep) {
   __shared__ int tmp[MD_BLOCK / kWave + 1];
   __shared__ int64_t base_sh;
-  // the post-order walk's stack in LDS: as private arrays it is dynamically indexed
-  // scratch, a memory round trip per access (this kernel took ~110 us for n = 5,000)
-  __shared__ int64_t lo[40], len[40];
-  __shared__ int st[40], lft[40];
   const int tid = threadIdx.x;
   const int32_t nd = *n_deferred;
   for (int32_t di = blockIdx.x; di < nd; di += gridDim.x) {
@@ -1138,7 +1134,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
     const int64_t maxL = md_max_leaves(n);
     const int64_t rows_b = md_align((int64_t)T * MD_GT * KW * 8);
     const int64_t cmat_b = md_align((int64_t)n * n * 4);
-    const int64_t leaf_b = md_align((5 * maxL + 1) * 4);        // starts, leaf nodes, program
+    const int64_t leaf_b = md_align((2 * maxL + 1) * 4);        // leaf starts, leaf node ids
     const int64_t lsum_b = md_align(2 * (2 * maxL) * (int64_t)n * 8);  // node values, row and column
     const int64_t tot_b = md_align((int64_t)n * 8);
     const int64_t rowsT_b = rows_b;  // the word-major copy the Gram kernel reads
@@ -1151,42 +1147,35 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
       continue;
     }
     if (tid == 0) {
-      // numpy's recursion over [0, n) as a post-order program: every node gets
-      // a value slot when it completes; leaves in order, internal nodes as
-      // (left slot, right slot, out slot) with children before parents.
+      // numpy's recursion over [0, n) (split at h = len/2 - (len/2) % 8 down to
+      // leaves of <= 128), numbered in post-order: leaf k's start and node id, and
+      // (implicitly) the internal nodes that complete right after it -- the
+      // ancestors below its deepest left turn.  Each leaf is found by a descent
+      // from the root in registers (no stack: a stack in LDS or scratch made this
+      // walk a memory round trip per step).  medoid_combine_kernel runs the same
+      // post-order as a stack machine over the ids.
       int32_t* start = reinterpret_cast<int32_t*>(arena + base + rows_b + rowsT_b + cmat_b);  // [maxL + 1]
       int32_t* lnode = start + (maxL + 1);                                           // [maxL]
-      int32_t* prog = lnode + maxL;                                                  // [3 * maxL]
-      int nl = 0, nq = 0, nid = 0, ret = 0;
-      int sp = 0;
-      lo[0] = 0; len[0] = n; st[0] = 0;
-      for (;;) {
-        if (st[sp] == 0 && len[sp] <= 128) {  // leaf
-          start[nl] = (int32_t)lo[sp];
-          lnode[nl++] = nid;
-          ret = nid++;
-        } else if (st[sp] == 0) {  // descend left
-          int64_t h = len[sp] / 2;
+      int nl = 0, nid = 0;
+      for (int64_t pos = 0; pos < n;) {
+        int64_t lo = 0, len = n;
+        int depth = 0, lastleft = -1;
+        while (len > 128) {
+          int64_t h = len / 2;
           h -= h % 8;
-          st[sp] = 1;
-          lo[sp + 1] = lo[sp]; len[sp + 1] = h; st[sp + 1] = 0;
-          ++sp;
-          continue;
-        } else if (st[sp] == 1) {  // left done: descend right
-          int64_t h = len[sp] / 2;
-          h -= h % 8;
-          lft[sp] = ret;
-          st[sp] = 2;
-          lo[sp + 1] = lo[sp] + h; len[sp + 1] = len[sp] - h; st[sp + 1] = 0;
-          ++sp;
-          continue;
-        } else {  // both done: internal node
-          prog[3 * nq] = lft[sp]; prog[3 * nq + 1] = ret; prog[3 * nq + 2] = nid;
-          ++nq;
-          ret = nid++;
+          if (pos < lo + h) {
+            len = h;
+            lastleft = depth;
+          } else {
+            lo += h;
+            len -= h;
+          }
+          ++depth;
         }
-        if (sp == 0) break;
-        --sp;
+        start[nl] = (int32_t)lo;
+        lnode[nl++] = nid++;
+        nid += depth - 1 - lastleft;  // the internal nodes this leaf completes
+        pos = lo + len;
       }
       start[nl] = n;
       M->KW = KW;
@@ -1650,9 +1639,6 @@ __device__ __forceinline__ void dual_leaf_cols(const uint32_t* colp, int64_t n, 
   row = rs;
   col = cs;
 }
-#ifndef SPX_MD_COMB_STACK
-#define SPX_MD_COMB_STACK 1  // combine: the pairwise tree as an LDS stack machine (no memory round trips)
-#endif
 constexpr int MD_LEAF_MAX = 128;  // a numpy pairwise leaf holds at most 128 terms
 
 // Leaf sums, grid-stride over (cluster, leaf, 256-wide chunk of i): thread i
@@ -1739,38 +1725,29 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_LEAF_MINW) void medoid_leaves_kern
 
 // Totals = (tree(row leaves) + tree(column leaves)) / n (most_similar_representative.py:98-100):
 // grid-stride over (cluster, 256-wide chunk of i); thread i runs the cluster's
-// post-order program over its node-value slots (coalesced across i).
+// post-order stack machine over its leaf sums (coalesced across i).
 __global__ __launch_bounds__(MD_BLOCK) void medoid_combine_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
                                                                   const int64_t* chunk_base, char* arena,
                                                                   double* totals_out) {
-#if SPX_MD_COMB_STACK
-  // The node ids are the post-order (plan2 numbers leaves and internal nodes as they
-  // complete), so the tree is evaluated as a stack machine over ids 0..2L-2: a leaf
-  // pushes its two sums (read from memory, independent loads), an internal node pops
-  // right and left and pushes left + right -- the same additions in the same order.
-  // The stack lives in LDS (uniform depth, one slot per thread): no dependent
-  // round trip through memory per node (one per node took ~80 us for n = 5,000).
-  // depth <= log2(n / 128) + 2: 14 for n < 2^20 (the n x n count matrix alone bounds
-  // n to ~2^18 in 288 GB); larger n keep the memory walk
+  // The node ids are the post-order (plan2), so the tree is evaluated as a stack
+  // machine over ids 0..2L-2: a leaf pushes its two sums (read from memory,
+  // independent loads), an internal node pops right and left and pushes left +
+  // right -- numpy's additions in numpy's order.  The stack lives in LDS (uniform
+  // depth, one slot per thread): no dependent round trip through memory per node.
+  // Depth <= log2(n / 128) + 2: 12 for the n whose n x n count matrix fits 288 GB.
   constexpr int kDepth = 16;
   __shared__ double stk[kDepth][2][MD_BLOCK];
   const int tid = threadIdx.x;
-#endif
   const int32_t nd = *n_deferred;
   const int64_t total = chunk_base[nd];
   for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {
     const int o = md_owner(chunk_base, nd, u);
     const MedoidMeta M = meta[o];
     const int n = M.n;
-    const int i = (int)(u - chunk_base[o]) * MD_BLOCK + threadIdx.x;
+    const int i = (int)(u - chunk_base[o]) * MD_BLOCK + tid;
     if (i >= n) continue;
-    const int32_t* prog = reinterpret_cast<const int32_t*>(arena + M.leaf_off) + (md_max_leaves(n) + 1) +
-                          md_max_leaves(n);
-    double* row = reinterpret_cast<double*>(arena + M.lsum_off) + i;
-    double* col = row + (int64_t)(2 * M.L - 1) * n;
-#if SPX_MD_COMB_STACK
-    if (n < (1 << 20)) {  // uniform
-    (void)prog;
+    const double* row = reinterpret_cast<const double*>(arena + M.lsum_off) + i;
+    const double* col = row + (int64_t)(2 * M.L - 1) * n;
     const int32_t* lnode = reinterpret_cast<const int32_t*>(arena + M.leaf_off) + (md_max_leaves(n) + 1);
     int sp = 0, kl = 0;
     for (int id = 0; id <= 2 * M.L - 2; ++id) {  // uniform
@@ -1788,20 +1765,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_combine_kernel(const MedoidMe
     const double t = ((0.0 + stk[0][0][tid]) + (0.0 + stk[0][1][tid])) / (double)n;
     reinterpret_cast<double*>(arena + M.tot_off)[i] = t;
     if (totals_out) totals_out[M.s0 + i] = t;
-    continue;
-    }
-#endif
-    {
-    for (int q = 0; q < M.L - 1; ++q) {
-      const int64_t l = prog[3 * q], r = prog[3 * q + 1], out = prog[3 * q + 2];
-      row[out * n] = row[l * n] + row[r * n];
-      col[out * n] = col[l * n] + col[r * n];
-    }
-    const int64_t root = 2 * M.L - 2;
-    const double t = ((0.0 + row[root * n]) + (0.0 + col[root * n])) / (double)n;
-    reinterpret_cast<double*>(arena + M.tot_off)[i] = t;
-    if (totals_out) totals_out[M.s0 + i] = t;
-    }
   }
 }
 

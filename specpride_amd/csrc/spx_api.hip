@@ -621,7 +621,7 @@ size_t medoid_cluster_bytes(int64_t n, int64_t p) {
   const int64_t L = spx::md_max_leaves(n);
   return (size_t)(spx::md_l1_bytes() + spx::md_align(B1 * 12 + 8) +
                   2 * spx::md_align(T * spx::MD_GT * KW * 8) +
-                  spx::md_align(n * n * 4) + spx::md_align((5 * L + 1) * 4) + spx::md_align(2 * (2 * L) * n * 8) +
+                  spx::md_align(n * n * 4) + spx::md_align((2 * L + 1) * 4) + spx::md_align(2 * (2 * L) * n * 8) +
                   spx::md_align(n * 8));
 }
 
