@@ -1201,10 +1201,11 @@ __device__ __forceinline__ int64_t md_xpose_tiles(const MedoidMeta& M) {  // 64 
 
 __global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
                                                                int64_t* tile_base, int64_t* unit_base,
-                                                               int64_t* chunk_base, int64_t* xpose_base) {
+                                                               int64_t* chunk_base, int64_t* xpose_base,
+                                                               int64_t* row_base) {
   __shared__ int64_t tmp[MD_BLOCK / kWave + 1];
   const int32_t nd = *n_deferred;
-  int64_t ct = 0, cu = 0, cc = 0, cx = 0;
+  int64_t ct = 0, cu = 0, cc = 0, cx = 0, cr = 0;
   for (int32_t i0 = 0; i0 < nd; i0 += MD_BLOCK) {
     const int32_t i = i0 + threadIdx.x;
     const bool ok = i < nd && meta[i].ok;
@@ -1222,8 +1223,18 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta*
     const int64_t ex = block_exclusive_scan<MD_BLOCK>(ok ? md_xpose_tiles(meta[i]) : int64_t(0), tmp, tot);
     if (i < nd) xpose_base[i] = cx + ex;
     cx += tot;
+    const int64_t er =
+        block_exclusive_scan<MD_BLOCK>(ok ? (int64_t)((meta[i].n + MD_GT - 1) / MD_GT * MD_GT) : 0, tmp, tot);
+    if (i < nd) row_base[i] = cr + er;
+    cr += tot;
   }
-  if (threadIdx.x == 0) { tile_base[nd] = ct; unit_base[nd] = cu; chunk_base[nd] = cc; xpose_base[nd] = cx; }
+  if (threadIdx.x == 0) {
+    tile_base[nd] = ct;
+    unit_base[nd] = cu;
+    chunk_base[nd] = cc;
+    xpose_base[nd] = cx;
+    row_base[nd] = cr;
+  }
 }
 
 
@@ -1235,8 +1246,12 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta*
 constexpr int MD_FILL_KW = 512;  // row words a wave builds in LDS (4 KB; 32,768 columns)
 constexpr int MD_FILL_U = 4;     // 64-peak chunks of a spectrum whose loads go out together
 
+#ifndef SPX_MD_FILL_FLAT
+#define SPX_MD_FILL_FLAT 1  // fill: each wave a contiguous run of the flat (cluster, row) list
+#endif
 __global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, MedoidParams P, const MedoidMeta* meta,
-                                                               const int32_t* n_deferred, char* arena) {
+                                                               const int32_t* n_deferred, const int64_t* row_base,
+                                                               char* arena) {
   const int32_t nd = *n_deferred;
   constexpr int W = MD_BLOCK / kWave;
 #if SPX_MD_FILL_LDS
@@ -1248,15 +1263,38 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, Medoid
   __shared__ unsigned long long lrow[W][MD_FILL_KW];
   unsigned long long* L = lrow[wave_id()];
 #endif
+#if SPX_MD_FILL_FLAT
+  // Every padded row of every deferred cluster, as one flat list (row_base: the
+  // exclusive scan of the padded row counts); wave q takes the contiguous run
+  // [q * per, (q + 1) * per), so the owner changes rarely and a giant's rows are
+  // spread over the whole grid instead of one y-slot of blocks (the old
+  // 64 x 32 grid walked the clusters 32 at a time: the n = 5,000 ones held it).
+  const int64_t total = row_base[nd];
+  const int64_t nwaves = (int64_t)gridDim.x * gridDim.y * W;
+  const int64_t per = (total + nwaves - 1) / nwaves;
+  const int64_t q = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * W + wave_id();
+  const int64_t g0 = q * per, g1 = g0 + per < total ? g0 + per : total;
+  int o = g0 < total ? md_owner(row_base, nd, g0) : 0;
+  for (int64_t g = g0; g < g1; ++g) {  // uniform per wave
+    while (g >= row_base[o + 1]) ++o;
+    const MedoidMeta M = meta[o];
+    if (!M.ok) continue;
+    const int r = (int)(g - row_base[o]);
+    const MedoidTables Tb = md_tables(arena, M);
+    unsigned long long* rows = reinterpret_cast<unsigned long long*>(arena + M.rows_off);
+#else
   for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
     const MedoidMeta M = meta[di];
     if (!M.ok) continue;
     const MedoidTables Tb = md_tables(arena, M);
     unsigned long long* rows = reinterpret_cast<unsigned long long*>(arena + M.rows_off);
     const int npad = (M.n + MD_GT - 1) / MD_GT * MD_GT;
+#endif
 #if SPX_MD_FILL_LDS
     if (M.KW <= MD_FILL_KW) {  // uniform
+#if !SPX_MD_FILL_FLAT
       for (int r = blockIdx.x * W + wave_id(); r < npad; r += gridDim.x * W) {
+#endif
         unsigned long long* row = rows + (int64_t)r * M.KW;
         for (int w = lane_id(); w < M.KW; w += kWave) L[w] = 0ull;
         if (r < M.n) {
@@ -1304,11 +1342,17 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, Medoid
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the next row's zeroing after these reads
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if !SPX_MD_FILL_FLAT
       }
+#endif
       continue;
     }
 #endif
+#if SPX_MD_FILL_FLAT
+    {
+#else
     for (int r = blockIdx.x * W + wave_id(); r < npad; r += gridDim.x * W) {
+#endif
       unsigned long long* row = rows + (int64_t)r * M.KW;
       for (int w = lane_id(); w < M.KW; w += kWave) row[w] = 0ull;
       if (r >= M.n) continue;

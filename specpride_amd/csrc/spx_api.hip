@@ -762,10 +762,12 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
   if (int rc = check_launch("medoid_l2_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_plan2_kernel, dim3(g), blk, 0, s, n_def, meta, arena, bump, arena_bytes, rep);
   if (int rc = check_launch("medoid_plan2_kernel")) return rc;
+  // row_base reuses pk_base (the peak passes are done with it)
+  int64_t* row_base = pk_base;
   hipLaunchKernelGGL(spx::medoid_scan_kernel, dim3(1), blk, 0, s, meta, n_def, tile_base, unit_base, chunk_base,
-                     xpose_base);
+                     xpose_base, row_base);
   if (int rc = check_launch("medoid_scan_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_fill_kernel, grid2, blk, 0, s, V, P, meta, n_def, arena);
+  hipLaunchKernelGGL(spx::medoid_fill_kernel, grid2, blk, 0, s, V, P, meta, n_def, row_base, arena);
   if (int rc = check_launch("medoid_fill_kernel")) return rc;
   hipLaunchKernelGGL(spx::medoid_transpose_kernel, dim3(4096), blk, 0, s, meta, n_def, xpose_base, arena);
   if (int rc = check_launch("medoid_transpose_kernel")) return rc;
