@@ -1195,8 +1195,12 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_plan2_kernel(const int32_t* n
 }
 
 // Exclusive scans of Gram tiles and leaf units over the deferred clusters (one workgroup).
-__device__ __forceinline__ int64_t md_xpose_tiles(const MedoidMeta& M) {  // 64 x 64-word transpose tiles
-  return (int64_t)((M.n + MD_GT - 1) / MD_GT * MD_GT / 64) * ((M.KW + 63) / 64);
+#ifndef SPX_MD_XP_ROWS
+#define SPX_MD_XP_ROWS 32  // transpose tiles of 32 rows x 64 words (16.6 KB of LDS: 9 workgroups per CU)
+#endif
+constexpr int MD_XPR = SPX_MD_XP_ROWS;
+__device__ __forceinline__ int64_t md_xpose_tiles(const MedoidMeta& M) {  // MD_XPR x 64-word transpose tiles
+  return (int64_t)((M.n + MD_GT - 1) / MD_GT * MD_GT / MD_XPR) * ((M.KW + 63) / 64);
 }
 
 __global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
@@ -1396,8 +1400,11 @@ constexpr int MD_GR_PF = SPX_GR_PF;  // words in flight per lane (divides 8: KW 
 // through LDS: both sides coalesced), for the register Gram's loads.
 __global__ __launch_bounds__(MD_BLOCK) void medoid_transpose_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
                                                                     const int64_t* xpose_base, char* arena) {
-  __shared__ unsigned long long tile[64][65];
-  const int tid = threadIdx.x, x = tid & 63, y0 = tid >> 6;
+  // tile = MD_XPR rows x 64 words: read as rows (lane = word), written as words (lane = row)
+  __shared__ unsigned long long tile[MD_XPR][65];
+  constexpr int RS = MD_BLOCK / 64;      // rows per read step
+  constexpr int WS = MD_BLOCK / MD_XPR;  // words per write step
+  const int tid = threadIdx.x;
   const int32_t nd = *n_deferred;
   const int64_t total = xpose_base[nd];
   for (int64_t g = blockIdx.x; g < total; g += gridDim.x) {  // every tile of every cluster, flat
@@ -1407,16 +1414,22 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_transpose_kernel(const Medoid
     const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(arena + M.rows_off);
     unsigned long long* rowsT = reinterpret_cast<unsigned long long*>(arena + M.rowsT_off);
     const int tw = (KW + 63) / 64;
+    const int t = (int)(g - xpose_base[o]);
+    const int r0 = (t / tw) * MD_XPR, w0 = (t % tw) * 64;
     {
-      const int t = (int)(g - xpose_base[o]);
-      const int r0 = (t / tw) * 64, w0 = (t % tw) * 64;
-      for (int y = y0; y < 64; y += MD_BLOCK / 64)
+      const int x = tid & 63, y0 = tid >> 6;
+#pragma unroll
+      for (int y = y0; y < MD_XPR; y += RS)
         tile[y][x] = w0 + x < KW ? rows[(int64_t)(r0 + y) * KW + w0 + x] : 0ull;
-      __syncthreads();
-      for (int y = y0; y < 64; y += MD_BLOCK / 64)
-        if (w0 + y < KW) rowsT[(int64_t)(w0 + y) * npad + r0 + x] = tile[x][y];
-      __syncthreads();
     }
+    __syncthreads();
+    {
+      const int x = tid % MD_XPR, y0 = tid / MD_XPR;
+#pragma unroll
+      for (int y = y0; y < 64; y += WS)
+        if (w0 + y < KW) rowsT[(int64_t)(w0 + y) * npad + r0 + x] = tile[x][y];
+    }
+    __syncthreads();
   }
 }
 __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(const MedoidMeta* meta, const int32_t* n_deferred,
