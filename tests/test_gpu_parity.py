@@ -757,6 +757,25 @@ def test_medoid_large_path_row_widths(gpu):
     np.testing.assert_array_equal(tot, ref_tot)
 
 
+def test_medoid_large_path_pairwise_tree_shapes(gpu):
+    """The large path's totals follow numpy's pairwise tree over n (leaves of <= 128,
+    splits at n/2 - (n/2) % 8): medoid_plan2_kernel numbers the leaves and internal
+    nodes in post-order by descents from the root, medoid_combine_kernel evaluates the
+    tree as a stack machine over those ids.  n at and around every leaf / split boundary
+    up to three levels (65 .. 513 spectra of short spectra, so the flat unit and row
+    grids hold many small deferred clusters), between ordinary small clusters:
+    representatives and totals bit-exact vs the C oracle."""
+    ns = [65, 127, 128, 129, 135, 136, 137, 255, 256, 257, 263, 264, 265, 511, 512, 513]
+    sizes = []
+    for n in ns:
+        sizes += [n, 3]
+    csr = make_clusters_np(len(sizes), seed=313, sizes=np.array(sizes), n_template=24)
+    rep, tot = engine.medoid(engine.DeviceBatch.from_host(csr), with_totals=True).to_host()
+    ref_rep, ref_tot = c_oracle.medoid_parallel(csr, with_totals=True)
+    np.testing.assert_array_equal(rep, ref_rep)
+    np.testing.assert_array_equal(tot, ref_tot)
+
+
 # ------------------------------------------------------- gather wire format
 def _wire_roundtrip(mz, it, max_count):
     import torch
