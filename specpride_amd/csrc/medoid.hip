@@ -188,28 +188,31 @@ __device__ __forceinline__ void md_defer(int64_t c, int64_t s0, int n, int32_t* 
 
 // ---------------------------------------------------------- small clusters
 // medoid_reg_kernel: every m/z read from HBM exactly ONCE (8 B per peak, the algorithmic minimum) and the
-// per-peak LDS traffic cut to two operations:
+// per-peak LDS traffic cut to four operations:
 //   P1  flat coalesced pass over the cluster's peaks (peak r = u*256 + tid,
-//       8 loads in flight per thread): absolute bin ceil(mz/tol) < 65,536, kept
+//       8 loads in flight per thread): absolute bin ceil(mz/tol) < 32,768, kept
 //       in registers as packed u16 (<= MR_UMAX per thread), union bitmap in LDS
-//       (32-bit LDS atomics).  The xcorr is a set intersection: no range pass,
-//       and unsorted spectra need no special path.
-//   P2  popcount prefix -> K compact columns (dense word and prefix arrays:
-//       bank-conflict-light ORs and rank reads)
-//   P3  bit-packed rows from the register bins: column = rank (two LDS reads),
-//       spectrum = the wave's start-bit word and its prefix, handed out by
-//       readlane (a wave's 64 peaks of a slice are one start-bit word); rows
-//       are set by 32-bit LDS atomics (neighbouring peaks share a row word)
-//   P4  one thread per pair i <= j: c_ij = popcount(row_i & row_j) into
-//       registers, then d_ij = 1 - c_ij/min(p_i, p_j) (one IEEE divide per pair)
-//       into the reference's n x n matrix (upper triangle incl. the diagonal,
-//       zeros below: most_similar_representative.py:91-93), aliasing the dead
-//       bitmap and rows
-//   P5  totals with numpy's pairwise tree (:98-100): 16 lanes per spectrum --
-//       8 accumulators of row i, 8 of column i -- combined
-//       ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) by shuffles, sequential tail,
-//       total = (row + col)/n
-//   P6  lowest index of the minimum (:103-110), one wave
+//       (32-bit LDS atomics).  Branch-free per batch of 8 (SPX_MD_P1B): the
+//       reciprocal product's ceil where certain and in range, one "bad" mask
+//       settled by md_bin's exact divide once per batch.  The xcorr is a set
+//       intersection: no range pass, and unsorted spectra need no special path.
+//   P2  popcount prefix -> K compact columns (SPX_MD_R32: a u16 prefix per
+//       32-bit occupancy word)
+//   P3  bit-packed rows from the register bins: column = rank (a u16 prefix and
+//       one bfe + popcount), spectrum = the slice's spectrum-end word and its
+//       prefix handed out by readlane, counted by two v_mbcnt (SPX_MD_MBC); rows
+//       set by 32-bit LDS atomics into words swizzled per bit position
+//       (SPX_MD_SWZ: a spectrum's neighbouring columns -- consecutive lanes --
+//       no longer serialise on one word)
+//   P4  pair counts: past 32 spectra on the matrix cores (FP4 0/1 Gram tiles, one
+//       per wave, SPX_MD_MFMA), else one thread per pair i <= j by AND + popcount;
+//       then d_ij = 1 - c_ij/min(p_i, p_j) (exact reciprocal form, md_dist_r) into
+//       the reference's n x n matrix (upper triangle incl. the diagonal, zeros
+//       below: most_similar_representative.py:91-93), aliasing the dead bitmap and rows
+//   P5  totals with numpy's pairwise tree (:98-100): one lane per spectrum, wave 0
+//       the rows, wave 1 the columns (8 strided accumulators combined
+//       ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), sequential tail), total = (row + col)/n
+//   P6  lowest index of the minimum (:103-110), wave 0 straight from P5's registers
 // Deferred (to the wide kernel, then the large path): n > 64, > MR_UMAX*256 peaks, a bin outside
 // [0, 65,536), > 64 * MD_KWMAX distinct bins.
 constexpr int MR_UMAX = 48;                  // peaks per thread (12,288 per cluster)
