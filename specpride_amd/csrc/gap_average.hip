@@ -1061,8 +1061,9 @@ __global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v
 // Scratch slice of the deferred path: every array starts 256-B aligned (the
 // 64-bit atomics on kmin/kmax fault on a misaligned address).
 struct GapSliceLayout {
-  int64_t bitmap, wprefix, cnt, gcnt, kmin, kmax, flags, total;
+  int64_t bitmap, wprefix, cnt, gcnt, kmin, kmax, flags, chunks, total;
 };
+constexpr int GA_GCH = 8 * GA_BLOCK;  // slots per chunk of the giants' flat step-4 passes
 __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
   GapSliceLayout L;
   int64_t o = 0;
@@ -1074,6 +1075,7 @@ __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
   L.kmin = take((int64_t)dcap * 8);
   L.kmax = take((int64_t)dcap * 8);
   L.flags = take((int64_t)dcap * 4);
+  L.chunks = take(((int64_t)dcap / GA_GCH + 2) * 4);  // step 4's per-chunk gap counts, then bases
   L.total = o;
   return L;
 }
@@ -1107,6 +1109,12 @@ constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS f
 #ifndef SPX_GA_HASH
 #define SPX_GA_HASH 1
 #endif
+#ifndef SPX_GA_FLAT4
+#define SPX_GA_FLAT4 1  // giants' step 4 over a flat (giant, chunk) grid (gap_giant_groups_kernel)
+#endif
+#ifndef SPX_GA_FLAT6
+#define SPX_GA_FLAT6 1  // giants' step 6 (emit) over the same flat grid; the per-giant step keeps the precursor
+#endif
 #ifndef SPX_GA_HASH3
 #define SPX_GA_HASH3 1  // pass 3 too: a tile's per-slot m/z extents in an LDS table, one global min/max per (tile, slot)
 #endif
@@ -1119,7 +1127,9 @@ constexpr int GA_HPROBE = 16;
 struct GapGiant {  // zeroed by the call's memset
   unsigned long long lo_inv, hi_key, imax_key;  // ~order key of the min m/z, order keys of max m/z, max |intensity|
   long long off;                                // its arena slice
-  int32_t c, dcap, ok, bad, status, D, E, pad;
+  int32_t c, dcap, ok, bad, status, D, E, pad;  // pad: step 4a's "a bucket spans mz_accuracy" flag (SPX_GA_FLAT4)
+  unsigned long long gmax_key;  // step 6a (SPX_GA_FLAT6): order key of the largest kept group intensity
+  int32_t gany, pad2;           // step 6a: some group has >= min_fraction spectra
 };
 
 struct GiantArgs {
@@ -1130,6 +1140,9 @@ struct GiantArgs {
   int gmax;
   char* arena;
   int wcap;
+  double* out_mz;     // step 6 over the flat grid (SPX_GA_FLAT6): the consensus outputs
+  double* out_int;
+  int64_t* out_count;
 };
 
 __device__ __forceinline__ GapState<uint32_t> gap_slice_state(char* base, int wcap, int dcap) {
@@ -1823,7 +1836,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, P
       }
       if (tid == 0) { H.D = D; H.status = st; }
     } else if constexpr (STEP == 4) {
-      if (st != kOk) continue;
+      if (SPX_GA_FLAT4 || st != kOk) continue;  // (SPX_GA_FLAT4: gap_giant_groups_kernel)
       int E = 0;
       st = gap_groups<false>(S, A.P, H.D, tmp, votes, E);
       if (tid == 0) { H.E = E; H.status = st; }
@@ -1834,11 +1847,19 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, P
         st = gap_body_nf(A.v, A.P, S, c, out, tmp, red, votes, reinterpret_cast<uint32_t*>(stage));
         __syncthreads();
       } else if (st == kOk) {
+#if SPX_GA_FLAT6
+        // the groups were emitted by gap_giant_groups_kernel<4..7>
+        (void)n;
+        (void)N;
+        (void)p0;
+        st = H.gany ? kOk : kEmpty;
+#else
         const GiantExtent X = giant_extent(H, A.P);
         int ex_m, ex_i;
         frexp(fmax(fabs(X.lo), fabs(X.hi)) * (double)N, &ex_m);
         frexp(X.imax * (double)N, &ex_i);
         st = gap_emit<false>(S, A.P, c, n, N, p0, H.E, 61 - ex_m, 61 - ex_i, out, tmp, red, votes);
+#endif
       }
       if (st == kDeferred) {
         if (tid == 0) { status[c] = kDeferred; atomicAdd(unresolved, 1); }
@@ -1848,6 +1869,208 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, P
       }
     }
     __syncthreads();  // the LDS is reused by the next giant
+  }
+}
+
+// Step 4 of the giants over a flat (giant, chunk of GA_GCH slots) space instead of one
+// workgroup per giant (whose 56 rounds of block scans over a 229k-slot giant made it a
+// latency chain, 0.24 ms for the skewed configs[3] batch): (a) per chunk, the gaps
+// inside it and any bucket wider than mz_accuracy; (b) per giant, the chunks' exclusive
+// bases, the group count E and the status; (c) per chunk, each slot's emitted group
+// and the group counts; (d) per chunk of E, the group-sum words zeroed (after (c) has
+// read every slot's extent).  The same gaps, groups and counts as gap_groups<false>.
+// LDS prefix over the giants of their chunk counts (of D slots, or of E groups);
+// pre[ng] = the total.  Call with the whole workgroup.
+__device__ __forceinline__ int giant_chunk_prefix(const GiantArgs& A, int* pre, int* tmp, bool of_groups) {
+  const int ng = min(*A.n_giant, A.gmax);
+  const int t = threadIdx.x;
+  int cnt = 0;
+  if (t < ng) {
+    const GapGiant& H = A.giants[t];
+    if (H.ok && !H.bad && H.status == kOk) cnt = ((of_groups ? H.E : H.D) + GA_GCH - 1) / GA_GCH;
+  }
+  int total;
+  const int e = block_exclusive_scan<GA_BLOCK, int>(cnt, tmp, total);
+  if (t < ng) pre[t] = e;
+  if (t == 0) pre[ng] = total;
+  __syncthreads();
+  return ng;
+}
+__device__ __forceinline__ int giant_chunk_owner(const int* pre, int ng, int t) {
+  int lo = 0, hi = ng;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (pre[mid] <= t) lo = mid; else hi = mid;
+  }
+  while (lo + 1 < ng && pre[lo + 1] <= t) ++lo;
+  return lo;
+}
+
+template <int PART>
+__global__ __launch_bounds__(GA_BLOCK) void gap_giant_groups_kernel(GiantArgs A) {
+  static_assert(GA_GMAX <= GA_BLOCK, "one thread per giant record");
+  __shared__ int pre[GA_GMAX + 1];
+  __shared__ int tmp[GA_NW + 1];
+  __shared__ int votes[2 * GA_NW];
+  const int tid = threadIdx.x;
+  const double acc = A.P.mz_accuracy;
+  auto key = [&](const uint64_t* a, int d) { return f64_from_order_key(a[d]); };
+  if constexpr (PART == 6) {  // (6c) one workgroup per giant: the kept groups' output bases, the count
+    const int ng = min(*A.n_giant, A.gmax);
+    for (int g = blockIdx.x; g < ng; g += gridDim.x) {
+      GapGiant& H = A.giants[g];
+      if (!H.ok || H.bad || H.status != kOk || !H.gany) continue;  // uniform
+      const GapSliceLayout Lo = gap_slice_layout(A.wcap, H.dcap);
+      int* ch = reinterpret_cast<int*>(A.arena + H.off + Lo.chunks);
+      const int nch = (H.E + GA_GCH - 1) / GA_GCH;
+      if (tid < kWave) {
+        int carry = 0;
+        for (int k0 = 0; k0 < nch; k0 += kWave) {
+          const int k = k0 + tid;
+          const int x = k < nch ? ch[k] : 0;
+          const int inc = wave_inclusive_sum(x);
+          if (k < nch) ch[k] = carry + inc - x;
+          carry += __shfl(inc, kWave - 1, kWave);
+        }
+        if (tid == 0) A.out_count[H.c] = carry;
+      }
+    }
+    return;
+  } else if constexpr (PART == 1) {  // (b) one workgroup per giant: the chunk bases, E, the status
+    const int ng = min(*A.n_giant, A.gmax);
+    for (int g = blockIdx.x; g < ng; g += gridDim.x) {
+      GapGiant& H = A.giants[g];
+      if (!H.ok || H.bad || H.status != kOk) continue;  // uniform
+      const GapSliceLayout Lo = gap_slice_layout(A.wcap, H.dcap);
+      int* ch = reinterpret_cast<int*>(A.arena + H.off + Lo.chunks);
+      const int nch = (H.D + GA_GCH - 1) / GA_GCH;
+      if (tid < kWave) {
+        int carry = 0;
+        for (int k0 = 0; k0 < nch; k0 += kWave) {
+          const int k = k0 + tid;
+          const int x = k < nch ? ch[k] : 0;
+          const int inc = wave_inclusive_sum(x);
+          if (k < nch) ch[k] = carry + inc - x;
+          carry += __shfl(inc, kWave - 1, kWave);
+        }
+        if (tid == 0) {
+          const int m_gaps = carry;
+          if (H.pad) H.status = kDeferred;  // a bucket spans mz_accuracy
+          else if (m_gaps == 0) H.status = kNoGap;
+          else H.E = m_gaps >= 2 ? m_gaps : 2;
+        }
+      }
+    }
+    return;
+  } else {
+    const int ng = giant_chunk_prefix(A, pre, tmp, PART >= 3);
+    const int total = pre[ng];
+    for (int t = blockIdx.x; t < total; t += gridDim.x) {  // uniform
+      const int g = giant_chunk_owner(pre, ng, t);
+      GapGiant& H = A.giants[g];
+      const int k = t - pre[g];
+      const GapState<uint32_t> S = gap_slice_state(A.arena + H.off, A.wcap, H.dcap);
+      const GapSliceLayout Lo = gap_slice_layout(A.wcap, H.dcap);
+      int* ch = reinterpret_cast<int*>(A.arena + H.off + Lo.chunks);
+      const int D = H.D;
+      const int db = k * GA_GCH + tid * 8;
+      if constexpr (PART == 3) {  // (d) the group-sum words
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int e = db + q;
+          if (e < H.E) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
+        }
+        continue;
+      }
+      if constexpr (PART >= 4) {  // step 6 over chunks of the E groups (gap_emit's three sweeps)
+        const int64_t c = H.c;
+        const int64_t s0 = A.v.cluster_off[c], n = A.v.cluster_off[c + 1] - s0;
+        const int64_t p0 = A.v.spec_off[s0], N = A.v.spec_off[A.v.cluster_off[c + 1]] - p0;
+        const GiantExtent X = giant_extent(H, A.P);
+        int ex_m, ex_i;
+        frexp(fmax(fabs(X.lo), fabs(X.hi)) * (double)N, &ex_m);
+        frexp(X.imax * (double)N, &ex_i);
+        const int sc_m = 61 - ex_m, sc_i = 61 - ex_i;
+        const double min_len = A.P.min_fraction * (double)n;
+        const int E = H.E;
+        auto isum = [&](int e) -> double { return ldexp((double)(int64_t)S.kmax[e], -sc_i); };
+        if constexpr (PART == 4) {  // (6a) the largest kept group intensity, any kept group
+          double gm = -__longlong_as_double(0x7ff0000000000000ll);
+          int anyg = 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int e = db + q;
+            if (e < E && (double)S.gcnt[e] >= min_len) {
+              gm = fmax(gm, isum(e) / (double)n);
+              anyg = 1;
+            }
+          }
+          gm = wave_max_dpp(gm);
+          const unsigned long long any_w = __ballot(anyg);
+          if (lane_id() == 0 && any_w) {
+            atomicMax(&H.gmax_key, f64_order_key(gm));
+            atomicOr(&H.gany, 1);
+          }
+          continue;
+        }
+        if (!H.gany) continue;  // uniform: kEmpty (the per-giant step reports it)
+        const double thr = f64_from_order_key(H.gmax_key) / A.P.dyn_range;
+        int keep[8], mine = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int e = db + q;
+          keep[q] = e < E && (double)S.gcnt[e] >= min_len && isum(e) / (double)n >= thr;
+          mine += keep[q];
+        }
+        int tot;
+        const int ex = block_exclusive_scan<GA_BLOCK, int>(mine, tmp, tot);
+        if constexpr (PART == 5) {  // (6b) kept groups per chunk
+          if (tid == 0) ch[k] = tot;
+        } else {  // (6d) the kept groups in order
+          int o = ch[k] + ex;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int e = db + q;
+            if (keep[q]) {
+              SPX_GUARD(o < N, "giant out c=%ld o=%d N=%ld\n", (long)c, o, (long)N)
+              A.out_mz[p0 + o] = ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e];
+              A.out_int[p0 + o] = isum(e) / (double)n;
+              ++o;
+            }
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+      int f[8], mine = 0, split = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {  // f[q]: a gap between slots d - 1 and d
+        const int d = db + q;
+        f[q] = d > 0 && d < D && (key(S.kmin, d) - key(S.kmax, d - 1)) >= acc;
+        mine += f[q];
+        if constexpr (PART == 0) split |= d < D && (key(S.kmax, d) - key(S.kmin, d)) >= acc;
+      }
+      int tot;
+      const int ex = block_exclusive_scan<GA_BLOCK, int>(mine, tmp, tot);
+      if constexpr (PART == 0) {  // (a)
+        if (block_any<GA_BLOCK, false>(split, votes, 1) && tid == 0) atomicOr(&H.pad, 1);
+        if (tid == 0) ch[k] = tot;
+      } else {  // (c)
+        int gg = ch[k] + ex;
+        const int E = H.E;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int d = db + q;
+          if (d < D) {
+            gg += f[q];
+            const int eg = min(gg, E - 1);
+            if (const uint32_t k_cnt = S.cnt[d]) atomicAdd(&S.gcnt[eg], k_cnt);  // giants count in pass 5
+            S.cnt[d] = (uint32_t)eg;
+          }
+        }
+      }
+      __syncthreads();  // tmp / votes reused by the next chunk
+    }
   }
 }
 

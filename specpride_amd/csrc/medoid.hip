@@ -487,7 +487,9 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
     if (lane < UMAX && w < nsw) { my_sw = L.u.a.sbits[w]; my_sp = L.u.a.spre[w]; }
   }
   __syncthreads();
+#if !SPX_MD_MBC
   const unsigned long long upto = (2ull << lane) - 1ull;  // bits 0..lane
+#endif
 #if SPX_MD_SWZ
   const uint32_t swz_nw = 2u * (uint32_t)KW;  // 32-bit words per row
   const uint32_t swz_m = swz_nw >= 32u ? 31u : (1u << (31 - __clz((int)swz_nw))) - 1u;  // 2^k - 1 < swz_nw
@@ -650,7 +652,9 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   __syncthreads();
   // D(a, b) of the reference's dense matrix: the upper triangle incl. the
   // diagonal, zeros below (most_similar_representative.py:91-93)
+#if !SPX_MD_P5L
   auto dval = [&](int a, int b) -> double { return b >= a ? L.u.d[row_start(a) + b - a] : 0.0; };
+#endif
 
   SPX_STAMP(5);
 #if SPX_MD_P5L

@@ -593,16 +593,29 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   if (int rc = check_launch("gap_average_global_kernel")) return rc;
   if (arena_bytes == 0) return SPX_SUCCESS;  // no cluster of this batch can be a giant
   // the giant clusters' pipeline
-  const spx::GiantArgs A{V, P2, giants, n_giant, gmax, arena, wcap};
+  const spx::GiantArgs A{V, P2, giants, n_giant, gmax, arena, wcap, O.mz, O.inten, O.count};
   const dim3 tiles(spx::GA_GIANT_GRID), per(gmax), blk(spx::GA_BLOCK);
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<1>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<2>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_step_kernel<0>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
                      unresolved);
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<3>, tiles, blk, 0, s, A);
+#if SPX_GA_FLAT4
+  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<0>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<1>, per, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<2>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<3>, tiles, blk, 0, s, A);
+#else
   hipLaunchKernelGGL(spx::gap_giant_step_kernel<4>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
                      unresolved);
+#endif
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<5>, tiles, blk, 0, s, A);
+#if SPX_GA_FLAT6
+  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<4>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<5>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<6>, per, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<7>, tiles, blk, 0, s, A);
+#endif
   hipLaunchKernelGGL(spx::gap_giant_step_kernel<6>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
                      unresolved);
   return check_launch("gap_giant pipeline");
