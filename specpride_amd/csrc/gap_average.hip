@@ -56,6 +56,9 @@ constexpr int GA_NW = GA_BLOCK / kWave;
 #define SPX_GA_UM 20
 #endif
 constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10,240 per cluster: n <= 51 at ~200 peaks)
+#ifndef SPX_GA_WMAXN
+#define SPX_GA_WMAXN 65536  // the wide kernel hands clusters of more peaks than this to the giant pipeline (0: none)
+#endif
 #ifndef SPX_GA_DEFERBIG
 #define SPX_GA_DEFERBIG 1  // the LDS kernel hands clusters past its register capacity on unread
 #endif
@@ -1045,6 +1048,12 @@ __global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v
   for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
     const int64_t c = striped_at(list, lbase, i);
     const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
+    if (SPX_GA_WMAXN > 0 && pn >= 2 && v.spec_off[ps0 + pn] - v.spec_off[ps0] > (int64_t)SPX_GA_WMAXN) {  // uniform
+      // too many peaks for one CU (the hybrid path re-reads its tail every pass): to the
+      // global kernel, which hands it to the giant pipeline spread over the grid
+      if (threadIdx.x == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+      continue;
+    }
     PrecLanes pl{0, 0.0, 0.0};
     if (pn <= kWave) pl = prec_lanes(v, ps0, pn);
     const int32_t st = gap_body<GA_WUM, false>(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
