@@ -1121,6 +1121,9 @@ constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS f
 #ifndef SPX_GA_FLAT4
 #define SPX_GA_FLAT4 1  // giants' step 4 over a flat (giant, chunk) grid (gap_giant_groups_kernel)
 #endif
+#ifndef SPX_GA_TPERM
+#define SPX_GA_TPERM 1  // giant passes 2 and 3: tiles in a scattered order (different giants side by side)
+#endif
 #ifndef SPX_GA_FLAT6
 #define SPX_GA_FLAT6 1  // giants' step 6 (emit) over the same flat grid; the per-giant step keeps the precursor
 #endif
@@ -1527,6 +1530,31 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
   int g = 0, cur = -1, E = 0, sc_m = 0, sc_i = 0;
   bool agg = false, hashed = false;
   int64_t gbase = 0, gtiles = ng > 0 ? tiles_of(A.giants[0]) : 0, p0 = 0, p1 = 0, kb = 0;
+#if SPX_GA_TPERM
+  // passes 2 and 3 take the tiles in a scattered order (t = u * P mod T): consecutive
+  // workgroups then work on different giants instead of 512 neighbouring tiles of one,
+  // whose per-tile flushes all hit the same template slots of one slice at once
+  constexpr bool kPerm = PASS == 2 || PASS == 3;
+  __shared__ long long tpre[kPerm ? GA_GMAX + 1 : 1];
+  __shared__ long long ttmp[kPerm ? GA_NW + 1 : 1];
+  long long tT = 0, tP = 1;
+  if constexpr (kPerm) {
+    const int64_t tc = tid < ng ? tiles_of(A.giants[tid]) : 0;
+    long long tot;
+    const long long e = block_exclusive_scan<GA_BLOCK, long long>((long long)tc, ttmp, tot);
+    if (tid < ng) tpre[tid] = e;
+    if (tid == 0) tpre[ng] = tot;
+    __syncthreads();
+    tT = tpre[ng];
+    // a multiplier coprime to T (T < 2^31 tiles)
+    const long long cands[4] = {40503, 65521, 7919, 1};
+    for (int q = 0; q < 4; ++q) {
+      long long a = cands[q], b = tT > 0 ? tT : 1;
+      while (b) { const long long r = a % b; a = b; b = r; }
+      if (a == 1) { tP = cands[q]; break; }
+    }
+  }
+#endif
   GapState<uint32_t> S{};
   // the hashed table after a tile: every occupied entry to the slice, the table emptied
   auto hflush = [&]() __attribute__((always_inline)) {
@@ -1563,12 +1591,30 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
       }
     }
   };
-  for (int64_t u = blockIdx.x;; u += gridDim.x) {  // uniform
-    while (g < ng && u >= gbase + gtiles) {
-      gbase += gtiles;
-      if (++g < ng) gtiles = tiles_of(A.giants[g]);
+  for (int64_t u0 = blockIdx.x;; u0 += gridDim.x) {  // uniform
+    int64_t u = u0;
+#if SPX_GA_TPERM
+    if constexpr (kPerm) {
+      if (u0 >= tT) break;
+      u = (int64_t)(((unsigned long long)u0 * (unsigned long long)tP) % (unsigned long long)tT);
+      int lo = 0, hi = ng;  // the giant with tpre[g] <= u < tpre[g + 1]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tpre[mid] <= u) lo = mid; else hi = mid;
+      }
+      while (lo + 1 < ng && tpre[lo + 1] <= u) ++lo;
+      g = lo;
+      gbase = tpre[g];
+      gtiles = tpre[g + 1] - tpre[g];
+    } else
+#endif
+    {
+      while (g < ng && u >= gbase + gtiles) {
+        gbase += gtiles;
+        if (++g < ng) gtiles = tiles_of(A.giants[g]);
+      }
+      if (g >= ng) break;
     }
-    if (g >= ng) break;
     const GapGiant& H = A.giants[g];
     if (g != cur) {  // this workgroup's first tile of giant g
       flush();
