@@ -1122,7 +1122,7 @@ constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS f
 #define SPX_GA_FLAT4 1  // giants' step 4 over a flat (giant, chunk) grid (gap_giant_groups_kernel)
 #endif
 #ifndef SPX_GA_TPERM
-#define SPX_GA_TPERM 1  // giant passes 2 and 3: tiles in a scattered order (different giants side by side)
+#define SPX_GA_TPERM 2  // giant tile passes (1: passes 2-3 only, 2: all): tiles in a scattered order (different giants side by side)
 #endif
 #ifndef SPX_GA_FLAT6
 #define SPX_GA_FLAT6 1  // giants' step 6 (emit) over the same flat grid; the per-giant step keeps the precursor
@@ -1534,7 +1534,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
   // passes 2 and 3 take the tiles in a scattered order (t = u * P mod T): consecutive
   // workgroups then work on different giants instead of 512 neighbouring tiles of one,
   // whose per-tile flushes all hit the same template slots of one slice at once
-  constexpr bool kPerm = PASS == 2 || PASS == 3;
+  constexpr bool kPerm = (PASS == 2 || PASS == 3) || (SPX_GA_TPERM >= 2 && (PASS == 1 || PASS == 5));
   __shared__ long long tpre[kPerm ? GA_GMAX + 1 : 1];
   __shared__ long long ttmp[kPerm ? GA_NW + 1 : 1];
   long long tT = 0, tP = 1;
