@@ -1130,6 +1130,9 @@ constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS f
 #ifndef SPX_GA_HASH3
 #define SPX_GA_HASH3 1  // pass 3 too: a tile's per-slot m/z extents in an LDS table, one global min/max per (tile, slot)
 #endif
+#ifndef SPX_GA_NOFILT
+#define SPX_GA_NOFILT 1  // giant passes 2-3: the tile flushes issue their atomics without reading the slice first (memory-side atomics: the read is a fabric round trip of its own)
+#endif
 #ifndef SPX_GA_HASH2
 #define SPX_GA_HASH2 1  // pass 2 too: a tile's bitmap words OR-ed in an LDS table, one global OR per (tile, word)
 #endif
@@ -1779,14 +1782,14 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           if (k) {
             if constexpr (PASS == 2) {
               const unsigned long long bits = agg_m[h];
-              if ((S.bitmap[k - 1u] & bits) != bits) atomicOr(&S.bitmap[k - 1u], bits);
+              if (SPX_GA_NOFILT || (S.bitmap[k - 1u] & bits) != bits) atomicOr(&S.bitmap[k - 1u], bits);
               agg_m[h] = 0ull;
             } else {
               unsigned long long* kmin = reinterpret_cast<unsigned long long*>(&S.kmin[k - 1u]);
               unsigned long long* kmax = reinterpret_cast<unsigned long long*>(&S.kmax[k - 1u]);
               const unsigned long long lo = agg_m[h], hi = agg_i[h];
-              if (lo < *kmin) atomicMin(kmin, lo);
-              if (hi > *kmax) atomicMax(kmax, hi);
+              if (SPX_GA_NOFILT || lo < *kmin) atomicMin(kmin, lo);
+              if (SPX_GA_NOFILT || hi > *kmax) atomicMax(kmax, hi);
               agg_m[h] = ~0ull;
               agg_i[h] = 0ull;
             }
