@@ -71,6 +71,12 @@ constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10
 #ifndef SPX_GA_P3INT
 #define SPX_GA_P3INT 0  // the LDS kernel reads the intensities in pass 3 instead of pass 1
 #endif
+#ifndef SPX_GA_BSKIP
+#define SPX_GA_BSKIP 2  // register rows: a batch of 8 rows no peak of the cluster reaches is skipped whole, passes (1) and m/z loads (2)
+#endif
+#ifndef SPX_GA_P2B
+#define SPX_GA_P2B 1  // pass 2 over the register rows: buckets by batches of 8, the exact division once per batch if needed
+#endif
 #ifndef SPX_GA_EARLY
 #define SPX_GA_EARLY 1  // wide kernel: intensities streamed during the bucket pass, bitmap zeroed under the m/z loads
 #endif
@@ -679,10 +685,20 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   for (int q = 0; q < UM; ++q) tags[q] = 0u;
   if (regs) {
 #pragma unroll
-    for (int u = 0; u < UM; ++u) {
-      const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
-      const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
-      rm[u] = N > 0 ? v.mz[kk] : 0.0;
+    for (int u0 = 0; u0 < UM; u0 += 8) {
+      // SPX_GA_BSKIP >= 2: a batch of rows no peak reaches is not loaded (uniform; the
+      // batch's loads stay together)
+      const bool live = SPX_GA_BSKIP < 2 || (int64_t)u0 * GA_BLOCK < N;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int u = u0 + q;
+        if (u < UM) {
+          const int64_t k = p0 + (int64_t)u * GA_BLOCK + tid;
+          const int64_t kk = k < p1 ? k : (N > 0 ? p0 : 0);
+          if (live) rm[u] = N > 0 ? v.mz[kk] : 0.0;
+          else rm[u] = 0.0;
+        }
+      }
     }
   }
   if (prank && pl && n <= kWave) {  // uniform: every wave's share of the precursor ranks
@@ -700,6 +716,9 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       if (N == 0) return;  // uniform: no peaks (and the batch may hold none to load)
 #pragma unroll
       for (int u0 = 0; u0 < UM; u0 += 8) {
+#if SPX_GA_BSKIP
+        if ((int64_t)u0 * GA_BLOCK >= N) break;  // uniform: no peak in rows u0.. (their tags stay 0)
+#endif
         double itb[8];
         if constexpr (kInten) {
 #pragma unroll
@@ -897,7 +916,59 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
       atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
     };
+#if SPX_GA_P2B
+    if (regs && N > 0) {  // uniform
+#pragma unroll
+      for (int u0 = 0; u0 < UM; u0 += 8) {
+#if SPX_GA_BSKIP
+        if ((int64_t)u0 * GA_BLOCK >= N) break;  // uniform
+#endif
+        // the reciprocal product's floor for all 8 rows (a lane past the cluster bins its
+        // clamped copy of peak 0: never used); where it is not certain, one divide below
+        uint32_t badm = 0u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int u = u0 + q;
+          if (u < UM) {
+            const double qv = rm[u] * P.inv_bucket_w;
+            const double t = floor(qv);
+            const double fr = qv - t;
+            const bool sure = (fabs(qv) < kDivFastLimit) & (fr > kDivBand) & (fr < 1.0 - kDivBand);
+            badm |= (uint32_t)!sure << q;
+            tags[u] = (uint32_t)((int64_t)__double2int_rz(t) - kb);
+          }
+        }
+        if (__builtin_expect(badm != 0u, 0)) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int u = u0 + q;
+            if (u < UM && ((badm >> q) & 1u)) tags[u] = (uint32_t)((int64_t)floor(rm[u] / P.bucket_w) - kb);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int u = u0 + q;
+          if (u < UM && p0 + (int64_t)u * GA_BLOCK + tid < p1) {
+            const int32_t b = (int32_t)tags[u];
+            SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%d nw=%ld\n", (long)c, b, (long)nw)
+            atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
+          }
+        }
+      }
+      if constexpr (kHy) {
+        if (hyb) {
+          gap_peaks<false>(v, ptail, p1, [&](int64_t, double m, double) {
+            int32_t tag = 0;
+            pass2(m, 0.0, tag, std::false_type{});
+          });
+        }
+      }
+    } else {
+      peaks_m_tag(pass2);
+    }
+#else
     peaks_m_tag(pass2);
+#endif
     bar();
   }
   int D;
