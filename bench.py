@@ -70,37 +70,207 @@ def parse():
     return ap.parse_args()
 
 
-def dist_init():
+class HipBackend:
+    """The product path of one rank: the HIP engine on ``cuda:LOCAL_RANK`` (inputs
+    generated in HBM), RCCL between ranks.  bench.py's step, timing and gather code
+    only talks to a backend through these methods; the CPU test suite swaps in a
+    stand-in (``SPX_BENCH_BACKEND``, tests/bench_oracle_backend.py) to drive the
+    launcher, the strong split, the gather and rank 0's reassembly under gloo."""
+    kind = "hip"
+    dist_backend = "nccl"
+
+    def __init__(self, local: int):
+        import torch
+
+        torch.cuda.set_device(local)
+        self.dev = torch.device("cuda", local)
+        self.stream = torch.cuda.current_stream()
+
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize()
+
+    def generate(self, clusters: int, seed: int):
+        from specpride_amd.synthetic import make_clusters_torch
+
+        return make_clusters_torch(clusters, seed=seed, device=self.dev)
+
+    def select(self, t, ids, co, so):
+        from specpride_amd.csr import SpectraCSR
+
+        return SpectraCSR.select_on_device(t, ids, co, so)
+
+    def batch(self, t):
+        from specpride_amd import engine
+
+        return engine.DeviceBatch.from_device(t)
+
+    def first_step(self, batch):
+        """The step once, checked: every cluster resolved by the launch the step makes,
+        and the fused pass (spx_bin_mean_medoid) equal to the two separate entry points,
+        consensus peaks and representatives bit for bit.  Returns (bm, md, separate)."""
+        import torch
+
+        from specpride_amd import engine
+
+        bm_sep = engine.bin_mean(batch)
+        md_sep = engine.medoid(batch, check=True)
+        bm, md = engine.bin_mean_medoid(batch, check=True)
+        torch.cuda.synchronize()
+        C = batch.n_clusters
+        st = bm.status.cpu().numpy()[:C]
+        rep = md.rep.cpu().numpy()[:C]
+        if np.any(st != 0) or np.any(rep < 0):
+            raise RuntimeError(f"unexpected statuses: bin-mean {np.unique(st)}, medoid min rep {rep.min()}")
+        same = (torch.equal(bm.count[:C], bm_sep.count[:C]) and torch.equal(md.rep[:C], md_sep.rep[:C]) and
+                all(torch.equal(a, b) for a, b in zip(bm.compact()[1:], bm_sep.compact()[1:])))
+        if not same:
+            raise RuntimeError("spx_bin_mean_medoid differs from spx_bin_mean + spx_medoid")
+        return bm, md, (bm_sep, md_sep)
+
+    def alloc(self, batch):
+        from specpride_amd import engine
+
+        return engine.bin_mean_medoid(batch, check=False)
+
+    def step(self, batch, bm, md):
+        from specpride_amd import engine
+
+        engine.bin_mean_medoid(batch, out_bm=bm, out_md=md, check=False)
+
+    def record(self):
+        import torch
+
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+    def wait(self, ev):
+        self.stream.wait_event(ev)
+
+    def first(self, batch):
+        return batch.t["cluster_off"][:-1]
+
+    def max_cluster_spectra(self, batch) -> int:
+        return int(batch.info.max_cluster_spectra)
+
+    def sample_results(self, t, ids, co, so) -> dict:
+        """World-1 results of clusters ``ids`` of the full batch ``t`` (rank 0, before
+        the strong split): the fused pass over just those clusters, on the host."""
+        sub = self.batch(self.select(t, ids, co, so))
+        bm, md, _ = self.first_step(sub)
+        h = bm.to_host()
+        first = sub.host_cluster_off[:-1]
+        rep = md.rep.cpu().numpy()[:sub.n_clusters]
+        return dict(count=np.diff(h["out_off"]), out_off=h["out_off"], out_mz=h["out_mz"], out_int=h["out_int"],
+                    member=np.where(rep >= 0, rep - first, rep))
+
+
+def make_backend(local: int):
+    """HipBackend, unless SPX_BENCH_BACKEND=module:Class names a test stand-in (the CPU
+    suite's launcher test; never set on the GPU box)."""
+    spec = os.environ.get("SPX_BENCH_BACKEND")
+    if not spec:
+        return HipBackend(local)
+    import importlib
+
+    mod, cls = spec.split(":")
+    return getattr(importlib.import_module(mod), cls)(local)
+
+
+def dist_init(be):
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        kw = {"device_id": torch.device("cuda", local)} if be.dist_backend == "nccl" else {}
+        dist.init_process_group(be.dist_backend, **kw)
     return rank, world, local
 
 
-def barrier(world):
-    import torch
+def barrier(world, be):
     import torch.distributed as dist
 
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    be.sync()
 
 
-def max_over_ranks(x: float, world: int) -> float:
+def max_over_ranks(x: float, world: int, be) -> float:
     import torch
     import torch.distributed as dist
 
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=be.dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def launch_ranks(args) -> int:
+    """``bench.py --gpus N`` outside a torchrun launch: start N fresh worker processes
+    of this script, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set
+    (rendezvous on 127.0.0.1), before this process makes any GPU call.  Rank 0 prints
+    the JSON line on this process's stdout; the other ranks' stdout goes to stderr.
+    Returns the first non-zero worker exit status (the others are then stopped), or 0.
+    More ranks than visible devices is an error: it never falls back to fewer GPUs."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+
+    n = args.gpus
+    if not os.environ.get("SPX_BENCH_BACKEND"):
+        import torch  # device_count() does not initialise HIP on this image
+
+        have = torch.cuda.device_count()
+        if n > have:
+            print(f"bench.py: --gpus {n} but only {have} HIP device(s) are visible", file=sys.stderr, flush=True)
+            return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs, rank_of = [], {}
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=r == 0))
+        rank_of[procs[-1].pid] = r
+    relay = threading.Thread(target=_relay_rank0, args=(procs[0].stdout,), daemon=True)
+    relay.start()
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {rank_of[p.pid]} exited with {code}; stopping the others",
+                          file=sys.stderr, flush=True)
+                    for q in procs:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for q in procs:  # only on an exception in this loop: our own children, by PID
+            q.kill()
+    relay.join(timeout=30)
+    return rc
+
+
+def _relay_rank0(pipe):
+    """Rank 0's stdout: the JSON line to this process's stdout, anything else the
+    communication libraries print (e.g. gloo's connection notice) to stderr."""
+    for line in pipe:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        (sys.stdout if line.startswith("{") else sys.stderr).flush()
 
 
 def consensus_bytes(batch, kept_peaks: int) -> int:
@@ -241,63 +411,93 @@ def cpu_baseline_parallel(n_clusters: int, seed: int):
                        f"cluster-parallel): {dt:.2f} s")}
 
 
-def headline(args, rank, world, local, out):
+def fused_bytes(batch, kept_peaks: int) -> int:
+    """Algorithmic HBM bytes of one fused step (spx_bin_mean_medoid): both methods'
+    bytes, as two separate launches would move them (the medoid reads the m/z again)."""
+    return consensus_bytes(batch, kept_peaks) + medoid_bytes(batch)
+
+
+def one_read_bytes(batch, kept_peaks: int) -> int:
+    """The step's single-read floor: every input read once (the consensus bytes, which
+    already read each m/z and intensity) plus the representative written (8 B/cluster)."""
+    return consensus_bytes(batch, kept_peaks) + 8 * batch.n_clusters
+
+
+def sample_ids(parts, per_rank: int = 512):
+    """Global cluster ids rank 0 checks the reassembled step against (every rank's
+    share, spread over its list)."""
+    pick = [p[np.linspace(0, len(p) - 1, min(per_rank, len(p))).astype(np.int64)] for p in parts if len(p)]
+    return np.unique(np.concatenate(pick)) if pick else np.zeros(0, np.int64)
+
+
+def check_assembled(a, want, ids, total_p):
+    """Rank 0's check of the reassembled last step: every representative resolved, the
+    planned peak total, and the sampled clusters bit-identical (counts, f64 peak bits,
+    member index) to a world-1 run of the same clusters.  Raises on any difference."""
+    ok_rep = bool(np.all(a["rep"] >= 0))
+    ok_total = int(a["out_off"][-1]) == int(total_p)
+    cnt = np.diff(a["out_off"])[ids]
+    same = np.array_equal(cnt, want["count"])
+    if same:
+        from specpride_amd.csr import concat_ranges
+
+        sel = concat_ranges(a["out_off"][ids], cnt)
+        same = (np.array_equal(a["out_mz"][sel].view(np.int64), want["out_mz"].view(np.int64)) and
+                np.array_equal(a["out_int"][sel].view(np.int64), want["out_int"].view(np.int64)))
+    member = a["rep"][ids] - a["cluster_off"][ids]
+    same_rep = np.array_equal(member, want["member"])
+    res = {"clusters": int(len(a["rep"])), "reps_resolved": ok_rep, "consensus_peaks": int(a["out_off"][-1]),
+           "planned_peaks": int(total_p), "sample_clusters": int(len(ids)),
+           "sample_equal_world1": bool(same and same_rep)}
+    res["ok"] = bool(ok_rep and ok_total and same and same_rep)
+    if not res["ok"]:
+        raise RuntimeError(f"rank 0's reassembled step differs from the plan or from world 1: {res}")
+    return res
+
+
+def headline(args, rank, world, local, out, be):
     import torch
 
-    from specpride_amd import engine, shard
-    from specpride_amd.csr import SpectraCSR
-    from specpride_amd.synthetic import make_clusters_torch
+    from specpride_amd import shard
 
-    dev = torch.device("cuda", local)
     strong = args.scaling == "strong"
     parts = loads = None
     global_co = None
+    want = ids = None
     if strong:
         # every rank generates the SAME seeded configs[4] batch and keeps the clusters the
         # size-balanced LPT plan gives it (shard.strong_partition, identical on every rank)
-        t = make_clusters_torch(args.clusters, seed=args.seed, device=dev)
+        t = be.generate(args.clusters, args.seed)
         if world > 1:
             global_co = t["cluster_off"].cpu().numpy()
             so = t["spec_off"].cpu().numpy()
             parts, loads = shard.strong_partition(global_co, so, world, "both")
+            if rank == 0:  # world-1 results of a sample of every rank's clusters, for the check
+                ids = sample_ids(parts)
+                want = be.sample_results(t, ids, global_co, so)
             full, t = t, None
-            t = SpectraCSR.select_on_device(full, parts[rank], global_co, so)
+            t = be.select(full, parts[rank], global_co, so)
             del full, so
-            torch.cuda.empty_cache()
+            if be.kind == "hip":
+                torch.cuda.empty_cache()
     else:
-        t = make_clusters_torch(args.clusters, seed=args.seed + 1000 * rank, device=dev)
-    batch = engine.DeviceBatch.from_device(t)
-    torch.cuda.synchronize()
+        t = be.generate(args.clusters, args.seed + 1000 * rank)
+    batch = be.batch(t)
+    be.sync()
 
-    # checked once, before timing: every cluster resolved by the launch the step makes, and
-    # the fused pass (spx_bin_mean_medoid: each cluster's bin-mean and medoid register
-    # bodies in one workgroup, then each method's leftover chain) equal to the two
-    # separate entry points, consensus peaks and representatives bit for bit
-    bm_sep = engine.bin_mean(batch)
-    md_sep = engine.medoid(batch, check=True)
-    bm, md = engine.bin_mean_medoid(batch, check=True)
-    torch.cuda.synchronize()
-    st = bm.status.cpu().numpy()[:batch.n_clusters]
-    rep = md.rep.cpu().numpy()[:batch.n_clusters]
-    if np.any(st != 0) or np.any(rep < 0):
-        raise RuntimeError(f"unexpected statuses: bin-mean {np.unique(st)}, medoid min rep {rep.min()}")
+    # checked once, before timing (HipBackend.first_step: statuses, fused == separate)
+    bm, md, separate = be.first_step(batch)
     kept = int(bm.count[:batch.n_clusters].sum().item())
-    C = batch.n_clusters
-    same = (torch.equal(bm.count[:C], bm_sep.count[:C]) and torch.equal(md.rep[:C], md_sep.rep[:C]) and
-            all(torch.equal(a, b) for a, b in zip(bm.compact()[1:], bm_sep.compact()[1:])))
-    if not same:
-        raise RuntimeError("spx_bin_mean_medoid differs from spx_bin_mean + spx_medoid")
-    large = engine.medoid_needs_large_path(batch) or bool(batch._ws.get("medoid_extra"))
-    stream = torch.cuda.current_stream()
-    first = batch.t["cluster_off"][:-1] if strong else None
+    first = be.first(batch) if strong else None
 
     # double-buffered results when gathering (step k's are in flight during step k+1)
     bufs = [(bm, md)]
     gat = None
     if world > 1:
-        bufs.append(engine.bin_mean_medoid(batch, check=False))
-        gat = shard.StepGatherer(batch.n_clusters, rank, world, batch.device,
-                                 wire_max_count=max(1, int(batch.info.max_cluster_spectra)))
+        bufs.append(be.alloc(batch))
+        gat = shard.StepGatherer(batch.n_clusters, rank, world, be.dev,
+                                 wire_max_count=max(1, be.max_cluster_spectra(batch)),
+                                 wire_ops=getattr(be, "wire_ops", None))
         total_c, total_p = gat.plan(kept)
 
     inflight = [None] * len(bufs)  # per buffer: the event of the gather reading it
@@ -306,23 +506,21 @@ def headline(args, rank, world, local, out):
         i = k % len(bufs)
         b, m = bufs[i]
         if inflight[i] is not None:
-            stream.wait_event(inflight[i])  # this buffer's previous gather (step k-2) is done
-        engine.bin_mean_medoid(batch, out_bm=b, out_md=m, check=False)
+            be.wait(inflight[i])  # this buffer's previous gather (step k-2) is done
+        be.step(batch, b, m)
         if gat is not None:
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            inflight[i] = gat.launch(b, m.rep, ev, first=first)
+            inflight[i] = gat.launch(b, m.rep, be.record(), first=first)
 
     for k in range(args.warmup):
         step(k)
-    barrier(world)
+    barrier(world, be)
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(k)
-    if gat is not None:
+    if gat is not None and gat.stream is not None:
         gat.stream.synchronize()
-    barrier(world)
-    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    barrier(world, be)
+    elapsed = max_over_ranks(time.perf_counter() - t0, world, be)
     if gat is not None and gat.check() != 0:
         raise RuntimeError(f"rank {rank}: {gat.check()} consensus peaks the gather wire format could not carry")
     total_clusters = (args.clusters if strong else world * batch.n_clusters)
@@ -331,34 +529,17 @@ def headline(args, rank, world, local, out):
     assembled = None
     if gat is not None and strong:
         # rank 0 reassembles the last step's gathered results in global cluster order
-        # (host-side index, after the timed region): every representative resolved and
-        # the consensus peak count equal to the sum the ranks planned
+        # (host-side index, after the timed region) and checks it (check_assembled)
         last = bufs[(args.warmup + args.steps - 1) % len(bufs)]
         if rank == 0:
-            own_member = torch.where(last[1].rep[:batch.n_clusters] >= 0,
-                                     last[1].rep[:batch.n_clusters] - first, last[1].rep[:batch.n_clusters])
+            r = last[1].rep[:batch.n_clusters]
+            own_member = torch.where(r >= 0, r - first, r)
             a = gat.assemble(parts, global_co, last[0], own_member)
-            assembled = {"clusters": int(len(a["rep"])), "reps_resolved": bool(np.all(a["rep"] >= 0)),
-                         "consensus_peaks": int(a["out_off"][-1]), "planned_peaks": int(total_p),
-                         "ok": bool(np.all(a["rep"] >= 0) and int(a["out_off"][-1]) == int(total_p))}
+            a["cluster_off"] = global_co
+            assembled = check_assembled(a, want, ids, total_p)
             del a
-        barrier(world)
+        barrier(world, be)
 
-    # per-kernel timing, after the timed region: HIP events on the stream the kernels
-    # are launched on -- around each whole entry point, and (spx_profile_*) around
-    # its dominant kernel's own launch inside the library
-    from specpride_amd import _lib
-
-    reps = max(3, args.steps)
-    _lib.profile_enable(True)
-    bm_ms_ep = time_launches(lambda: engine.bin_mean(batch, out=bm_sep), reps, stream)
-    md_ms_ep = time_launches(lambda: engine.medoid(batch, out=md_sep, check=False), reps, stream)
-    fu_ms_ep = time_launches(lambda: engine.bin_mean_medoid(batch, out_bm=bm, out_md=md, check=False), reps, stream)
-    fu_k = kernel_ms("bin_mean_medoid_kernel")
-    bm_ms = kernel_ms("bin_mean_reg_kernel")
-    md_ms = kernel_ms("medoid_reg_kernel")
-    _lib.profile_enable(False)
-    bm_bytes = consensus_bytes(batch, kept)
     out.update({
         "metric": "clusters/sec (whole node) for medoid + binned consensus",
         "value": round(value, 1),
@@ -380,15 +561,10 @@ def headline(args, rank, world, local, out):
                    "parallelism": (f"cluster-sharded x{world}, size-balanced LPT buckets of one batch "
                                    "(cost = peaks + n*peaks/64)" if strong and world > 1
                                    else f"cluster-sharded x{world}"),
+                   "launcher": ("bench.py --gpus N (own worker processes)" if os.environ.get("SPX_BENCH_SPAWNED")
+                                else ("external (torchrun)" if world > 1 else "single process")),
                    "gather": ("per-step RCCL gather of reps + compacted consensus peaks to rank 0, "
-                              "overlapped with the next step" if world > 1 else "none (1 GPU: results stay in HBM)"),
-                   "medoid_large_path": bool(large)},
-        "roofline": roofline("spx_bin_mean", "bin_mean_reg_kernel", bm_bytes, bm_ms_ep,
-                             load_pmc_traffic("bin_mean_reg_kernel", batch), kernel_ms=bm_ms),
-        "roofline_medoid": roofline("spx_medoid", "medoid_reg_kernel", medoid_bytes(batch), md_ms_ep,
-                                    load_pmc_traffic("medoid_reg_kernel", batch), kernel_ms=md_ms),
-        "kernels": {"spx_bin_mean_ms": round(bm_ms_ep, 4), "spx_medoid_ms": round(md_ms_ep, 4),
-                    "bin_mean_reg_kernel_ms": round(bm_ms, 4), "medoid_reg_kernel_ms": round(md_ms, 4)},
+                              "overlapped with the next step" if world > 1 else "none (1 GPU: results stay in HBM)")},
     })
     if gat is not None:
         out["config"]["gathered_clusters_per_step"] = total_c
@@ -403,17 +579,62 @@ def headline(args, rank, world, local, out):
     if assembled is not None:
         out["config"]["assembled_last_step"] = assembled
     out["config"]["step"] = ("spx_bin_mean_medoid: one fused pass per cluster (bin-mean + medoid register bodies "
-                             "in one workgroup, then each method's leftover kernels); checked bit-identical to "
-                             "spx_bin_mean + spx_medoid before timing")
-    out["kernels"]["spx_bin_mean_medoid_ms"] = round(fu_ms_ep, 4)
-    out["kernels"]["bin_mean_medoid_kernel_ms"] = round(fu_k, 4)
+                             "in one workgroup); the leftover chains only when a register body handed a cluster "
+                             "on (spx_bin_mean_medoid_stage); checked bit-identical to spx_bin_mean + spx_medoid "
+                             "before timing")
+    if be.kind == "hip":
+        kernel_lines(args, rank, world, out, be, batch, bm, md, separate, kept)
+    del bm, md, separate, bufs, batch, t
+    if be.kind == "hip":
+        torch.cuda.empty_cache()
+
+
+def kernel_lines(args, rank, world, out, be, batch, bm, md, separate, kept):
+    """Per-kernel timing after the timed region: HIP events on the stream the kernels
+    are launched on -- around each whole entry point, and (spx_profile_*) around its
+    dominant kernel's own launch inside the library.  ``roofline`` is the fused step's
+    (the kernel the headline times); the separate entry points' lines beside it."""
+    import torch
+
+    from specpride_amd import _lib, engine
+
+    bm_sep, md_sep = separate
+    stream = be.stream
+    large = engine.medoid_needs_large_path(batch) or bool(batch._ws.get("medoid_extra"))
+    reps = max(3, args.steps)
+    _lib.profile_enable(True)
+    bm_ms_ep = time_launches(lambda: engine.bin_mean(batch, out=bm_sep), reps, stream)
+    md_ms_ep = time_launches(lambda: engine.medoid(batch, out=md_sep, check=False), reps, stream)
+    fu_ms_ep = time_launches(lambda: engine.bin_mean_medoid(batch, out_bm=bm, out_md=md, check=False), reps, stream)
+    fu_k = kernel_ms("bin_mean_medoid_kernel")
+    bm_ms = kernel_ms("bin_mean_reg_kernel")
+    md_ms = kernel_ms("medoid_reg_kernel")
+    _lib.profile_enable(False)
+    bm_bytes = consensus_bytes(batch, kept)
+    fu = roofline("spx_bin_mean_medoid", "bin_mean_medoid_kernel", fused_bytes(batch, kept), fu_ms_ep,
+                  load_pmc_traffic("bin_mean_medoid_kernel", batch), kernel_ms=fu_k)
+    one = one_read_bytes(batch, kept)
+    fu["one_read_bytes"] = int(one)
+    fu["one_read_frac"] = round(one / (fu_ms_ep * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    fu["bytes_definition"] = ("bin-mean (16 B/peak + 20 B/spectrum + 32 B/cluster + 16 B/kept peak) + medoid "
+                              "(8 B/peak + 8 B/spectrum + 16 B/cluster), as the two separate launches move them; "
+                              "one_read_frac: the single-read floor (each input once + 8 B/cluster rep)")
+    out["config"]["medoid_large_path"] = bool(large)
+    out["roofline"] = fu
+    out["roofline_bin_mean"] = roofline("spx_bin_mean", "bin_mean_reg_kernel", bm_bytes, bm_ms_ep,
+                                        load_pmc_traffic("bin_mean_reg_kernel", batch), kernel_ms=bm_ms)
+    out["roofline_medoid"] = roofline("spx_medoid", "medoid_reg_kernel", medoid_bytes(batch), md_ms_ep,
+                                      load_pmc_traffic("medoid_reg_kernel", batch), kernel_ms=md_ms)
+    out["kernels"] = {"spx_bin_mean_medoid_ms": round(fu_ms_ep, 4), "bin_mean_medoid_kernel_ms": round(fu_k, 4),
+                      "spx_bin_mean_ms": round(bm_ms_ep, 4), "spx_medoid_ms": round(md_ms_ep, 4),
+                      "bin_mean_reg_kernel_ms": round(bm_ms, 4), "medoid_reg_kernel_ms": round(md_ms, 4)}
     if rank == 0 and world == 1 and not args.no_extras:
         # the same step through the two separate entry points (the two CLIs' calls)
         sep_ms = time_launches(lambda: (engine.bin_mean(batch, out=bm_sep),
                                         engine.medoid(batch, out=md_sep, check=False)), reps, stream)
         out["separate_step"] = {"entry_points": "spx_bin_mean + spx_medoid", "ms": round(sep_ms, 4),
                                 "clusters_per_s": round(batch.n_clusters / (sep_ms * 1e-3), 1),
-                                "fused_ms_per_step": round(elapsed / args.steps * 1e3, 4)}
+                                "fused_ms_per_step": out["ms_per_step"]}
         # gap-average consensus on the same resident batch (average_spectrum_clustering.py:26-148)
         ga = engine.gap_average(batch)
         torch.cuda.synchronize()
@@ -429,8 +650,6 @@ def headline(args, rank, world, local, out):
                                                    consensus_bytes(batch, gkept), ga_ms,
                                                    load_pmc_traffic("gap_average_lds_kernel", batch), kernel_ms=ga_k)}
         del ga
-    del bm, md, bm_sep, md_sep, bufs, batch, t
-    torch.cuda.empty_cache()
 
 
 def north_star(args, out):
@@ -734,13 +953,19 @@ def tier3(args, out):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        os.environ["SPX_BENCH_SPAWNED"] = "1"
+        sys.exit(launch_ranks(args))
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world0 != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world0}")
     want_cpu = world0 == 1 and not args.no_cpu_baseline and args.cpu_sample > 0
     cpu_par = cpu_baseline_parallel(4 * args.cpu_sample, args.seed) if want_cpu else None
-    rank, world, local = dist_init()
+    be = make_backend(int(os.environ.get("LOCAL_RANK", "0")))
+    rank, world, local = dist_init(be)
     out = {}
-    headline(args, rank, world, local, out)
-    if rank == 0 and world == 1 and not args.no_extras:
+    headline(args, rank, world, local, out, be)
+    if rank == 0 and world == 1 and not args.no_extras and be.kind == "hip":
         config3(args, out)
         bin_mean_shapes(args, out)
         medoid_shapes(args, out)

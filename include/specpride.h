@@ -190,6 +190,24 @@ int spx_bin_mean_medoid(const spx_csr *csr, const spx_bin_params *bin_params, co
                         void *bin_workspace, size_t bin_workspace_bytes, const spx_medoid_params *medoid_params,
                         int64_t *rep, double *totals, void *medoid_workspace, size_t medoid_workspace_bytes,
                         void *stream);
+/* spx_bin_mean_medoid in two halves (ABI 2, round 6):
+ *   stage 1: the fused register pass alone (bin_mean_medoid_kernel); the clusters either
+ *            register body hands on stay on its list.  With `handoff` (a DEVICE int32[2],
+ *            nullable) it also writes how many: [0] bin-mean, [1] medoid;
+ *   stage 2: both leftover chains (the 21 bin-mean and 1-12 medoid kernels that take
+ *            what the register bodies could not), on the SAME workspaces, untouched
+ *            since stage 1;
+ *   stage 0: both (= spx_bin_mean_medoid).
+ * Which clusters a register body hands on depends only on the batch and the parameters,
+ * so a caller that saw both counts at 0 after stage 1 may run the same (unchanged) batch
+ * with stage 1 alone and skip ~22 launches that would find their lists empty; results
+ * are then identical to stage 0.  Any other caller runs stage 2 (or stage 0). */
+int spx_bin_mean_medoid_stage(const spx_csr *csr, const spx_bin_params *bin_params, const spx_batch_info *info,
+                              spx_peaks_out *out, double *prec_out, int32_t *charge_out, int32_t *status,
+                              void *bin_workspace, size_t bin_workspace_bytes,
+                              const spx_medoid_params *medoid_params, int64_t *rep, double *totals,
+                              void *medoid_workspace, size_t medoid_workspace_bytes, void *stream, int stage,
+                              int32_t *handoff);
 
 /* distance(spec1, spec2, 'xcorr') = 1 - xCorrelationPrescore for n_pairs (global
  * spectrum index) pairs: out[p] for pairs[2p], pairs[2p+1].  The per-call API

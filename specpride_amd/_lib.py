@@ -65,7 +65,7 @@ class SpxCosineParams(ctypes.Structure):
 
 # every symbol include/specpride.h declares (checked by tests/test_host.py)
 EXPORTED = ["spx_bin_mean_workspace_size", "spx_bin_mean", "spx_bin_mean_stage", "spx_gap_average_workspace_size", "spx_gap_average",
-            "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_bin_mean_medoid", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
+            "spx_medoid_workspace_size", "spx_medoid_needs_large_path", "spx_medoid", "spx_bin_mean_medoid", "spx_bin_mean_medoid_stage", "spx_xcorr_distance", "spx_binned_cosine_workspace_size", "spx_binned_cosine", "spx_best_score",
             "spx_compact_peaks", "spx_wire_pack", "spx_wire_unpack", "spx_copy_h2d", "spx_copy_d2h",
             "spx_abi_version", "spx_last_error", "spx_profile_enable", "spx_profile_read",
             "spx_medoid_gram_operand_bits"]
@@ -149,6 +149,8 @@ def lib():
     L.spx_copy_d2h.argtypes = [_p, _p, _sz, _p]
     # symbols added in ABI 2's round 4 (bound when present: A/B runs load older builds)
     for name, argtypes in (("spx_bin_mean_medoid", [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _p, _p, _p, _p, _sz, _p]),
+                           ("spx_bin_mean_medoid_stage",
+                            [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _p, _p, _p, _p, _sz, _p, _i32, _p]),
                            ("spx_profile_enable", [_i32]), ("spx_profile_read", [ctypes.c_char_p, _p, _p]),
                            ("spx_medoid_gram_operand_bits", [])):
         if hasattr(L, name):

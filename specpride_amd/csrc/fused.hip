@@ -48,4 +48,19 @@ __global__ __launch_bounds__(BM_BLOCK, SPX_FU_MINW) void bin_mean_medoid_kernel(
   });
 }
 
+// The hand-off counts of one fused pass (spx_bin_mean_medoid_stage, stage 1): the
+// clusters each register body left on its list -- out[0] bin-mean (for
+// bin_mean_wide_kernel), out[1] medoid (for medoid_wide_kernel).  Both zero: the
+// leftover chains (stage 2) have nothing to do for this batch.
+__global__ __launch_bounds__(kWave) void handoff_count_kernel(const int32_t* bm_counts, const int32_t* md_counts,
+                                                              int32_t* out) {
+  const int l = threadIdx.x;
+  const int32_t a = wave_sum(bm_counts[l * kListLine]);
+  const int32_t b = wave_sum(md_counts[l * kListLine]);
+  if (l == 0) {
+    out[0] = a;
+    out[1] = b;
+  }
+}
+
 }  // namespace spx

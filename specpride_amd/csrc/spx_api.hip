@@ -363,10 +363,15 @@ int bin_mean_validate(const spx_csr* csr, const spx_bin_params* params, const sp
   return SPX_SUCCESS;
 }
 
+// What one bin_mean_impl call launches.  kBmAll/kBmFront/kBmChain are spx_bin_mean_stage's
+// stages 0/1/2; kBmHead (the memset and the head kernel only) and kBmTail (everything after
+// the head, on the same workspace) split spx_bin_mean_medoid_stage's pass.
+enum BmStage { kBmAll = 0, kBmFront = 1, kBmChain = 2, kBmHead = 3, kBmTail = 4 };
+
 int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
                   spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* workspace,
                   size_t workspace_bytes, void* stream, int stage, const BinMeanHead* head) {
-  if (stage < 0 || stage > 2) return fail(SPX_EINVAL, "spx_bin_mean_stage: stage must be 0, 1 or 2");
+  if (stage < kBmAll || stage > kBmTail) return fail(SPX_EINVAL, "spx_bin_mean_stage: stage must be 0, 1 or 2");
   if (int rc = bin_mean_validate(csr, params, info, out, prec_out, charge_out, status, workspace, workspace_bytes))
     return rc;
   const int64_t C = csr->n_clusters;
@@ -410,7 +415,7 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
   // stage 0/1: the counters (first 256 B), the bump pointer (next 256 B) and the
   // striped list's counters after them, then the register path, whose leftovers
   // (longer spectra, more spectra, unsorted, > 1,536 bins) all go to the wide kernel
-  if (stage != 2) {
+  if (stage == kBmAll || stage == kBmFront || stage == kBmHead) {
     if (hipMemsetAsync(W.counters, 0, 512 + spx::kListCountBytes, s) != hipSuccess)
       return check_launch("spx_bin_mean memset");
     if (head) {
@@ -422,12 +427,15 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
       prof.end();
       if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
     }
+  }
+  if (stage == kBmHead) return SPX_SUCCESS;  // the head's leftovers stay on W.rest for kBmTail
+  if (stage != kBmChain) {
     hipLaunchKernelGGL(spx::bin_mean_wide_kernel, gcl, dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out,
                        status, W.rest, W.def, n_def, W.glist, n_glist);
     if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
   }
-  if (stage == 1) return global_pass();  // clusters past the wide kernel keep status SPX_UNRESOLVED
-  if (stage == 2) {
+  if (stage == kBmFront) return global_pass();  // clusters past the wide kernel keep status SPX_UNRESOLVED
+  if (stage == kBmChain) {
     // the global kernel's list was consumed by stage 1: the chain's own start at 0
     if (hipMemsetAsync(n_glist, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
   }
@@ -501,6 +509,7 @@ extern "C" {
 int spx_bin_mean_stage(const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info,
                        spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* workspace,
                        size_t workspace_bytes, void* stream, int stage) {
+  if (stage < 0 || stage > 2) return fail(SPX_EINVAL, "spx_bin_mean_stage: stage must be 0, 1 or 2");
   return bin_mean_impl(csr, params, info, out, prec_out, charge_out, status, workspace, workspace_bytes, stream, stage,
                        nullptr);
 }
@@ -801,11 +810,13 @@ struct FusedCtx {
   int64_t* rep;
   double* totals;
   int64_t C;
+  const int32_t* bm_counts;  // set by the launch: the bin-mean hand-off list's stripe counters
 };
 
 int fused_head(void* ctx, const spx::CsrView& V, const spx::BinMeanParams& P, const spx::PeaksOut& O, double* prec_out,
                int32_t* charge_out, int32_t* status, const spx::StripedList& rest, hipStream_t s) {
-  const FusedCtx& F = *static_cast<const FusedCtx*>(ctx);
+  FusedCtx& F = *static_cast<FusedCtx*>(ctx);
+  F.bm_counts = rest.counts;
   ProfScope prof(5, s);
   hipLaunchKernelGGL(spx::bin_mean_medoid_kernel, dim3((unsigned)F.C), dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out,
                      charge_out, status, rest, F.md->P, F.rep, F.totals, F.md->wide);
@@ -821,26 +832,54 @@ int spx_medoid(const spx_csr* csr, const spx_medoid_params* params, int64_t* rep
   return medoid_impl(csr, params, rep, totals, workspace, workspace_bytes, stream, 0, nullptr);
 }
 
-int spx_bin_mean_medoid(const spx_csr* csr, const spx_bin_params* bin_params, const spx_batch_info* info,
-                        spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* bin_workspace,
-                        size_t bin_workspace_bytes, const spx_medoid_params* medoid_params, int64_t* rep,
-                        double* totals, void* medoid_workspace, size_t medoid_workspace_bytes, void* stream) {
+int spx_bin_mean_medoid_stage(const spx_csr* csr, const spx_bin_params* bin_params, const spx_batch_info* info,
+                              spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status,
+                              void* bin_workspace, size_t bin_workspace_bytes, const spx_medoid_params* medoid_params,
+                              int64_t* rep, double* totals, void* medoid_workspace, size_t medoid_workspace_bytes,
+                              void* stream, int stage, int32_t* handoff) {
   if (!csr_ok(csr)) return fail(SPX_EINVAL, "spx_bin_mean_medoid: null argument");
+  if (stage < 0 || stage > 2) return fail(SPX_EINVAL, "spx_bin_mean_medoid_stage: stage must be 0, 1 or 2");
   // both methods' checks before anything is enqueued (and before the empty-batch return)
   if (int rc = bin_mean_validate(csr, bin_params, info, out, prec_out, charge_out, status, bin_workspace,
                                  bin_workspace_bytes))
     return rc;
   if (int rc = medoid_validate(csr, medoid_params, rep, medoid_workspace)) return rc;
-  if (csr->n_clusters == 0) return SPX_SUCCESS;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (csr->n_clusters == 0) {
+    if (stage == 1 && handoff && hipMemsetAsync(handoff, 0, 2 * sizeof(int32_t), s) != hipSuccess)
+      return check_launch("spx_bin_mean_medoid_stage memset");
+    return SPX_SUCCESS;
+  }
+  if (stage == 2) {  // both leftover chains, on the workspaces stage 1 left
+    if (int rc = bin_mean_impl(csr, bin_params, info, out, prec_out, charge_out, status, bin_workspace,
+                               bin_workspace_bytes, stream, kBmTail, nullptr))
+      return rc;
+    return medoid_impl(csr, medoid_params, rep, totals, medoid_workspace, medoid_workspace_bytes, stream, 2, nullptr);
+  }
   MedoidHead H{};
   if (int rc = medoid_impl(csr, medoid_params, rep, totals, medoid_workspace, medoid_workspace_bytes, stream, 1, &H))
     return rc;
-  FusedCtx F{&H, rep, totals, csr->n_clusters};
+  FusedCtx F{&H, rep, totals, csr->n_clusters, nullptr};
   const BinMeanHead head{fused_head, &F};
   if (int rc = bin_mean_impl(csr, bin_params, info, out, prec_out, charge_out, status, bin_workspace,
-                             bin_workspace_bytes, stream, 0, &head))
+                             bin_workspace_bytes, stream, stage == 0 ? kBmAll : kBmHead, &head))
     return rc;
-  return medoid_impl(csr, medoid_params, rep, totals, medoid_workspace, medoid_workspace_bytes, stream, 2, nullptr);
+  if (stage == 0)
+    return medoid_impl(csr, medoid_params, rep, totals, medoid_workspace, medoid_workspace_bytes, stream, 2, nullptr);
+  if (handoff) {
+    hipLaunchKernelGGL(spx::handoff_count_kernel, dim3(1), dim3(spx::kWave), 0, s, F.bm_counts, H.wide.counts, handoff);
+    return check_launch("handoff_count_kernel");
+  }
+  return SPX_SUCCESS;
+}
+
+int spx_bin_mean_medoid(const spx_csr* csr, const spx_bin_params* bin_params, const spx_batch_info* info,
+                        spx_peaks_out* out, double* prec_out, int32_t* charge_out, int32_t* status, void* bin_workspace,
+                        size_t bin_workspace_bytes, const spx_medoid_params* medoid_params, int64_t* rep,
+                        double* totals, void* medoid_workspace, size_t medoid_workspace_bytes, void* stream) {
+  return spx_bin_mean_medoid_stage(csr, bin_params, info, out, prec_out, charge_out, status, bin_workspace,
+                                   bin_workspace_bytes, medoid_params, rep, totals, medoid_workspace,
+                                   medoid_workspace_bytes, stream, 0, nullptr);
 }
 
 }  // extern "C"

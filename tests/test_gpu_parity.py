@@ -680,6 +680,14 @@ def test_fused_bin_mean_medoid_equals_separate_calls(gpu, synth, shape):
     rep2, _ = engine.medoid(engine.DeviceBatch.from_host(csr)).to_host()
     np.testing.assert_array_equal(rep[:csr.n_clusters], rep2[:csr.n_clusters])
     np.testing.assert_array_equal(rep[:csr.n_clusters], c_oracle.medoid(csr))
+    # the checked call ran stage 1, read the hand-off counts and ran stage 2 only if a
+    # register body handed a cluster on; an unchecked call then runs stage 1 alone (synth:
+    # nothing handed on) or the whole pass (mixed) -- the same outputs either way
+    clean = [v for k, v in b._ws.items() if isinstance(k, tuple) and k[0] == "fused_clean"]
+    assert clean == [shape == "synth"]
+    bm3, md3 = engine.bin_mean_medoid(b, check=False)
+    assert_bin_mean_equal(bm3.to_host(), got)
+    np.testing.assert_array_equal(md3.rep.cpu().numpy()[:csr.n_clusters], rep[:csr.n_clusters])
 
 
 def test_bin_mean_mz_representations(gpu, synth):

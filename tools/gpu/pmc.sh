@@ -7,8 +7,8 @@ R=${GRAFT_REPO_ROOT:-$PWD}
 cd "$R"
 rm -rf gpurun_out/pmc && mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-K=${K:-'spx::(bin_mean_reg_kernel|medoid_reg_kernel|gap_average_lds_kernel)'}
-P="$R/tools/profile_kernels.py --which ${WHICH:-bm,md,ga} --clusters ${CLUSTERS:-100000} --reps 2"
+K=${K:-'spx::(bin_mean_reg_kernel|medoid_reg_kernel|gap_average_lds_kernel|bin_mean_medoid_kernel)'}
+P="$R/tools/profile_kernels.py --which ${WHICH:-bm,md,ga,fu} --clusters ${CLUSTERS:-100000} --reps 2"
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$K" -d "$R/gpurun_out/pmc/$name" -o "$name" --output-format csv -- python3 $P > "gpurun_out/pmc/$name.log" 2>&1 || { tail -5 "gpurun_out/pmc/$name.log"; return 1; }
