@@ -260,7 +260,10 @@ int spx_compact_peaks(const spx_csr *csr, const spx_peaks_out *src, const int64_
  * batch's largest cluster size), 9 or 10 bytes a peak instead of 16; spx_wire_unpack
  * rebuilds the doubles bit for bit (mz = M == 0 ? NaN : f64(M)/c, inten = f64(I)/c,
  * binning.py:211-218).  A peak no count <= max_count rebuilds exactly (not a bin-mean
- * output) is sent as NaN and counted in *n_fail (device int32, zeroed by the caller). */
+ * output) is sent as NaN and counted in *n_fail (device int32, zeroed by the caller).
+ * The inputs are meant to be spx_bin_mean outputs: a peak whose rebuild fails costs
+ * max_count exact tests (the search cannot stop early), so pass the batch's real largest
+ * cluster size as max_count, not the 65,535 bound. */
 int spx_wire_pack(const double *mz, const double *inten, int64_t n, int32_t max_count, float *mi, void *count,
                   int32_t count_bytes, int32_t *n_fail, void *stream);
 int spx_wire_unpack(const float *mi, const void *count, int32_t count_bytes, int64_t n, double *mz, double *inten,

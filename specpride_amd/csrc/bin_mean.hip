@@ -679,9 +679,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 #pragma unroll
   for (int j = 0; j < BR_PFC; ++j) {
     const int bo = boffb(j);
-#ifndef SPX_DG_NOMZ
     if (j >= BR_KM) rm[j] = bf_load(rmz, bo, 0);
-#endif
     ri[j] = bf_load(rit, bo, 0);
   }
   if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
@@ -732,17 +730,10 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     constexpr int j = decltype(jc)::value;
     double m;
     const double it = ri[j % BR_PFC];
-#ifdef SPX_DG_NOMZ  // diagnostic build (results wrong by design): no m/z re-read in phase C
-    if constexpr (j < BR_KM) m = mk[j];
-    else m = it;
-#else
     if constexpr (j < BR_KM) m = mk[j];
     else m = rm[j % BR_PFC];
-#endif
     const int bo = boffb(j + BR_PFC);
-#ifndef SPX_DG_NOMZ
     if constexpr (j + BR_PFC >= BR_KM) rm[j % BR_PFC] = bf_load(rmz, bo, 0);
-#endif
     ri[j % BR_PFC] = bf_load(rit, bo, 0);
     const int slot = code[j];
     BinAcc a = L.u.acc[slot];
@@ -750,9 +741,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     a.m = (float)((double)a.m + m);
     a.n += 1u;
     L.u.acc[slot] = a;
-#ifndef SPX_DG_NOBAR  // diagnostic build (results wrong by design): no per-spectrum barrier
     lds_barrier();
-#endif
   });
   SPX_STAMP(4);
 
@@ -769,337 +758,12 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   return kOk;
 }
 
-// ------------------------------------------------------------------------
-// Fold-by-slot register path (round 5; SPX_BR_FOLD).  Phases A and B1 are the
-// register path's (bins, last-in-bin, occupancy, codes -> slots), with phase A
-// reading the spectra last to first, so the first spectra phase C gathers are the
-// most recently read ones.  What changes is the fold.  The register path folds
-// spectrum by spectrum: every step is an LDS read-modify-write of the slot records
-// and a workgroup barrier (~600 cycles per spectrum, a chain no other work hides).
-// Here the fold belongs to the SLOT:
-//   B2  contributions per slot (one LDS add per contribution, rides B1's loop)
-//   B3  quorum n >= int(0.25 n_spec)+1 per slot (binning.py:181-183, 209-210): the
-//       kept slots get kept indices k in slot (= bin) order (block scan)
-//   B4  every contribution to a kept slot writes its peak position (u8) into
-//       pos[j / 4][k] byte j % 4 (0xFF: spectrum j has no peak in that bin)
-//   C   one lane per kept slot walks j = 0 .. n-1, gathers the (m/z, intensity)
-//       of its peaks (a ring of SPX_BF_RING gathers in flight; consecutive lanes
-//       hold consecutive bins, so a wave's gather covers a few cache lines) and
-//       folds I = f32(f64(I) + inten), M = f32(f64(M) + mz) in REGISTERS: the
-//       reference's float32 accumulation order (binning.py:198-199), no barrier,
-//       no LDS round trip, and no non-kept contribution is ever read or added
-//   D   the lane writes its mean at its output position (a ballot prefix over the
-//       kept slots whose intensity sum is not NaN, binning.py:212-222)
-// The table takes ceil(n/4) * K dwords over the dead bitmap; a cluster whose table
-// does not fit (the quorum off, or a very wide cluster) is handed to the wide
-// kernel, as every cluster this path does not take is.
-#ifndef SPX_BR_FOLD
-#define SPX_BR_FOLD 0  // measured slower on configs[4] (round 5: 9.26 vs 7.98 ms): kept for the A/B record
-#endif
-#ifndef SPX_BF_RING
-#define SPX_BF_RING 8  // phase-C gathers in flight per lane
-#endif
-#ifndef SPX_BF_REVERSE
-#define SPX_BF_REVERSE 1  // phase A reads the spectra last to first
-#endif
-constexpr int BF_SLOTS = BM_DCAP + kWave;          // slots + one dummy per lane
-constexpr int BF_POSW = (BR_W32 + kWave) * 3 / 2;  // pos-table dwords: the dead bitmap + prefix
-constexpr int BF_NQ = (BR_NMAX + 3) / 4;           // pos dwords per kept slot (4 spectra each)
-
-struct BinFoldSmem {
-  union alignas(16) {
-    struct {
-      uint32_t bits[BR_W32 + kWave];  // + one dummy word per lane (bits 0, prefix BM_DCAP + lane)
-      uint16_t pre[BR_W32 + kWave];
-    } b;                     // A-B1
-    uint32_t pos[BF_POSW];   // B4-C
-  } u;
-  union alignas(16) {
-    uint32_t cnt[BF_SLOTS];  // B2-B3: contributions per slot
-    uint16_t kidx[BF_SLOTS]; // B3-B4: kept index per slot (0xFFFF: not kept)
-  } s;
-  double prec[BR_NMAX];
-  int wcnt[(BM_DCAP / BM_BLOCK) * (BM_BLOCK / kWave)];  // D: emitted slots per (round, wave)
-  int votes[2 * (BM_BLOCK / kWave)];
-  int tmp[BM_BLOCK / kWave + 1];
-};
-static_assert(sizeof(BinFoldSmem::u) == (size_t)BF_POSW * 4, "the pos table covers the bitmap and prefix exactly");
-static_assert(BF_SLOTS % 4 == 0 && BF_SLOTS / 4 <= 2 * BM_BLOCK, "counts zeroed as two uint4 per thread");
-
-__device__ __forceinline__ int32_t bin_mean_fold_path(const CsrView& v, const BinMeanParams& P, BinFoldSmem& L,
-                                                      int64_t c, const PeaksOut& out, double* prec_out,
-                                                      int32_t* charge_out) {
-  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
-  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1], n64 = s1 - s0;
-  if (n64 < 1 || n64 > BR_NMAX || P.n_words > BM_WMAX) return kNotHere;
-  const int n = (int)n64;
-  const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
-  if (p1 == p0 || p1 - p0 >= (int64_t(1) << 28)) return kNotHere;
-  // lane j of every wave: spectrum j's [lo, hi) relative to p0, charge, precursor
-  const int jl = lane < n ? lane : n - 1;
-  const int32_t rlo = (int32_t)(v.spec_off[s0 + jl] - p0), rhi = (int32_t)(v.spec_off[s0 + jl + 1] - p0);
-  const int32_t z0 = v.charge[s0];
-  const bool mine = lane < n;
-  const int32_t zl = v.charge[s0 + jl];
-  const double pl = v.prec_mz[s0 + jl];
-  if (__ballot(mine & ((rhi - rlo) > BM_FASTLEN)) != 0ull) return kNotHere;  // uniform (same in every wave)
-  if (__ballot(mine & (zl != z0)) != 0ull) {  // binning.py:205-206: nothing emitted
-    if (tid == 0) { out.count[c] = 0; prec_out[c] = __longlong_as_double(0x7ff8000000000000ll); charge_out[c] = 0; }
-    return kMixedCharge;
-  }
-  if (wid == 0 && mine) L.prec[lane] = pl;
-  {
-    uint4* z = reinterpret_cast<uint4*>(L.u.b.bits) + tid * (BR_WPT / 4);
-#pragma unroll
-    for (int k = 0; k < BR_WPT / 4; ++k) z[k] = make_uint4(0u, 0u, 0u, 0u);
-    if (tid < kWave) {  // the dummy words (the last cluster's pos table overwrote them)
-      L.u.b.bits[BR_W32 + tid] = 0u;
-      L.u.b.pre[BR_W32 + tid] = (uint16_t)(BM_DCAP + tid);
-    }
-    uint4* zc = reinterpret_cast<uint4*>(L.s.cnt);
-    zc[tid] = make_uint4(0u, 0u, 0u, 0u);
-    if (tid + BM_BLOCK < BF_SLOTS / 4) zc[tid + BM_BLOCK] = make_uint4(0u, 0u, 0u, 0u);
-  }
-  lds_barrier();
-  SPX_STAMP(1);
-
-  const int fpos = wid * (kWave - 1) + lane;  // this lane's peak in every spectrum
-  const bool owner = lane < kWave - 1;
-  const __amdgpu_buffer_rsrc_t rmz = bf_rsrc(v.mz + p0, (int)(p1 - p0));
-  const __amdgpu_buffer_rsrc_t rit = bf_rsrc(v.inten + p0, (int)(p1 - p0));
-  // step t of phases A-B4 is spectrum jof(t): last to first
-  auto jof = [&](int t) -> int {
-    if constexpr (SPX_BF_REVERSE) return n - 1 - t;
-    else return t;
-  };
-
-  // ---- A: bins, last-in-bin, occupancy, codes (the register path's phase A)
-  int32_t code[BR_NMAX];
-  uint32_t* bm32 = L.u.b.bits;
-  int bad = 0;
-  {
-    double ra[BR_PFA];
-    int rl[BR_PFA];
-    auto fetch = [&](int t, double& m, int& len) __attribute__((always_inline)) {
-      const int jj = t < n ? jof(t) : 0;
-      const int a = __builtin_amdgcn_readlane(rlo, jj), e = __builtin_amdgcn_readlane(rhi, jj);
-      len = e - a;
-      m = bf_load(rmz, (a + fpos) * 8, 0);
-    };
-#pragma unroll
-    for (int j = 0; j < BR_NMAX; ++j) code[j] = -1;
-    auto body = [&](auto jc, const double m, const int len) __attribute__((always_inline)) {
-      constexpr int j = decltype(jc)::value;
-      const bool act = fpos < len;
-      const bool inr = act & (m >= P.minimum) & (m < P.maximum);
-      const int32_t kb = bin_small(m, P);
-      const int32_t key = inr ? kb : ((act & (m < P.minimum)) ? -1 : 0x7fffffff);
-      const int32_t kn = wave_next(key, 0x7fffffff);
-      bad |= (int)(owner & act & ((m != m) | (key > kn)));
-      const bool valid = owner & inr & (kn != key);  // the last peak of its bin (binning.py:197-199)
-      atomicOr(&bm32[valid ? key >> 5 : lane], valid ? 1u << (key & 31) : 0u);
-      code[j] = valid ? key : -1;
-      asm volatile("" : "+v"(code[j]));
-    };
-#pragma unroll
-    for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
-    reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
-      constexpr int j = decltype(jc)::value;
-      const double m = ra[j % BR_PFA];
-      const int len = rl[j % BR_PFA];
-      fetch(j + BR_PFA, ra[j % BR_PFA], rl[j % BR_PFA]);
-      body(jc, m, len);
-    });
-  }
-  if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
-  SPX_STAMP(2);
-
-  // ---- B1 + B2: slots in bin order, codes -> slots, contributions per slot
-  const int D = reg_prefix_arrays(L.u.b.bits, L.u.b.pre, L.tmp);
-  if (D > BM_DCAP) return kDeferred;
-  {
-    constexpr int G = SPX_BR_BG;
-    int nn = __builtin_amdgcn_readfirstlane(n);
-#pragma unroll
-    for (int j0 = 0; j0 < BR_NMAX; j0 += G) {
-      asm volatile("" : "+s"(nn));
-      if (j0 < nn) {
-        uint32_t wb[G], wp[G];
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-          if (j0 + q < BR_NMAX) {
-            const uint32_t w = min((uint32_t)code[j0 + q] >> 5, (uint32_t)(BR_W32 + lane));
-            wb[q] = L.u.b.bits[w];
-            wp[q] = L.u.b.pre[w];
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-          if (j0 + q < BR_NMAX) {
-            const uint32_t b = (uint32_t)code[j0 + q];
-            code[j0 + q] = (int32_t)wp[q] + __popc(wb[q] & ((1u << (b & 31)) - 1u));
-            // a code without contribution (and every step past n: code -1) counts into
-            // this lane's dummy slot
-            atomicAdd(&L.s.cnt[code[j0 + q]], 1u);
-          }
-        }
-      }
-    }
-  }
-  lds_barrier();  // B1's bitmap reads and B2's counts are complete in every wave
-  // the bitmap and prefix are dead: clear them for the position table
-  {
-    uint4* z = reinterpret_cast<uint4*>(L.u.pos);
-    for (int k = tid; k < BF_POSW / 4; k += BM_BLOCK) z[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
-  }
-
-  // ---- B3: the quorum, kept indices in slot order
-  const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
-  constexpr int PER = BM_DCAP / BM_BLOCK;  // 6 contiguous slots per thread
-  static_assert(PER == 6, "three b64 count reads per thread");
-  int K;
-  {
-    uint32_t cv[PER];
-    const uint2* src = reinterpret_cast<const uint2*>(L.s.cnt) + tid * (PER / 2);
-#pragma unroll
-    for (int k = 0; k < PER / 2; ++k) {
-      const uint2 q = src[k];
-      cv[2 * k] = q.x;
-      cv[2 * k + 1] = q.y;
-    }
-    int local = 0;
-    uint32_t keepm = 0u;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const bool keep = tid * PER + i < D && cv[i] >= quorum;
-      keepm |= (uint32_t)keep << i;
-      local += keep;
-    }
-    // (the scan's first barrier follows every wave's count reads: kidx may overwrite them)
-    int base = block_exclusive_scan<BM_BLOCK, int, true, false>(local, L.tmp, K);
-    uint32_t kk[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const bool keep = (keepm >> i) & 1u;
-      kk[i] = keep ? (uint32_t)base : 0xFFFFu;
-      base += keep;
-    }
-    uint32_t* dst = reinterpret_cast<uint32_t*>(L.s.kidx) + tid * (PER / 2);
-#pragma unroll
-    for (int k = 0; k < PER / 2; ++k) dst[k] = kk[2 * k] | (kk[2 * k + 1] << 16);
-    if (tid < kWave) L.s.kidx[BM_DCAP + tid] = 0xFFFFu;  // the dummies
-  }
-  const int nq = (n + 3) >> 2;
-  if (K * nq > BF_POSW) return kDeferred;  // the table does not fit: the wide kernel takes it
-  lds_barrier();
-  SPX_STAMP(3);
-
-  // ---- B4: each kept contribution's peak position into its (spectrum, kept slot) byte
-  if (K > 0) {
-    constexpr int G = SPX_BR_BG;
-    uint8_t* pb = reinterpret_cast<uint8_t*>(L.u.pos);
-    int nn = __builtin_amdgcn_readfirstlane(n);
-#pragma unroll
-    for (int j0 = 0; j0 < BR_NMAX; j0 += G) {
-      asm volatile("" : "+s"(nn));
-      if (j0 < nn) {
-        uint32_t kx[G];
-#pragma unroll
-        for (int q = 0; q < G; ++q)
-          if (j0 + q < BR_NMAX) kx[q] = L.s.kidx[code[j0 + q]];
-#pragma unroll
-        for (int q = 0; q < G; ++q) {
-          if (j0 + q < BR_NMAX && kx[q] != 0xFFFFu) {  // (steps past n: dummies, never kept)
-            const int j = jof(j0 + q);
-            pb[(((j >> 2) * K + (int)kx[q]) << 2) + (j & 3)] = (uint8_t)fpos;
-          }
-        }
-      }
-    }
-  }
-  lds_barrier();
-  SPX_STAMP(4);
-
-  // ---- C + D: one lane per kept slot, in rounds of 256 kept slots
-  constexpr int R = SPX_BF_RING;
-  const unsigned long long below = (1ull << lane) - 1ull;
-  int total = 0;
-  double* __restrict__ omz = out.mz + p0;
-  double* __restrict__ oint = out.inten + p0;
-  const int rounds = (K + BM_BLOCK - 1) / BM_BLOCK;
-  for (int r = 0; r < rounds; ++r) {
-    const int k = r * BM_BLOCK + tid;
-    const bool act = k < K;
-    uint32_t pw[BF_NQ];
-#pragma unroll
-    for (int q = 0; q < BF_NQ; ++q) pw[q] = L.u.pos[(q < nq ? q * K : 0) + (act ? k : 0)];
-    auto posb = [&](int j) -> uint32_t { return (pw[j >> 2] >> (8 * (j & 3))) & 0xFFu; };
-    double rm[R], ri[R];
-    auto gather = [&](int j, double& m, double& it) __attribute__((always_inline)) {
-      const int jj = j < n ? j : n - 1;
-      const uint32_t b = posb(j);
-      const int bo = (__builtin_amdgcn_readlane(rlo, jj) + (int)(b == 0xFFu ? 0u : b)) * 8;
-      m = bf_load(rmz, bo, 0);
-      it = bf_load(rit, bo, 0);
-    };
-#pragma unroll
-    for (int j = 0; j < R; ++j) gather(j, rm[j], ri[j]);
-    float M = 0.0f, I = 0.0f;
-    uint32_t cn = 0u;
-    reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
-      constexpr int j = decltype(jc)::value;
-      const double m = rm[j % R], it = ri[j % R];
-      if constexpr (j + R < BR_NMAX) gather(j + R, rm[j % R], ri[j % R]);
-      const bool valid = act & (posb(j) != 0xFFu);
-      const float M2 = (float)((double)M + m), I2 = (float)((double)I + it);
-      M = valid ? M2 : M;
-      I = valid ? I2 : I;
-      cn += valid;
-    });
-    // D: this round's means at their output positions (binning.py:209-222)
-    const bool keep = act && !isnan(I);  // cn >= quorum >= 1 by construction
-    const unsigned long long bal = __ballot(keep);
-    if (lane == 0) L.wcnt[r * (BM_BLOCK / kWave) + wid] = __popcll(bal);
-    lds_barrier();
-    int before = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < BM_BLOCK / kWave; ++w) {
-      const int x = L.wcnt[r * (BM_BLOCK / kWave) + w];
-      tot += x;
-      before += w < wid ? x : 0;
-    }
-    if (keep) {
-      const int o = total + before + __popcll(bal & below);
-      const double cd = (double)cn;
-      oint[o] = (double)I / cd;
-      omz[o] = M == 0.0f ? __longlong_as_double(0x7ff8000000000000ll) : (double)M / cd;
-    }
-    total += tot;
-  }
-  SPX_STAMP(5);
-  if (tid == 0) {
-    out.count[c] = total;
-    charge_out[c] = z0;
-    prec_out[c] = pw_sum_small([&](int64_t j) { return L.prec[j]; }, n) / (double)n;  // np.mean (binning.py:224)
-  }
-  return kOk;
-}
-
-#if SPX_BR_FOLD
-using BinHeadSmem = BinFoldSmem;
-__device__ __forceinline__ int32_t bin_mean_head_path(const CsrView& v, const BinMeanParams& P, BinHeadSmem& L,
-                                                      int64_t c, const PeaksOut& out, double* prec_out,
-                                                      int32_t* charge_out) {
-  return bin_mean_fold_path(v, P, L, c, out, prec_out, charge_out);
-}
-#else
 using BinHeadSmem = BinRegSmem;
 __device__ __forceinline__ int32_t bin_mean_head_path(const CsrView& v, const BinMeanParams& P, BinHeadSmem& L,
                                                       int64_t c, const PeaksOut& out, double* prec_out,
                                                       int32_t* charge_out) {
   return bin_mean_reg_path(v, P, L, c, out, prec_out, charge_out);
 }
-#endif
 
 // Register-code kernel: one workgroup per cluster.  Clusters this path does not
 // take (kNotHere) and kDeferred ones (unsorted, NaN, too many distinct bins) go

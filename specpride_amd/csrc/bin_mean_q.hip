@@ -460,9 +460,6 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_place_kernel(CsrView v, B
 #ifndef SPX_QF_NS
 #define SPX_QF_NS 8
 #endif
-#ifndef SPX_QF_DIAG
-#define SPX_QF_DIAG 0  // A/B diagnostics only: 1 = no fold arithmetic, 2 = no loads (wrong results)
-#endif
 constexpr int QF_TS = SPX_QF_TS;             // spectra per stage
 constexpr int QF_NS = SPX_QF_NS;             // ring stages (QF_NS x QF_TS KB of rows)
 constexpr int QF_LOADERS = 4;                // loader waves
@@ -536,7 +533,7 @@ __global__ __launch_bounds__(QF_BLOCK, 1) void bin_mean_q_fold_kernel(const QMet
         q_glds4(Pg + (int64_t)sp * 2 + (lane & 1), &L.p[slot][0]);
       }
     };
-    if (wid > 0 && SPX_QF_DIAG != 2)
+    if (wid > 0)
       for (int st = 0; st < min(QF_NS - 1, nst); ++st) issue(st);
     float si = 0.0f, sm = 0.0f;
     uint32_t cnt = 0;
@@ -548,8 +545,8 @@ __global__ __launch_bounds__(QF_BLOCK, 1) void bin_mean_q_fold_kernel(const QMet
       }
       __builtin_amdgcn_s_barrier();
       if (wid > 0) {
-        if (t + QF_NS - 1 < nst && SPX_QF_DIAG != 2) issue(t + QF_NS - 1);  // into the slot folded in iteration t - 1
-      } else if (SPX_QF_DIAG != 1) {
+        if (t + QF_NS - 1 < nst) issue(t + QF_NS - 1);  // into the slot folded in iteration t - 1
+      } else {
         const int slot = t % QF_NS;
         const int steps = min(QF_TS, n - t * QF_TS);  // uniform
         // the stage's words and entries read first (stale ones past `steps` are

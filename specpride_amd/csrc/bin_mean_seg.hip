@@ -135,10 +135,7 @@ constexpr int SG_GROUP = SG_GQ * (kWave - 1);  // peaks per group (252)
 // intensities alongside.  f(k, key, last, spectrum-in-block, m/z, intensity).
 // SG_WR groups are in flight per wave: a ring of register groups, unrolled so
 // every slot is a fixed register set, each refilled with the group SG_WR ahead.
-#ifndef SPX_WALK_R
-#define SPX_WALK_R 1
-#endif
-constexpr int SG_WR = SPX_WALK_R + 1;  // ring slots (groups in flight + the one processed)
+constexpr int SG_WR = 2;  // ring slots (one group in flight + the one processed)
 
 struct NoChunkHook {
   __device__ void operator()(int) const {}

@@ -59,26 +59,8 @@ constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10
 #ifndef SPX_GA_WMAXN
 #define SPX_GA_WMAXN 65536  // the wide kernel hands clusters of more peaks than this to the giant pipeline (0: none)
 #endif
-#ifndef SPX_GA_DEFERBIG
-#define SPX_GA_DEFERBIG 1  // the LDS kernel hands clusters past its register capacity on unread
-#endif
 #ifndef SPX_GA_WUM
 #define SPX_GA_WUM 20
-#endif
-#ifndef SPX_GA_HYBRID
-#define SPX_GA_HYBRID 1  // wide/global kernels: past UM * BLOCK peaks, the first UM * BLOCK stay in registers
-#endif
-#ifndef SPX_GA_P3INT
-#define SPX_GA_P3INT 0  // the LDS kernel reads the intensities in pass 3 instead of pass 1
-#endif
-#ifndef SPX_GA_BSKIP
-#define SPX_GA_BSKIP 2  // register rows: a batch of 8 rows no peak of the cluster reaches is skipped whole, passes (1) and m/z loads (2)
-#endif
-#ifndef SPX_GA_P2B
-#define SPX_GA_P2B 1  // pass 2 over the register rows: buckets by batches of 8, the exact division once per batch if needed
-#endif
-#ifndef SPX_GA_EARLY
-#define SPX_GA_EARLY 1  // wide kernel: intensities streamed during the bucket pass, bitmap zeroed under the m/z loads
 #endif
 // the wide kernel's (40 spilled 135 VGPRs even at its 256-VGPR budget)
 constexpr int GA_WUM = SPX_GA_WUM;
@@ -675,7 +657,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   // hybrid (not the LDS kernel, which hands such clusters on): the first UM * BLOCK
   // peaks are register-resident and tagged like a small cluster's, only the tail is
   // re-read per pass (600-peak spectra: clusters of 10,800 to 30,000 peaks)
-  constexpr bool kHy = !kDeferBig && SPX_GA_HYBRID;
+  constexpr bool kHy = !kDeferBig;
   const bool hyb = kHy && !inreg;  // uniform
   const bool regs = inreg || hyb;
   const int64_t ptail = p0 + (int64_t)UM * GA_BLOCK;
@@ -686,9 +668,9 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   if (regs) {
 #pragma unroll
     for (int u0 = 0; u0 < UM; u0 += 8) {
-      // SPX_GA_BSKIP >= 2: a batch of rows no peak reaches is not loaded (uniform; the
-      // batch's loads stay together)
-      const bool live = SPX_GA_BSKIP < 2 || (int64_t)u0 * GA_BLOCK < N;
+      // a batch of rows no peak reaches is not loaded (uniform; the batch's loads stay
+      // together)
+      const bool live = (int64_t)u0 * GA_BLOCK < N;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int u = u0 + q;
@@ -716,9 +698,7 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       if (N == 0) return;  // uniform: no peaks (and the batch may hold none to load)
 #pragma unroll
       for (int u0 = 0; u0 < UM; u0 += 8) {
-#if SPX_GA_BSKIP
         if ((int64_t)u0 * GA_BLOCK >= N) break;  // uniform: no peak in rows u0.. (their tags stay 0)
-#endif
         double itb[8];
         if constexpr (kInten) {
 #pragma unroll
@@ -759,7 +739,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
 
   double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
   int bad = 0;
-#if SPX_GA_EARLY
   // The wide kernel (LDS state, m/z in registers, one workgroup per CU: its
   // latencies are not covered by a second workgroup): the intensities are needed
   // only for max |intensity| (pass 5's fixed-point scale) and their finiteness,
@@ -768,33 +747,10 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
   // two per CU, the same order measured 16.68 -> 17.18 ms: its pass-1 loads had
   // overlapped the m/z loads; profiles/r04_ab_gap_early.txt.)
   const bool early = kL && !kDeferBig && inreg && n > 1 && N >= 2;  // uniform
-#else
-  const bool early = false;
-#endif
-#if SPX_GA_P3INT
-  // The LDS kernel (every peak register-resident): the intensities are read in pass 3,
-  // not pass 1 -- pass 5's second read then follows the first by one step (the gaps),
-  // not by passes 2-4, and finds them in L2 instead of the fabric
-  const bool late = kDeferBig && kL && inreg && n > 1 && N >= 2;  // uniform
-#else
-  const bool late = false;
-#endif
   if (early) {
 #pragma unroll
     for (int k = 0; k < GA_WMAX / GA_BLOCK; ++k) S.bitmap[k * GA_BLOCK + tid] = 0ull;
     // 1a: m/z extrema and finiteness from registers
-#pragma unroll
-    for (int u = 0; u < UM; ++u) {
-      if (p0 + (int64_t)u * GA_BLOCK + tid < p1) {
-        bad |= !isfinite(rm[u]);
-        lo = fmin(lo, rm[u]);
-        hi = fmax(hi, rm[u]);
-      }
-    }
-    if (any(bad, 0)) return kNonFinite;
-  } else if (late) {
-    // 1 (SPX_GA_P3INT): the m/z extrema and finiteness from registers only; the
-    // intensities' max and finiteness come with pass 3 (below)
 #pragma unroll
     for (int u = 0; u < UM; ++u) {
       if (p0 + (int64_t)u * GA_BLOCK + tid < p1) {
@@ -916,13 +872,10 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
       SPX_GUARD(b >= 0 && b < nw * 64, "gap bitmap c=%ld b=%ld nw=%ld\n", (long)c, (long)b, (long)nw)
       atomicOr(&S.bitmap[b >> 6], 1ull << (b & 63));
     };
-#if SPX_GA_P2B
     if (regs && N > 0) {  // uniform
 #pragma unroll
       for (int u0 = 0; u0 < UM; u0 += 8) {
-#if SPX_GA_BSKIP
         if ((int64_t)u0 * GA_BLOCK >= N) break;  // uniform
-#endif
         // the reciprocal product's floor for all 8 rows (a lane past the cluster bins its
         // clamped copy of peak 0: never used); where it is not certain, one divide below
         uint32_t badm = 0u;
@@ -966,9 +919,6 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     } else {
       peaks_m_tag(pass2);
     }
-#else
-    peaks_m_tag(pass2);
-#endif
     bar();
   }
   int D;
@@ -994,28 +944,9 @@ __device__ int32_t gap_body(const CsrView& v, const GapParams& P, const GapState
     atomicAdd(&S.cnt[slot], 1u);
     atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[slot]), (unsigned long long)key);
     atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[slot]), (unsigned long long)key);
-    if (late) {
-      bad |= !isfinite(it);
-      imax = fmax(imax, fabs(it));
-    }
   };
-  if (late) {
-    peaks_g(std::true_type{}, std::true_type{}, pass3);
-    // the block's max |intensity| (pass 5's scale) and the intensities' finiteness
-    imax = wave_max_dpp(imax);
-    const bool wbad = __ballot(bad) != 0ull;
-    if (lane == 0) { red[2 * GA_NW + wid] = imax; votes[GA_NW + wid] = wbad; }
-    bar();
-    int nf = 0;
-    for (int w = 0; w < GA_NW; ++w) {
-      imax = fmax(imax, red[2 * GA_NW + w]);
-      nf |= votes[GA_NW + w];
-    }
-    if (nf) return kNonFinite;
-  } else {
-    peaks_m_tag(pass3);
-    bar();
-  }
+  peaks_m_tag(pass3);
+  bar();
 
   SPX_GA_STAMP(4);
   int E;
@@ -1091,7 +1022,7 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   if (pn <= kWave) pl = prec_lanes(v, ps0, pn);
   // a cluster past the register capacity goes to the wide kernel unread: streamed
   // here it would only be deferred after its bitmap pass (600-peak spectra from n ~ 18)
-  const int32_t st = gap_body<GA_UM, SPX_GA_DEFERBIG>(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
+  const int32_t st = gap_body<GA_UM, true>(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
   if (st == kDeferred || st == kNonFinite) {  // non-finite: the global kernel's gap_body_nf
     if (threadIdx.x == 0) {
       status[c] = kDeferred;
@@ -1173,9 +1104,6 @@ __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
 constexpr int64_t GA_GIANT_N = 16384;
 constexpr int GA_GMAX = 256;                      // giant records per call
 constexpr int64_t GA_TILE = 2 * GA_BATCH * GA_BLOCK;  // peaks per tile
-#ifndef SPX_GA_GBATCH
-#define SPX_GA_GBATCH 1  // giant passes 2-3: a batch's global reads before its atomics
-#endif
 #ifndef SPX_GA_GGRID
 #define SPX_GA_GGRID 512  // skewed configs[3] gap-average: 1024 4.21 ms, 512 3.77-3.79, 256 3.78-3.80, 4096 6.05
 #endif
@@ -1186,35 +1114,14 @@ constexpr int GA_GAGG = 2560;                     // groups pass 5 sums in LDS f
 // spectra touches ~1-2k groups), flushed to the slice after each tile -- one global
 // add per (tile, group) instead of per peak.  A peak whose probe runs past
 // GA_HPROBE slots adds globally.  Integer adds, so the totals do not change.
-#ifndef SPX_GA_HASH
-#define SPX_GA_HASH 1
-#endif
-#ifndef SPX_GA_FLAT4
-#define SPX_GA_FLAT4 1  // giants' step 4 over a flat (giant, chunk) grid (gap_giant_groups_kernel)
-#endif
-#ifndef SPX_GA_TPERM
-#define SPX_GA_TPERM 2  // giant tile passes (1: passes 2-3 only, 2: all): tiles in a scattered order (different giants side by side)
-#endif
-#ifndef SPX_GA_FLAT6
-#define SPX_GA_FLAT6 1  // giants' step 6 (emit) over the same flat grid; the per-giant step keeps the precursor
-#endif
-#ifndef SPX_GA_HASH3
-#define SPX_GA_HASH3 1  // pass 3 too: a tile's per-slot m/z extents in an LDS table, one global min/max per (tile, slot)
-#endif
-#ifndef SPX_GA_NOFILT
-#define SPX_GA_NOFILT 1  // giant passes 2-3: the tile flushes issue their atomics without reading the slice first (memory-side atomics: the read is a fabric round trip of its own)
-#endif
-#ifndef SPX_GA_HASH2
-#define SPX_GA_HASH2 1  // pass 2 too: a tile's bitmap words OR-ed in an LDS table, one global OR per (tile, word)
-#endif
 constexpr int GA_HCAP = 2048;
 constexpr int GA_HPROBE = 16;
 
 struct GapGiant {  // zeroed by the call's memset
   unsigned long long lo_inv, hi_key, imax_key;  // ~order key of the min m/z, order keys of max m/z, max |intensity|
   long long off;                                // its arena slice
-  int32_t c, dcap, ok, bad, status, D, E, pad;  // pad: step 4a's "a bucket spans mz_accuracy" flag (SPX_GA_FLAT4)
-  unsigned long long gmax_key;  // step 6a (SPX_GA_FLAT6): order key of the largest kept group intensity
+  int32_t c, dcap, ok, bad, status, D, E, pad;  // pad: step 4a's "a bucket spans mz_accuracy" flag
+  unsigned long long gmax_key;  // step 6a: order key of the largest kept group intensity
   int32_t gany, pad2;           // step 6a: some group has >= min_fraction spectra
 };
 
@@ -1226,7 +1133,7 @@ struct GiantArgs {
   int gmax;
   char* arena;
   int wcap;
-  double* out_mz;     // step 6 over the flat grid (SPX_GA_FLAT6): the consensus outputs
+  double* out_mz;     // step 6 over the flat grid: the consensus outputs
   double* out_int;
   int64_t* out_count;
 };
@@ -1561,13 +1468,13 @@ template <int PASS>
 __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) {
   __shared__ double red[GA_NW * 3];
   __shared__ int votes[2 * GA_NW];
-  constexpr bool kH3 = (PASS == 3 && SPX_GA_HASH3 && SPX_GA_GBATCH) || (PASS == 2 && SPX_GA_HASH2 && SPX_GA_GBATCH);
+  constexpr bool kH3 = PASS == 3 || PASS == 2;
   // pass 2 (kH3 too): agg_m holds the hashed words' OR-ed bits
   // pass 5: group sums (agg_m, agg_i); pass 3 (kH3): the hashed slots' min / max m/z keys
   __shared__ unsigned long long agg_m[PASS == 5 ? GA_GAGG : (kH3 ? GA_HCAP : 1)];
   __shared__ unsigned long long agg_i[PASS == 5 ? GA_GAGG : (kH3 && PASS == 3 ? GA_HCAP : 1)];
   __shared__ uint32_t agg_c[PASS == 5 ? GA_GAGG : 1];
-  __shared__ uint32_t hkey[(PASS == 5 && SPX_GA_HASH) || kH3 ? GA_HCAP : 1];  // group / slot + 1 (0: empty)
+  __shared__ uint32_t hkey[PASS == 5 || kH3 ? GA_HCAP : 1];  // group / slot + 1 (0: empty)
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
   const int ng = min(*A.n_giant, A.gmax);
   auto peaks_of = [&](const GapGiant& H, int64_t& p0, int64_t& p1) {
@@ -1604,11 +1511,10 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
   int g = 0, cur = -1, E = 0, sc_m = 0, sc_i = 0;
   bool agg = false, hashed = false;
   int64_t gbase = 0, gtiles = ng > 0 ? tiles_of(A.giants[0]) : 0, p0 = 0, p1 = 0, kb = 0;
-#if SPX_GA_TPERM
   // passes 2 and 3 take the tiles in a scattered order (t = u * P mod T): consecutive
   // workgroups then work on different giants instead of 512 neighbouring tiles of one,
   // whose per-tile flushes all hit the same template slots of one slice at once
-  constexpr bool kPerm = (PASS == 2 || PASS == 3) || (SPX_GA_TPERM >= 2 && (PASS == 1 || PASS == 5));
+  constexpr bool kPerm = PASS == 1 || PASS == 2 || PASS == 3 || PASS == 5;
   __shared__ long long tpre[kPerm ? GA_GMAX + 1 : 1];
   __shared__ long long ttmp[kPerm ? GA_NW + 1 : 1];
   long long tT = 0, tP = 1;
@@ -1628,11 +1534,10 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
       if (a == 1) { tP = cands[q]; break; }
     }
   }
-#endif
   GapState<uint32_t> S{};
   // the hashed table after a tile: every occupied entry to the slice, the table emptied
   auto hflush = [&]() __attribute__((always_inline)) {
-    if constexpr (PASS == 5 && SPX_GA_HASH) {
+    if constexpr (PASS == 5) {
       lds_barrier();
       for (int h = tid; h < GA_HCAP; h += GA_BLOCK) {
         const uint32_t k = hkey[h];
@@ -1667,7 +1572,6 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
   };
   for (int64_t u0 = blockIdx.x;; u0 += gridDim.x) {  // uniform
     int64_t u = u0;
-#if SPX_GA_TPERM
     if constexpr (kPerm) {
       if (u0 >= tT) break;
       u = (int64_t)(((unsigned long long)u0 * (unsigned long long)tP) % (unsigned long long)tT);
@@ -1681,7 +1585,6 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
       gbase = tpre[g];
       gtiles = tpre[g + 1] - tpre[g];
     } else
-#endif
     {
       while (g < ng && u >= gbase + gtiles) {
         gbase += gtiles;
@@ -1709,7 +1612,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           // per group at the end (integer adds: the same totals)
           E = H.E;
           agg = E <= GA_GAGG;
-          hashed = SPX_GA_HASH && !agg;
+          hashed = !agg;
           if (agg) {
             for (int e = tid; e < E; e += GA_BLOCK) { agg_m[e] = 0ull; agg_i[e] = 0ull; agg_c[e] = 0u; }
             lds_barrier();
@@ -1750,7 +1653,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
         }
       }
       lds_barrier();  // red and votes are reused by the next tile
-    } else if (SPX_GA_GBATCH && (PASS == 2 || PASS == 3)) {
+    } else if (PASS == 2 || PASS == 3) {
       // passes 2-3 in batches of GA_BATCH peaks per thread: every global read a
       // batch needs (bitmap words; ranks, then the slots' extrema) goes out before
       // its first atomic -- an atomic in between would order each read behind it
@@ -1853,14 +1756,14 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           if (k) {
             if constexpr (PASS == 2) {
               const unsigned long long bits = agg_m[h];
-              if (SPX_GA_NOFILT || (S.bitmap[k - 1u] & bits) != bits) atomicOr(&S.bitmap[k - 1u], bits);
+              atomicOr(&S.bitmap[k - 1u], bits);
               agg_m[h] = 0ull;
             } else {
               unsigned long long* kmin = reinterpret_cast<unsigned long long*>(&S.kmin[k - 1u]);
               unsigned long long* kmax = reinterpret_cast<unsigned long long*>(&S.kmax[k - 1u]);
               const unsigned long long lo = agg_m[h], hi = agg_i[h];
-              if (SPX_GA_NOFILT || lo < *kmin) atomicMin(kmin, lo);
-              if (SPX_GA_NOFILT || hi > *kmax) atomicMax(kmax, hi);
+              atomicMin(kmin, lo);
+              atomicMax(kmax, hi);
               agg_m[h] = ~0ull;
               agg_i[h] = 0ull;
             }
@@ -1894,22 +1797,20 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
             atomicAdd(&agg_c[eg], 1u);
             return;
           }
-          if constexpr (SPX_GA_HASH) {
-            if (hashed) {
-              const uint32_t want = eg + 1u;
-              uint32_t h = (eg * 2654435761u) >> (32 - 11);  // log2(GA_HCAP) = 11
-              for (int probe = 0; probe < GA_HPROBE; ++probe, h = (h + 1u) & (GA_HCAP - 1)) {
-                uint32_t k = hkey[h];
-                if (k == 0u) {
-                  const uint32_t old = atomicCAS(&hkey[h], 0u, want);
-                  k = old == 0u ? want : old;
-                }
-                if (k == want) {
-                  atomicAdd(&agg_m[h], qm);
-                  atomicAdd(&agg_i[h], qi);
-                  atomicAdd(&agg_c[h], 1u);
-                  return;
-                }
+          if (hashed) {
+            const uint32_t want = eg + 1u;
+            uint32_t h = (eg * 2654435761u) >> (32 - 11);  // log2(GA_HCAP) = 11
+            for (int probe = 0; probe < GA_HPROBE; ++probe, h = (h + 1u) & (GA_HCAP - 1)) {
+              uint32_t k = hkey[h];
+              if (k == 0u) {
+                const uint32_t old = atomicCAS(&hkey[h], 0u, want);
+                k = old == 0u ? want : old;
+              }
+              if (k == want) {
+                atomicAdd(&agg_m[h], qm);
+                atomicAdd(&agg_i[h], qi);
+                atomicAdd(&agg_c[h], 1u);
+                return;
               }
             }
           }
@@ -1918,7 +1819,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           atomicAdd(&S.gcnt[eg], 1u);
         }
       });
-      if constexpr (PASS == 5 && SPX_GA_HASH) {
+      if constexpr (PASS == 5) {
         if (hashed) hflush();  // uniform: the giant's mode
       }
     }
@@ -1932,6 +1833,7 @@ template <int STEP>
 __global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, PeaksOut out, double* prec_out,
                                                                  int32_t* charge_out, double* rt_out,
                                                                  int32_t* status, int32_t* unresolved) {
+  static_assert(STEP == 0 || STEP == 6, "steps 4 and 6a-d run over the flat grid (gap_giant_groups_kernel)");
   __shared__ int tmp[GA_NW + 1];
   __shared__ int votes[2 * GA_NW];
   __shared__ double red[GA_NW * 3];
@@ -1964,11 +1866,6 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, P
         }
       }
       if (tid == 0) { H.D = D; H.status = st; }
-    } else if constexpr (STEP == 4) {
-      if (SPX_GA_FLAT4 || st != kOk) continue;  // (SPX_GA_FLAT4: gap_giant_groups_kernel)
-      int E = 0;
-      st = gap_groups<false>(S, A.P, H.D, tmp, votes, E);
-      if (tid == 0) { H.E = E; H.status = st; }
     } else {
       const int64_t s0 = A.v.cluster_off[c], n = A.v.cluster_off[c + 1] - s0;
       const int64_t p0 = A.v.spec_off[s0], N = A.v.spec_off[A.v.cluster_off[c + 1]] - p0;
@@ -1976,19 +1873,11 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, P
         st = gap_body_nf(A.v, A.P, S, c, out, tmp, red, votes, reinterpret_cast<uint32_t*>(stage));
         __syncthreads();
       } else if (st == kOk) {
-#if SPX_GA_FLAT6
         // the groups were emitted by gap_giant_groups_kernel<4..7>
         (void)n;
         (void)N;
         (void)p0;
         st = H.gany ? kOk : kEmpty;
-#else
-        const GiantExtent X = giant_extent(H, A.P);
-        int ex_m, ex_i;
-        frexp(fmax(fabs(X.lo), fabs(X.hi)) * (double)N, &ex_m);
-        frexp(X.imax * (double)N, &ex_i);
-        st = gap_emit<false>(S, A.P, c, n, N, p0, H.E, 61 - ex_m, 61 - ex_i, out, tmp, red, votes);
-#endif
       }
       if (st == kDeferred) {
         if (tid == 0) { status[c] = kDeferred; atomicAdd(unresolved, 1); }

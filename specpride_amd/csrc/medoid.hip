@@ -37,35 +37,8 @@ constexpr int MD_NMAX = 64;
 #ifndef SPX_MD_MINW
 #define SPX_MD_MINW 7
 #endif
-#ifndef SPX_MD_MFMA
-#define SPX_MD_MFMA 1  // P4's pair counts on the matrix cores (FP4 Gram tiles), not AND + popcount
-#endif
 #ifndef SPX_MD_MFMA_NMIN
 #define SPX_MD_MFMA_NMIN 32  // ... for clusters of more spectra than this
-#endif
-#ifndef SPX_MD_P5L
-#define SPX_MD_P5L 1  // P5 with one lane per spectrum (rows on wave 0, columns on wave 1)
-#endif
-#ifndef SPX_MD_RECIP
-#define SPX_MD_RECIP 1  // P4's quotients from per-spectrum reciprocals (exact, md_dist_r)
-#endif
-#ifndef SPX_MD_R32
-#define SPX_MD_R32 1  // column ranks from 32-bit occupancy words with u16 prefixes
-#endif
-#ifndef SPX_MD_MBC
-#define SPX_MD_MBC 1  // P3's spectrum index from spectrum-end bits by v_mbcnt
-#endif
-#ifndef SPX_MD_L1RUNS
-#define SPX_MD_L1RUNS 1  // level-1 pass: one LDS atomic per run of lanes sharing a word
-#endif
-#ifndef SPX_MD_SWZ
-#define SPX_MD_SWZ 1  // P3's row words swizzled per bit position (no same-word LDS atomics)
-#endif
-#ifndef SPX_MD_P6W
-#define SPX_MD_P6W 1  // P6's argmin in wave 0 right after P5 (totals in registers)
-#endif
-#ifndef SPX_MD_P1B
-#define SPX_MD_P1B 1  // P1 bins a batch of 8 branch-free; the rare exact divide once per batch
 #endif
 constexpr int MD_KWMAX = SPX_MD_KWMAX;  // row words (odd stride): <= 64 * MD_KWMAX occupied bins per small cluster
 
@@ -192,20 +165,20 @@ __device__ __forceinline__ void md_defer(int64_t c, int64_t s0, int n, int32_t* 
 //   P1  flat coalesced pass over the cluster's peaks (peak r = u*256 + tid,
 //       8 loads in flight per thread): absolute bin ceil(mz/tol) < 32,768, kept
 //       in registers as packed u16 (<= MR_UMAX per thread), union bitmap in LDS
-//       (32-bit LDS atomics).  Branch-free per batch of 8 (SPX_MD_P1B): the
+//       (32-bit LDS atomics).  Branch-free per batch of 8: the
 //       reciprocal product's ceil where certain and in range, one "bad" mask
 //       settled by md_bin's exact divide once per batch.  The xcorr is a set
 //       intersection: no range pass, and unsorted spectra need no special path.
-//   P2  popcount prefix -> K compact columns (SPX_MD_R32: a u16 prefix per
+//   P2  popcount prefix -> K compact columns (a u16 prefix per
 //       32-bit occupancy word)
 //   P3  bit-packed rows from the register bins: column = rank (a u16 prefix and
 //       one bfe + popcount), spectrum = the slice's spectrum-end word and its
-//       prefix handed out by readlane, counted by two v_mbcnt (SPX_MD_MBC); rows
+//       prefix handed out by readlane, counted by two v_mbcnt; rows
 //       set by 32-bit LDS atomics into words swizzled per bit position
-//       (SPX_MD_SWZ: a spectrum's neighbouring columns -- consecutive lanes --
+//       (a spectrum's neighbouring columns -- consecutive lanes --
 //       no longer serialise on one word)
 //   P4  pair counts: past 32 spectra on the matrix cores (FP4 0/1 Gram tiles, one
-//       per wave, SPX_MD_MFMA), else one thread per pair i <= j by AND + popcount;
+//       per wave), else one thread per pair i <= j by AND + popcount;
 //       then d_ij = 1 - c_ij/min(p_i, p_j) (exact reciprocal form, md_dist_r) into
 //       the reference's n x n matrix (upper triangle incl. the diagonal, zeros
 //       below: most_similar_representative.py:91-93), aliasing the dead bitmap and rows
@@ -240,13 +213,13 @@ struct MedoidRegSmem {
       unsigned long long bits[MR_WMAX];
       uint32_t pre[MR_WMAX];
       unsigned long long rows[MD_NMAX * KWMAX];
-      unsigned long long sbits[UMAX * BLOCK / 64];  // bit r: peak r starts spectrum >= 1 (SPX_MD_MBC: ends a spectrum)
+      unsigned long long sbits[UMAX * BLOCK / 64];  // bit r: peak r starts spectrum >= 1 (ends a spectrum)
       uint8_t spre[UMAX * BLOCK / 64];              // spectra started (ended) before word w
     } a;                                         // P0..P4a
     double d[MR_TRI];                            // P4b..P5: d(i, j), j >= i, row-major packed
     struct {
       double d[MR_TRI];
-      double col[MD_NMAX];                       // P5 (SPX_MD_P5L): column sums, past d
+      double col[MD_NMAX];                       // P5: column sums, past d
     } t;
   } u;
   int32_t soff[MD_NMAX + 1];
@@ -303,13 +276,9 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   }
   for (int j = 1 + tid; j < n; j += BLOCK) {
     const int r = L.soff[j];
-#if SPX_MD_MBC
     // end bits: peak r - 1 closes spectrum j - 1 (r >= 1 unless spectrum 0 is
     // empty, and then the binary search decides)
     if (r >= 1 && r < np) atomicOr(&L.u.a.sbits[(r - 1) >> 6], 1ull << ((r - 1) & 63));
-#else
-    if (r < np) atomicOr(&L.u.a.sbits[r >> 6], 1ull << (r & 63));
-#endif
   }
   __syncthreads();
   const bool has_empty = L.red[1] != 0;
@@ -346,7 +315,7 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
           mb[bt & 1][q] = mzc[r < np ? r : 0];
         }
       }
-      if (bt > 0 && SPX_MD_P1B) {  // bin batch bt - 1
+      if (bt > 0) {  // bin batch bt - 1
         const int pb = bt - 1;
         uint32_t* const bits32 = reinterpret_cast<uint32_t*>(L.u.a.bits);
         uint32_t bad = 0u;
@@ -434,7 +403,6 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   {
     // all MR_WMAX records (P0 cleared them), RPT
     // contiguous per thread, read unconditionally: the reads pipeline
-#if SPX_MD_R32
     // per 32-bit word: a u16 prefix (K <= 32,768) in the same 2 KB
     constexpr int RPT = 2 * MR_WMAX / BLOCK;
     const int w0 = tid * RPT;
@@ -452,22 +420,6 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       pre16[w0 + k] = (uint16_t)base;
       base += __popc(b[k]);
     }
-#else
-    constexpr int RPT = MR_WMAX / BLOCK;
-    const int w0 = tid * RPT;
-    unsigned long long b[RPT];
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) b[k] = L.u.a.bits[w0 + k];
-    int local = 0;
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) local += __popcll(b[k]);
-    int base = block_exclusive_scan<BLOCK, int, true>(local, L.tmp, K);
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      L.u.a.pre[w0 + k] = (uint32_t)base;
-      base += __popcll(b[k]);
-    }
-#endif
   }
   // row stride KW is odd: lanes reading rows j, j+1, ... at one word hit
   // different LDS banks (an even stride of u64s would fold them together)
@@ -487,13 +439,8 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
     if (lane < UMAX && w < nsw) { my_sw = L.u.a.sbits[w]; my_sp = L.u.a.spre[w]; }
   }
   __syncthreads();
-#if !SPX_MD_MBC
-  const unsigned long long upto = (2ull << lane) - 1ull;  // bits 0..lane
-#endif
-#if SPX_MD_SWZ
   const uint32_t swz_nw = 2u * (uint32_t)KW;  // 32-bit words per row
   const uint32_t swz_m = swz_nw >= 32u ? 31u : (1u << (31 - __clz((int)swz_nw))) - 1u;  // 2^k - 1 < swz_nw
-#endif
 #pragma unroll
   for (int u = 0; u < UMAX; ++u) {
     if (u * BLOCK < np) {  // uniform
@@ -503,30 +450,19 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       const int spw = __builtin_amdgcn_readlane(my_sp, u);
       if (r < np) {
         const uint32_t b = (bins[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-#if SPX_MD_R32
         // rank in a 32-bit word: its u16 prefix + the popcount of the bits below b
         const uint32_t w32 = b >> 5;
         const int col = (int)reinterpret_cast<const uint16_t*>(L.u.a.pre)[w32] +
                         __popc(__builtin_amdgcn_ubfe(reinterpret_cast<const uint32_t*>(L.u.a.bits)[w32], 0u, b & 31u));
-#else
-        const int col = (int)L.u.a.pre[b >> 6] + __popcll(L.u.a.bits[b >> 6] & ((1ull << (b & 63)) - 1ull));
-#endif
         // empty spectra share a start bit: then the binary search
         const unsigned long long sw = ((unsigned long long)swhi << 32) | swlo;
-#if SPX_MD_MBC
         // spectra closed before peak r: the word's prefix + its end bits below this
         // lane (peak r is bit `lane` of its word) -- two v_mbcnt
         (void)sw;
         const int sp = has_empty ? spectrum_of(L.soff, n, r)
                                  : (int)__builtin_amdgcn_mbcnt_hi(swhi, __builtin_amdgcn_mbcnt_lo(swlo, (uint32_t)spw));
-#else
-        const int sp = has_empty ? spectrum_of(L.soff, n, r) : spw + __popcll(sw & upto);
-#endif
         // 32-bit halves: consecutive peaks of a spectrum share a row word, and
         // same-address LDS atomics serialise -- half as many per address
-#ifdef SPX_DG_P3LANE  // diagnostic (wrong results): each lane ORs into a word of its own -- no conflicts
-        atomicOr(reinterpret_cast<uint32_t*>(L.u.a.rows) + (tid & 255) + ((__mul24(sp, KW) + (col >> 5)) & 0), 1u << (col & 31));
-#elif SPX_MD_SWZ
         // word (col/32 + (col & m)) mod NW32: a bijection per bit position, so P4's
         // row-AND popcounts and Gram sums are unchanged, while neighbouring columns of a
         // spectrum -- consecutive lanes -- land in different words (a shared word
@@ -534,13 +470,9 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
         uint32_t wq = (uint32_t)(col >> 5) + ((uint32_t)col & swz_m);
         wq = min(wq, wq - swz_nw);
         atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[__mul24(sp, KW)]) + wq, 1u << (col & 31));
-#else
-        atomicOr(reinterpret_cast<uint32_t*>(&L.u.a.rows[__mul24(sp, KW)]) + (col >> 5), 1u << (col & 31));
-#endif
       }
     }
   }
-#if SPX_MD_RECIP
   // each spectrum's exact reciprocal for P4's quotients (totals is free until P5;
   // spectra here hold at most PMAX <= 65,536 peaks, md_dist_r's checked range)
   static_assert(PMAX <= 65536, "md_dist_r's exact range");
@@ -548,7 +480,6 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
     const int p = L.soff[tid + 1] - L.soff[tid];
     L.totals[tid] = p > 0 ? 1.0 / (double)p : 0.0;
   }
-#endif
   __syncthreads();
   SPX_STAMP(4);
 
@@ -560,7 +491,7 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
   // the one 32 x 32 tile and its epilogue while the pairs spread over the whole workgroup
   // (stamps, configs[4]: P4 n 41-50 14.4k -> 11.7k cycles, n 11-25 5.7k -> 8.7k)
   bool mfma_p4 = false;
-  if constexpr (SPX_MD_MFMA && BLOCK == MD_BLOCK) mfma_p4 = n > SPX_MD_MFMA_NMIN;  // uniform
+  if constexpr (BLOCK == MD_BLOCK) mfma_p4 = n > SPX_MD_MFMA_NMIN;  // uniform
   if (mfma_p4) {
   // P4 on the matrix cores: c_ij = |B_i ∩ B_j| = the Gram of the 0/1 rows, one
   // 32 x 32 tile per wave -- (0,0) for n <= 32; (0,0), (0,1), (1,1) for n <= 64 --
@@ -599,12 +530,8 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
         const int i = ta * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
         if (i <= j && j < n) {
           const uint32_t cnt = (uint32_t)acc[q];
-#if SPX_MD_RECIP
           L.u.d[row_start(i) + j - i] =
               md_dist_r(cnt, L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
-#else
-          L.u.d[row_start(i) + j - i] = md_dist(cnt, L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
-#endif
         }
       }
     }
@@ -640,24 +567,16 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
     for (int q = 0; q < PPT; ++q) {
       if (pij[q] >= 0) {
         const int i = pij[q] >> 8, j = pij[q] & 0xff;
-#if SPX_MD_RECIP
         L.u.d[row_start(i) + j - i] =
             md_dist_r(pc[q], L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
-#else
-        L.u.d[row_start(i) + j - i] = md_dist(pc[q], L.soff[i + 1] - L.soff[i], L.soff[j + 1] - L.soff[j]);
-#endif
       }
     }
   }
   __syncthreads();
   // D(a, b) of the reference's dense matrix: the upper triangle incl. the
   // diagonal, zeros below (most_similar_representative.py:91-93)
-#if !SPX_MD_P5L
-  auto dval = [&](int a, int b) -> double { return b >= a ? L.u.d[row_start(a) + b - a] : 0.0; };
-#endif
 
   SPX_STAMP(5);
-#if SPX_MD_P5L
   // P5: totals, one lane per spectrum (n <= 64): wave 0 sums row i, wave 1 column i, each
   // with numpy's leaf order -- 8 strided accumulators over j < lim = n - n % 8 (in order),
   // combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the sequential tail; n < 8 is all
@@ -695,54 +614,12 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
     const double t = (sum + L.u.t.col[i5]) / (double)n;  // (row + col) / n
     L.totals[i5] = t;
     if (totals_out) totals_out[s0 + i5] = t;
-#if SPX_MD_P6W
     sum = t;  // wave 0 keeps lane i's total for P6
-#endif
   }
-#else
-  // P5: totals, 16 lanes per spectrum (8 row accumulators, 8 column ones)
-  const int k = lane & 7;
-  const bool colside = (lane & 8) != 0;
-  const int lim = n - (n % 8);
-  for (int i0 = 0; i0 < n; i0 += BLOCK / 16) {  // uniform
-    const int i = i0 + tid / 16;
-    const bool valid = i < n;
-    const int ii = valid ? i : 0;
-    // row ii or column ii of D
-    auto e = [&](int j) { return colside ? dval(j, ii) : dval(ii, j); };
-    double s = 0.0;
-    if (n >= 8) {
-      double r = e(k);
-      for (int j = 8 + k; j < lim; j += 8) r += e(j);
-      r += xor_f64<1>(r);
-      r += xor_f64<2>(r);
-      r += xor_f64<4>(r);  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))
-      s = r;
-      for (int j = lim; j < n; ++j) s += e(j);  // the sequential tail
-    } else {
-      for (int j = 0; j < n; ++j) s += e(j);  // 0.0 + a0 + a1 + ...
-    }
-    s = 0.0 + s;
-    const double other = xor_f64<8>(s);
-    if (valid && (lane & 15) == 0) {
-      const double t = (s + other) / (double)n;  // (row + col) / n
-      L.totals[i] = t;
-      if (totals_out) totals_out[s0 + i] = t;
-    }
-  }
-#endif
-#if SPX_MD_P5L && SPX_MD_P6W
   // P6 straight from wave 0's registers (lane i holds total i): no barrier, no LDS
   SPX_STAMP(6);
   if (wid == 0) {
     double t = valid5 ? sum : __longlong_as_double(0x7ff0000000000000ll);
-#else
-  __syncthreads();
-  SPX_STAMP(6);
-  // P6: first index of the minimum (:103-110)
-  if (tid < kWave) {
-    double t = tid < n ? L.totals[tid] : __longlong_as_double(0x7ff0000000000000ll);
-#endif
     int idx = tid < n ? tid : 0x7fffffff;
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
@@ -1017,7 +894,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_l1_kernel(CsrView v, MedoidPa
     if (M.l1_off < 0 || !md_range(M, blo, nw1) || nw1 == 0 || k0 >= k1) continue;
     for (int w = tid; w < nw1; w += MD_BLOCK) l1s[w] = 0ull;
     __syncthreads();
-#if SPX_MD_L1RUNS
     // neighbouring peaks fall in the same 64-bin block or the next: ~40 lanes of a
     // wave OR into one level-1 word, so each run of lanes with one 32-bit word
     // ORs its bits together first and its last lane issues the atomic
@@ -1028,12 +904,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_l1_kernel(CsrView v, MedoidPa
       uint32_t val = act ? 1u << (blk & 31) : 0u;
       if (wave_or_runs(key, val) && act) atomicOr(&l1s32[key], val);
     });
-#else
-    md_unit_peaks(v, k0, k1, [&](double m) {
-      const int64_t blk = (md_bin(m, P) - blo) >> 6;
-      atomicOr(&l1s[blk >> 6], 1ull << (blk & 63));
-    });
-#endif
     __syncthreads();
     unsigned long long* l1 = reinterpret_cast<unsigned long long*>(arena + M.l1_off);
     for (int w = tid; w < nw1; w += MD_BLOCK)
@@ -1251,21 +1121,14 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_scan_kernel(const MedoidMeta*
 
 // Bit rows, one wave per (padded) row: zero the row's words, drain the stores,
 // then OR in one bit per peak (peaks may be unsorted; duplicates are idempotent).
-#ifndef SPX_MD_FILL_LDS
-#define SPX_MD_FILL_LDS 1
-#endif
 constexpr int MD_FILL_KW = 512;  // row words a wave builds in LDS (4 KB; 32,768 columns)
 constexpr int MD_FILL_U = 4;     // 64-peak chunks of a spectrum whose loads go out together
 
-#ifndef SPX_MD_FILL_FLAT
-#define SPX_MD_FILL_FLAT 1  // fill: each wave a contiguous run of the flat (cluster, row) list
-#endif
 __global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, MedoidParams P, const MedoidMeta* meta,
                                                                const int32_t* n_deferred, const int64_t* row_base,
                                                                char* arena) {
   const int32_t nd = *n_deferred;
   constexpr int W = MD_BLOCK / kWave;
-#if SPX_MD_FILL_LDS
   // One wave per row.  A row of at most MD_FILL_KW words is built in the wave's
   // LDS slice (no zeroing round trip through memory, no global atomics) and then
   // written with plain coalesced stores; the peaks of up to MD_FILL_U chunks
@@ -1273,8 +1136,6 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, Medoid
   // (three dependent round trips per 256 peaks instead of three per 64).
   __shared__ unsigned long long lrow[W][MD_FILL_KW];
   unsigned long long* L = lrow[wave_id()];
-#endif
-#if SPX_MD_FILL_FLAT
   // Every padded row of every deferred cluster, as one flat list (row_base: the
   // exclusive scan of the padded row counts); wave q takes the contiguous run
   // [q * per, (q + 1) * per), so the owner changes rarely and a giant's rows are
@@ -1293,19 +1154,7 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, Medoid
     const int r = (int)(g - row_base[o]);
     const MedoidTables Tb = md_tables(arena, M);
     unsigned long long* rows = reinterpret_cast<unsigned long long*>(arena + M.rows_off);
-#else
-  for (int32_t di = blockIdx.y; di < nd; di += gridDim.y) {
-    const MedoidMeta M = meta[di];
-    if (!M.ok) continue;
-    const MedoidTables Tb = md_tables(arena, M);
-    unsigned long long* rows = reinterpret_cast<unsigned long long*>(arena + M.rows_off);
-    const int npad = (M.n + MD_GT - 1) / MD_GT * MD_GT;
-#endif
-#if SPX_MD_FILL_LDS
     if (M.KW <= MD_FILL_KW) {  // uniform
-#if !SPX_MD_FILL_FLAT
-      for (int r = blockIdx.x * W + wave_id(); r < npad; r += gridDim.x * W) {
-#endif
         unsigned long long* row = rows + (int64_t)r * M.KW;
         for (int w = lane_id(); w < M.KW; w += kWave) L[w] = 0ull;
         if (r < M.n) {
@@ -1353,17 +1202,9 @@ __global__ __launch_bounds__(MD_BLOCK) void medoid_fill_kernel(CsrView v, Medoid
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the next row's zeroing after these reads
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#if !SPX_MD_FILL_FLAT
-      }
-#endif
       continue;
     }
-#endif
-#if SPX_MD_FILL_FLAT
     {
-#else
-    for (int r = blockIdx.x * W + wave_id(); r < npad; r += gridDim.x * W) {
-#endif
       unsigned long long* row = rows + (int64_t)r * M.KW;
       for (int w = lane_id(); w < M.KW; w += kWave) row[w] = 0ull;
       if (r >= M.n) continue;
@@ -1390,13 +1231,7 @@ typedef int md_i32x16 __attribute__((ext_vector_type(16)));
 #define SPX_GR_MINW 3  // 3 waves per SIMD (167 unified registers, the accumulators in VGPRs)
 #endif
 constexpr int MD_GR_PF = SPX_GR_PF;  // words in flight per lane (divides 8: KW is a multiple of 8)
-#ifndef SPX_GR_FP4
-#define SPX_GR_FP4 1
-#endif
-#ifndef SPX_GR_TR
-#define SPX_GR_TR 1  // the mirrored Gram entries written through a wave-private LDS transpose
-#endif
-// SPX_GR_FP4: the 0/1 operands as FP4 e2m1 (1.0 = nibble 0b0010) through
+// The 0/1 operands as FP4 e2m1 (1.0 = nibble 0b0010) through
 // v_mfma_f32_32x32x64_f8f6f4 (the MX-scaled instruction at unit scale): one MFMA per
 // 64-bin word and (a, b) block instead of two, from half the expansion VALU (a
 // 32-bin half word -> 4 dwords of 8 nibbles, 2 ops each).  Products are 1.0 or 0,
@@ -1443,9 +1278,7 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
                                                                    const int64_t* tile_base, char* arena) {
   const int lane = lane_id();
   const int fr = lane & 31, fh = lane >> 5;
-#if SPX_GR_TR
   __shared__ uint32_t tr[MD_BLOCK / kWave][32][33];
-#endif
   const int32_t nd = *n_deferred;
   const int64_t total = tile_base[nd];
   const int64_t wstride = (int64_t)gridDim.x * (MD_BLOCK / kWave);
@@ -1462,20 +1295,12 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
     const unsigned long long* rows = reinterpret_cast<const unsigned long long*>(arena + M.rowsT_off);
     // rows this lane loads: A blocks 0/1 (64-row tile), B blocks 0..NB-1 (zero past npad)
     const unsigned long long* pa = rows + ti * MD_WT + fr;
-#ifdef SPX_GR_DIAG  // diagnostic only (results wrong): every wave reads the same B rows (L2-resident)
-    const unsigned long long* pb = rows + fr;
-#else
     const unsigned long long* pb = rows + (int64_t)tj * MD_WTN + fr;
-#endif
     bool bok[MD_GR_NB];
 #pragma unroll
     for (int b = 0; b < MD_GR_NB; ++b) bok[b] = (int64_t)tj * MD_WTN + b * 32 < npad;
 
-#if SPX_GR_FP4
     md_f32x16 acc[2][MD_GR_NB];
-#else
-    md_i32x16 acc[2][MD_GR_NB];
-#endif
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1494,16 +1319,6 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
     };
 #pragma unroll
     for (int q = 0; q < MD_GR_PF; ++q) load(q, ring[q]);
-#if !SPX_GR_FP4
-    // one fragment: 16 bytes of the 32-bin half c, dwords 4h..4h+3
-    auto frag = [&](uint32_t c) __attribute__((always_inline)) {
-      md_i32x4 f;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) f[g] = (int)((c >> (4 * fh + g)) & 0x01010101u);
-      return f;
-    };
-#endif
-#if SPX_GR_FP4
     // lane half fh takes bins 32fh..32fh+31 of the word: dword g, nibble p = bin
     // 32fh + g + 4p (the same k order for A and B)
     auto frag4 = [&](uint64_t w) __attribute__((always_inline)) {
@@ -1516,7 +1331,6 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
       f[4] = f[5] = f[6] = f[7] = 0;
       return f;
     };
-#endif
     for (int w0 = 0; w0 < KW; w0 += MD_GR_PF) {  // KW is a multiple of 8
 #pragma unroll
       for (int q = 0; q < MD_GR_PF; ++q) {
@@ -1524,7 +1338,6 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
 #pragma unroll
         for (int k = 0; k < NR; ++k) cur[k] = ring[q][k];
         load(w0 + q + MD_GR_PF, ring[q]);
-#if SPX_GR_FP4
         {
           md_i32x8 fa[2], fb[MD_GR_NB];
 #pragma unroll
@@ -1537,21 +1350,6 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
             for (int b = 0; b < MD_GR_NB; ++b)
               acc[a][b] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[a], fb[b], acc[a][b], 4, 4, 0, 0, 0, 0);
         }
-#else
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          md_i32x4 fa[2], fb[MD_GR_NB];
-#pragma unroll
-          for (int a = 0; a < 2; ++a) fa[a] = frag((uint32_t)(cur[a] >> (32 * hf)));
-#pragma unroll
-          for (int b = 0; b < MD_GR_NB; ++b) fb[b] = frag((uint32_t)(cur[2 + b] >> (32 * hf)));
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < MD_GR_NB; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[a], fb[b], acc[a][b], 0, 0, 0);
-        }
-#endif
       }
     }
     // C/D layout (32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
@@ -1568,12 +1366,8 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
           if (i < M.n && j < M.n && i <= j) {
             const uint32_t cnt = (uint32_t)acc[a][b][q];
             cmat[(int64_t)i * M.n + j] = cnt;  // row i: the lanes write consecutive j
-#if !SPX_GR_TR
-            cmat[(int64_t)j * M.n + i] = cnt;  // column: one line per lane
-#endif
           }
         }
-#if SPX_GR_TR && !defined(SPX_DG_NOMIRROR)  // (diagnostic build: no mirrored entries, totals wrong by design)
         // the mirrored entries (j, i): through a wave-private 32 x 33 LDS tile so
         // that the lanes write consecutive columns of each row j (the direct
         // column store put every lane on its own cache line: 19% of the kernel)
@@ -1591,7 +1385,6 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_GR_MINW) void medoid_gram_reg_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the next block's writes after these reads
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
       }
   }
 }
@@ -1639,12 +1432,6 @@ __device__ __forceinline__ void dual_leaf_at(const F& f, int lo, int m, int i, d
   col = cs;
 }
 
-#ifndef SPX_MD_LEAF_W
-#define SPX_MD_LEAF_W 1
-#endif
-#ifndef SPX_MD_LEAF_B
-#define SPX_MD_LEAF_B 1  // leaves: count loads issued 16 at a time, ahead of the distances
-#endif
 
 // dual_leaf_at over column i of the count matrix (colp = cmat + i, row stride n) with
 // the loads separated from the arithmetic: 16 counts in flight per lane, then the
@@ -1707,7 +1494,7 @@ constexpr int MD_LEAF_MAX = 128;  // a numpy pairwise leaf holds at most 128 ter
 
 // Leaf sums, grid-stride over (cluster, leaf, 256-wide chunk of i): thread i
 // reads column i of the symmetric count matrix (coalesced across i).  With
-// SPX_MD_LEAF_W each wave first writes the leaf's spectrum sizes and their
+// Each wave first writes the leaf's spectrum sizes and their
 // reciprocals into its own LDS slice (no workgroup barrier: a wave's LDS
 // operations complete in order), and the j loop reads them back as broadcasts:
 // one division per spectrum and lane instead of one per (i, j).  Clusters whose
@@ -1718,10 +1505,8 @@ constexpr int MD_LEAF_MAX = 128;  // a numpy pairwise leaf holds at most 128 ter
 __global__ __launch_bounds__(MD_BLOCK, SPX_MD_LEAF_MINW) void medoid_leaves_kernel(CsrView v, const MedoidMeta* meta,
                                                                  const int32_t* n_deferred, const int64_t* unit_base,
                                                                  char* arena) {
-#if SPX_MD_LEAF_W
   __shared__ double rj_s[MD_BLOCK / kWave][MD_LEAF_MAX];
   __shared__ int pj_s[MD_BLOCK / kWave][MD_LEAF_MAX];
-#endif
   const int32_t nd = *n_deferred;
   const int64_t total = unit_base[nd];
   for (int64_t u = blockIdx.x; u < total; u += gridDim.x) {
@@ -1737,7 +1522,6 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_LEAF_MINW) void medoid_leaves_kern
     const uint32_t* cmat = reinterpret_cast<const uint32_t*>(arena + M.cmat_off);
     const int64_t* so = v.spec_off + M.s0;
     double row, col;
-#if SPX_MD_LEAF_W
     if (m <= MD_LEAF_MAX) {  // uniform
       double* R = rj_s[wave_id()];
       int* Pp = pj_s[wave_id()];
@@ -1760,20 +1544,14 @@ __global__ __launch_bounds__(MD_BLOCK, SPX_MD_LEAF_MINW) void medoid_leaves_kern
         if (i >= n) continue;
         const int pi = (int)pi64;
         const double ri = pi > 0 ? 1.0 / (double)pi : 0.0;
-#if SPX_MD_LEAF_B
         dual_leaf_cols(cmat + i, n, [&](int j, uint32_t c) { return md_dist_r(c, pi, ri, Pp[j - lo], R[j - lo]); }, lo,
                        m, i, row, col);
-#else
-        dual_leaf_at([&](int j) { return md_dist_r(cmat[(int64_t)j * n + i], pi, ri, Pp[j - lo], R[j - lo]); }, lo,
-                     m, i, row, col);
-#endif
       } else {
         if (i >= n) continue;
         dual_leaf_at([&](int j) { return md_dist(cmat[(int64_t)j * n + i], pi64, so[j + 1] - so[j]); }, lo, m, i,
                      row, col);
       }
     } else
-#endif
     {
       if (i >= n) continue;
       const int64_t pi = so[i + 1] - so[i];

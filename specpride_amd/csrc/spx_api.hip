@@ -19,6 +19,26 @@
 #include <vector>
 
 #include "../../include/specpride.h"
+
+// Earlier rounds' A/B switches were folded into the source at their kept settings
+// (round 6), and the diagnostic variants whose results were wrong by design were
+// deleted: git history and profiles/r0*_ab_* keep the record.  A build that still asks
+// for one of them fails here instead of silently producing something else.
+#if defined(SPX_DG_NOMZ) || defined(SPX_DG_NOBAR) || defined(SPX_DG_P3LANE) || defined(SPX_DG_NOMIRROR) || \
+    defined(SPX_GR_DIAG) || defined(SPX_QF_DIAG) || defined(SPX_BR_FOLD) || defined(SPX_BF_RING) ||       \
+    defined(SPX_BF_REVERSE)
+#error "diagnostic / rejected variants are not part of libspecpride_hip (see git history)"
+#endif
+#if defined(SPX_GA_FLAT4) || defined(SPX_GA_FLAT6) || defined(SPX_GA_HASH) || defined(SPX_GA_HASH2) ||     \
+    defined(SPX_GA_HASH3) || defined(SPX_GA_NOFILT) || defined(SPX_GA_TPERM) || defined(SPX_GA_GBATCH) ||  \
+    defined(SPX_GA_HYBRID) || defined(SPX_GA_P3INT) || defined(SPX_GA_BSKIP) || defined(SPX_GA_P2B) ||     \
+    defined(SPX_GA_EARLY) || defined(SPX_GA_DEFERBIG) || defined(SPX_MD_MFMA) || defined(SPX_MD_P5L) ||    \
+    defined(SPX_MD_RECIP) || defined(SPX_MD_R32) || defined(SPX_MD_MBC) || defined(SPX_MD_L1RUNS) ||       \
+    defined(SPX_MD_SWZ) || defined(SPX_MD_P6W) || defined(SPX_MD_P1B) || defined(SPX_MD_FILL_LDS) ||       \
+    defined(SPX_MD_FILL_FLAT) || defined(SPX_MD_LEAF_W) || defined(SPX_MD_LEAF_B) || defined(SPX_GR_FP4) ||\
+    defined(SPX_GR_TR) || defined(SPX_WALK_R)
+#error "this A/B switch was folded into the source at its kept setting in round 6 (see git history)"
+#endif
 #include "best_score.hip"
 #include "bin_mean.hip"
 #include "bin_mean_seg.hip"
@@ -228,7 +248,7 @@ int spx_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
   return SPX_SUCCESS;
 }
 
-int spx_medoid_gram_operand_bits(void) { return SPX_GR_FP4 ? 4 : 8; }
+int spx_medoid_gram_operand_bits(void) { return 4; }  // FP4 e2m1 (the i8 form is in git history, round 3)
 
 // ------------------------------------------------------------------ bin-mean
 // range records of the split path: every range holds >= SP_CAPW occupied bins
@@ -609,22 +629,15 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   hipLaunchKernelGGL(spx::gap_giant_step_kernel<0>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
                      unresolved);
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<3>, tiles, blk, 0, s, A);
-#if SPX_GA_FLAT4
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<0>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<1>, per, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<2>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<3>, tiles, blk, 0, s, A);
-#else
-  hipLaunchKernelGGL(spx::gap_giant_step_kernel<4>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
-                     unresolved);
-#endif
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<5>, tiles, blk, 0, s, A);
-#if SPX_GA_FLAT6
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<4>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<5>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<6>, per, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<7>, tiles, blk, 0, s, A);
-#endif
   hipLaunchKernelGGL(spx::gap_giant_step_kernel<6>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
                      unresolved);
   return check_launch("gap_giant pipeline");
@@ -681,15 +694,17 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
     arena += medoid_cluster_bytes(hco[c + 1] - hco[c], hso[hco[c + 1]] - hso[hco[c]]);
   }
   // Room for run-time deferrals on top: the arena bytes of the 256 largest at-risk
-  // clusters (all of them when fewer), and never less than 8 slots of the largest
-  // small cluster.  A call that still runs out reports SPX_REP_ARENA for the rest, and
-  // a re-run with those clusters in `extra` has room for every one.
+  // clusters (all of them when fewer) PLUS 8 slots of the largest small cluster -- the
+  // fixed headroom is for clusters deferred for another reason (an m/z past the
+  // register kernel's bin range), which the at-risk list does not predict.  A call that
+  // still runs out reports SPX_REP_ARENA for the rest, and a re-run with those clusters
+  // in `extra` has room for every one.
   const size_t slots = std::min<size_t>(risk.size(), 256);
   if (slots < risk.size())
     std::nth_element(risk.begin(), risk.begin() + (ptrdiff_t)slots, risk.end(), std::greater<size_t>());
   size_t reserve = 0;
   for (size_t k = 0; k < slots; ++k) reserve += risk[k];
-  reserve = std::max(reserve, 8 * margin);
+  reserve += 8 * margin;
   return fixed + arena + reserve + (size_t(1) << 20);
 }
 

@@ -236,6 +236,11 @@ class HostPipeline:
             c0, c1 = slot.chunk
             with torch.cuda.device(self.device):
                 md = engine.medoid(batch, out=md, check=True)  # the current stream, synchronised reads
+                # the slot's next H2D (_h2d waits on slot.done) is ordered after this medoid
+                # by an event, not by the implicit sync of the read below
+                done = torch.cuda.Event()
+                done.record(torch.cuda.current_stream(self.device))
+                slot.done = done
                 r2 = md.rep[:c1 - c0].cpu().numpy()
             res["rep"][c0:c1] = np.where(r2 >= 0, r2 + co[c0], r2)
 
