@@ -490,6 +490,12 @@ constexpr int BR_PFC = SPX_BR_PFC;    // phase-C (m/z, intensity) loads in fligh
 // none 2.24, 6 2.20, 8 2.14 ms); 12 or 20 at 4 waves/SIMD measured 2.28 / 2.23 ms
 // (fewer clusters in flight)
 constexpr int BR_KM = SPX_BR_KM;
+#ifndef SPX_BR_PFA_MD
+#define SPX_BR_PFA_MD 6  // the fused pass's phase-A ring depth (8: 11.32 ms, 6: 11.16 at KM 4; configs[4])
+#endif
+#ifndef SPX_BR_KM_MD
+#define SPX_BR_KM_MD 4  // the same for the fused pass (phase A holds its medoid bins too: 8 spilled, 12.37 ms; 6: 12.29; 4: 11.32; 2: 11.17)
+#endif
 #ifndef SPX_BR_BG
 #define SPX_BR_BG 4  // phase-B steps whose LDS reads issue together (8: 2 VGPRs spilled)
 #endif
@@ -502,6 +508,10 @@ struct alignas(16) BinAcc {
 
 // LDS of the register path.  The occupancy bitmap (32-bit words + per-word rank
 // prefix) is dead once every code is a slot, so the accumulators overlay it.
+// The fused pass (bin_mean_medoid_kernel) also keeps the medoid's union bitmap of
+// ceil(mz/tol) bins (< 32,768: most_similar_representative.py:15) and its u16 prefix
+// in the slack of phases A-B (the accumulators of C-D need more LDS than A-B).
+constexpr int BR_MDW32 = 1024;  // 32-bit words of the medoid's bins (32,768 bins)
 struct BinRegSmem {
   union alignas(16) {
     struct {
@@ -509,6 +519,8 @@ struct BinRegSmem {
       // a lane's no-contribution code maps to its own dummy accumulator record
       uint32_t bits[BR_W32 + kWave];
       uint16_t pre[BR_W32 + kWave];
+      alignas(16) uint32_t mdbits[BR_MDW32];  // fused pass only
+      uint16_t mdpre[BR_MDW32];
     } b;                         // phases A-B
     BinAcc acc[BM_DCAP + kWave];  // phases C-D; [BM_DCAP + lane]: dummies
   } u;
@@ -552,6 +564,56 @@ __device__ __forceinline__ int reg_prefix_arrays(const uint32_t* bits, uint16_t*
 }
 __device__ __forceinline__ int reg_prefix(BinRegSmem& L) { return reg_prefix_arrays(L.u.b.bits, L.u.b.pre, L.tmp); }
 
+// reg_prefix and the medoid's bitmap prefix (4 contiguous words per thread) in ONE
+// block scan: each count is <= the cluster's peaks (<= 50 x 252 = 12,600), so the two
+// local sums travel packed, bin-mean in the low and the medoid in the high 16 bits.
+// Returns the bin-mean's occupied bins; *md_total the medoid's (its column count K).
+__device__ __forceinline__ int reg_prefix_md(BinRegSmem& L, int* md_total) {
+  const uint4* src = reinterpret_cast<const uint4*>(L.u.b.bits) + threadIdx.x * (BR_WPT / 4);
+  uint32_t w[BR_WPT];
+#pragma unroll
+  for (int k = 0; k < BR_WPT / 4; ++k) {
+    const uint4 q = src[k];
+    w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
+  }
+  static_assert(BR_MDW32 == 4 * BM_BLOCK, "one b128 of medoid words per thread");
+  const uint4 mq = reinterpret_cast<const uint4*>(L.u.b.mdbits)[threadIdx.x];
+  const uint32_t mw[4] = {mq.x, mq.y, mq.z, mq.w};
+  int local = 0, mlocal = 0;
+#pragma unroll
+  for (int k = 0; k < BR_WPT; ++k) local += __popc(w[k]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) mlocal += __popc(mw[k]);
+  int total;
+  const int packed = block_exclusive_scan<BM_BLOCK, int, true, false>(local | (mlocal << 16), L.tmp, total);
+  int base = packed & 0xFFFF, mbase = (int)((uint32_t)packed >> 16);
+  uint2* dst = reinterpret_cast<uint2*>(L.u.b.pre) + threadIdx.x * (BR_WPT / 4);
+#pragma unroll
+  for (int k = 0; k < BR_WPT / 4; ++k) {
+    uint32_t p[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { p[i] = (uint32_t)base; base += __popc(w[4 * k + i]); }
+    dst[k] = make_uint2(p[0] | (p[1] << 16), p[2] | (p[3] << 16));
+  }
+  uint32_t mp[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { mp[i] = (uint32_t)mbase; mbase += __popc(mw[i]); }
+  reinterpret_cast<uint2*>(L.u.b.mdpre)[threadIdx.x] = make_uint2(mp[0] | (mp[1] << 16), mp[2] | (mp[3] << 16));
+  lds_barrier();
+  *md_total = (int)((uint32_t)total >> 16);
+  return total & 0xFFFF;
+}
+
+// What the fused pass's register path hands the medoid (bin_mean_reg_path_t<true>):
+// the medoid's tolerance in, and out: `out` (a peak's ceil(mz/tol) outside
+// [0, 32,768): the medoid reads the m/z itself), K (its occupied bins) and this lane's
+// spectrum [rlo, rhi) (lane j: spectrum min(j, n-1)), relative to the cluster's first peak.
+struct MdSide {
+  double tol, inv_tol;
+  int out, K;
+  int32_t rlo, rhi;
+};
+
 // f(integral_constant<int, J>) for J = 0, 1, ... while J < n (n <= sizeof...(Js)):
 // a compile-time-unrolled loop with a uniform early exit.  Register arrays are
 // indexed by the constant J, and after the exit nothing is merged back (a
@@ -575,10 +637,22 @@ __device__ __forceinline__ void reg_steps(int n, F&& f) {
   unrolled_while(n, f, std::make_integer_sequence<int, BR_NMAX>{});
 }
 
-__device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const BinMeanParams& P, BinRegSmem& L,
-                                                     int64_t c, const PeaksOut& out, double* prec_out,
-                                                     int32_t* charge_out) {
+// kMd (the fused pass, bin_mean_medoid_kernel): phase A also computes each peak's
+// medoid bin ceil(mz/tol) from the same m/z load and ORs it into the medoid's union
+// bitmap; phase B turns it into the medoid's column (its rank among the cluster's
+// occupied medoid bins).  code[j] then carries the bin-mean slot in its low and the
+// medoid column in its high 16 bits, so the medoid builds its bit rows from registers
+// (medoid_from_codes, fused.hip) and never reads the m/z again.  kMd = false is the
+// register kernel's own path, unchanged.
+template <bool kMd>
+__device__ __forceinline__ int32_t bin_mean_reg_path_t(const CsrView& v, const BinMeanParams& P, BinRegSmem& L,
+                                                       int64_t c, const PeaksOut& out, double* prec_out,
+                                                       int32_t* charge_out, int32_t (&code)[BR_NMAX], MdSide* md) {
   const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  // spectra whose m/z phase A keeps for phase C (the fused pass needs registers for
+  // its medoid bins in phase A)
+  constexpr int KM = kMd ? SPX_BR_KM_MD : BR_KM;
+  constexpr int PFA = kMd ? SPX_BR_PFA_MD : BR_PFA;  // phase-A ring depth
   const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1], n64 = s1 - s0;
   if (n64 < 1 || n64 > BR_NMAX || P.n_words > BM_WMAX) return kNotHere;
   const int n = (int)n64;
@@ -597,6 +671,11 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     return kMixedCharge;
   }
   if (wid == 0 && mine) L.prec[lane] = pl;
+  if constexpr (kMd) {
+    md->rlo = rlo;
+    md->rhi = rhi;
+    reinterpret_cast<uint4*>(L.u.b.mdbits)[tid] = make_uint4(0u, 0u, 0u, 0u);
+  }
   {
     uint4* z = reinterpret_cast<uint4*>(L.u.b.bits) + tid * (BR_WPT / 4);
 #pragma unroll
@@ -607,7 +686,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     }
   }
   lds_barrier();
-  SPX_STAMP(1);
+  SPX_STAMP2(1, -1);
 
   const int fpos = wid * (kWave - 1) + lane;  // this lane's peak in every spectrum
   const bool owner = lane < kWave - 1;
@@ -625,15 +704,14 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   };
 
   // ---- A: bins, last-in-bin, occupancy, codes (branch-free per lane)
-  int32_t code[BR_NMAX];
-  double mk[BR_KM > 0 ? BR_KM : 1];  // m/z of spectra 0..BR_KM-1, kept from phase A
+  double mk[KM > 0 ? KM : 1];  // m/z of spectra 0..BR_KM-1, kept from phase A
   uint32_t* bm32 = L.u.b.bits;
-  int bad = 0;
+  int bad = 0, mdout = 0;
   {
     // ring slot: this lane's m/z of spectrum j and the spectrum's length (read
     // once, when the load is issued)
-    double ra[BR_PFA];
-    int rl[BR_PFA];
+    double ra[PFA];
+    int rl[PFA];
     auto fetch = [&](int j, double& m, int& len) __attribute__((always_inline)) {
       const int jj = j < n ? j : n - 1;
       const int a = __builtin_amdgcn_readlane(rlo, jj), e = __builtin_amdgcn_readlane(rhi, jj);
@@ -645,7 +723,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     for (int j = 0; j < BR_NMAX; ++j) code[j] = -1;
     auto body = [&](auto jc, const double m, const int len) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      if constexpr (j < BR_KM) mk[j] = m;
+      if constexpr (j < KM) mk[j] = m;
       const bool act = fpos < len;
       const bool inr = act & (m >= P.minimum) & (m < P.maximum);
       const int32_t kb = bin_small(m, P);  // used only where inr
@@ -658,18 +736,38 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
       // a lane without a contribution ORs 0 into a word of its own (same-address
       // LDS atomics serialise; distinct words do not)
       atomicOr(&bm32[valid ? key >> 5 : lane], valid ? 1u << (key & 31) : 0u);
-      code[j] = valid ? key : -1;
+      if constexpr (kMd) {
+        // the medoid's bin of the same peak, ceil(mz / tol) exactly (md_bin): the
+        // reciprocal product where it is certain, else the division (~1 peak in 10^7)
+        const bool mact = owner & act;
+        const double q = m * md->inv_tol;
+        const double t = ceil(q);
+        const double f = t - q;
+        uint32_t mb = (uint32_t)__double2int_rz(t);
+        if (__builtin_expect(mact & !((f > kDivBand) & (f < 1.0 - kDivBand) & (mb < 32u * BR_MDW32)), 0)) {
+          const int64_t bb = ceil_div_exact(m, md->tol, md->inv_tol);
+          const bool in = bb >= 0 && bb < 32 * BR_MDW32;
+          mdout |= !in;
+          mb = in ? (uint32_t)bb : 0u;
+        }
+        // no peak here: 0 ORed into a word of the lane's own (same-address atomics serialise)
+        atomicOr(&L.u.b.mdbits[mact ? mb >> 5 : lane], mact ? 1u << (mb & 31) : 0u);
+        // bin-mean bin in the low 17 bits (0x1FFFF: no contribution), medoid bin above
+        code[j] = (valid ? key : 0x1FFFF) | (int32_t)((mact ? mb : 0u) << 17);
+      } else {
+        code[j] = valid ? key : -1;
+      }
       // opaque to the compiler: phase B must not keep each step's 64-bit valid mask
       // live instead (50 SGPR pairs: spills)
       asm volatile("" : "+v"(code[j]));
     };
 #pragma unroll
-    for (int j = 0; j < BR_PFA; ++j) fetch(j, ra[j], rl[j]);
+    for (int j = 0; j < PFA; ++j) fetch(j, ra[j], rl[j]);
     reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
-      const double m = ra[j % BR_PFA];
-      const int len = rl[j % BR_PFA];
-      fetch(j + BR_PFA, ra[j % BR_PFA], rl[j % BR_PFA]);
+      const double m = ra[j % PFA];
+      const int len = rl[j % PFA];
+      fetch(j + PFA, ra[j % PFA], rl[j % PFA]);
       body(jc, m, len);
     });
   }
@@ -679,15 +777,29 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
 #pragma unroll
   for (int j = 0; j < BR_PFC; ++j) {
     const int bo = boffb(j);
-    if (j >= BR_KM) rm[j] = bf_load(rmz, bo, 0);
+    if (j >= KM) rm[j] = bf_load(rmz, bo, 0);
     ri[j] = bf_load(rit, bo, 0);
   }
-  if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
-  SPX_STAMP(2);
+  if constexpr (kMd) {
+    // one barrier for both votes: bit 0 bin-mean's (unsorted / NaN), bit 1 the medoid's
+    const int w = (__ballot(bad) != 0ull ? 1 : 0) | (__ballot(mdout) != 0ull ? 2 : 0);
+    if (lane == 0) L.votes[wid] = w;
+    lds_barrier();
+    int r = 0;
+#pragma unroll
+    for (int k = 0; k < BM_BLOCK / kWave; ++k) r |= L.votes[k];
+    md->out = r >> 1;
+    if (r & 1) return kDeferred;  // generic kernel redoes it
+  } else {
+    if (block_any<BM_BLOCK, true>(bad, L.votes, 0)) return kDeferred;  // generic kernel redoes it
+  }
+  SPX_STAMP2(2, 1);
 
   // ---- B: slots in bin order, codes -> slots (the contribution count rides
   // phase C's read-modify-write)
-  const int D = reg_prefix(L);
+  int D;
+  if constexpr (kMd) D = reg_prefix_md(L, &md->K);
+  else D = reg_prefix(L);
   if (D > BM_DCAP) return kDeferred;
   // Every step is the same two LDS reads and a popcount -- no branch: a code
   // without contribution (-1: word 0x7FFFFFF, clamped to this lane's dummy word,
@@ -701,20 +813,34 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     for (int j0 = 0; j0 < BR_NMAX; j0 += G) {
       asm volatile("" : "+s"(nn));  // one uniform guard per group, evaluated in place
       if (j0 < nn) {
-        uint32_t wb[G], wp[G];
+        uint32_t wb[G], wp[G], mwb[G], mwp[G];
 #pragma unroll
         for (int q = 0; q < G; ++q) {
           if (j0 + q < BR_NMAX) {
-            const uint32_t w = min((uint32_t)code[j0 + q] >> 5, (uint32_t)(BR_W32 + lane));
+            const uint32_t lo = kMd ? (uint32_t)code[j0 + q] & 0x1FFFFu : (uint32_t)code[j0 + q];
+            const uint32_t w = min(lo >> 5, (uint32_t)(BR_W32 + lane));
             wb[q] = L.u.b.bits[w];
             wp[q] = L.u.b.pre[w];
+            if constexpr (kMd) {
+              const uint32_t mw = (uint32_t)code[j0 + q] >> 22;  // the medoid bin's word
+              mwb[q] = L.u.b.mdbits[mw];
+              mwp[q] = L.u.b.mdpre[mw];
+            }
           }
         }
 #pragma unroll
         for (int q = 0; q < G; ++q) {
           if (j0 + q < BR_NMAX) {
             const uint32_t b = (uint32_t)code[j0 + q];
-            code[j0 + q] = (int32_t)wp[q] + __popc(wb[q] & ((1u << (b & 31)) - 1u));
+            const int32_t slot = (int32_t)wp[q] + __popc(wb[q] & ((1u << (b & 31)) - 1u));
+            if constexpr (kMd) {
+              // the medoid column: rank of the bin among the cluster's medoid bins
+              const uint32_t mb = b >> 17;
+              const uint32_t col = mwp[q] + __popc(mwb[q] & ((1u << (mb & 31)) - 1u));
+              code[j0 + q] = slot | (int32_t)(col << 16);
+            } else {
+              code[j0 + q] = slot;
+            }
           }
         }
       }
@@ -723,19 +849,24 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
   lds_barrier();  // the bitmap is dead: the accumulators take its place
   for (int d = tid; d < D; d += BM_BLOCK) L.u.acc[d] = BinAcc{0.0f, 0.0f, 0u, 0u};
   lds_barrier();
-  SPX_STAMP(3);
+  SPX_STAMP2(3, 2);
 
   // ---- C: the ordered fold (spectrum order per slot = the reference's order)
   reg_steps(n, [&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     double m;
     const double it = ri[j % BR_PFC];
-    if constexpr (j < BR_KM) m = mk[j];
+    if constexpr (j < KM) m = mk[j];
     else m = rm[j % BR_PFC];
     const int bo = boffb(j + BR_PFC);
-    if constexpr (j + BR_PFC >= BR_KM) rm[j % BR_PFC] = bf_load(rmz, bo, 0);
+    if constexpr (j + BR_PFC >= KM) rm[j % BR_PFC] = bf_load(rmz, bo, 0);
     ri[j % BR_PFC] = bf_load(rit, bo, 0);
-    const int slot = code[j];
+    const int slot = kMd ? code[j] & 0xFFFF : code[j];
+    if constexpr (kMd && (j & 1)) {
+      // both slots used: spectra j-1 and j's medoid columns share code[j-1] (low, high
+      // half) from here on, so code[j] is dead through phase D (registers for the emit)
+      code[j - 1] = (int32_t)(((uint32_t)code[j - 1] >> 16) | ((uint32_t)code[j] & 0xFFFF0000u));
+    }
     BinAcc a = L.u.acc[slot];
     a.i = (float)((double)a.i + it);
     a.m = (float)((double)a.m + m);
@@ -743,7 +874,7 @@ __device__ __forceinline__ int32_t bin_mean_reg_path(const CsrView& v, const Bin
     L.u.acc[slot] = a;
     lds_barrier();
   });
-  SPX_STAMP(4);
+  SPX_STAMP2(4, 3);
 
   // ---- D: quorum filter and ordered output (binning.py:181-183, 209-222)
   const uint32_t quorum = P.apply_quorum ? (uint32_t)((double)n * 0.25) + 1u : 1u;
@@ -762,7 +893,8 @@ using BinHeadSmem = BinRegSmem;
 __device__ __forceinline__ int32_t bin_mean_head_path(const CsrView& v, const BinMeanParams& P, BinHeadSmem& L,
                                                       int64_t c, const PeaksOut& out, double* prec_out,
                                                       int32_t* charge_out) {
-  return bin_mean_reg_path(v, P, L, c, out, prec_out, charge_out);
+  int32_t code[BR_NMAX];
+  return bin_mean_reg_path_t<false>(v, P, L, c, out, prec_out, charge_out, code, nullptr);
 }
 
 // Register-code kernel: one workgroup per cluster.  Clusters this path does not

@@ -229,6 +229,175 @@ struct MedoidRegSmem {
   int votes[2 * (BLOCK / kWave)];
 };
 
+// P4..P6 of a small cluster whose bit rows (n rows of KW words, swizzled as P3
+// sets them) are in L.u.a.rows and whose spectrum offsets are in L.soff: the pair
+// counts, the reference's distance matrix, the pairwise-tree totals and the
+// lowest-index argmin.  Shared by medoid_small_body and the fused pass's
+// medoid_from_codes (fused.hip), so both give the same bits.
+template <int BLOCK, int UMAX, int KWMAX>
+__device__ __forceinline__ void medoid_tail(MedoidRegSmem<BLOCK, UMAX, KWMAX>& L, int n, int KW, int64_t s0,
+                                            int64_t c, int64_t* rep, double* totals_out) {
+  constexpr int PMAX = UMAX * BLOCK;
+  const int tid = threadIdx.x, lane = lane_id(), wid = wave_id();
+  // each spectrum's exact reciprocal for P4's quotients (totals is free until P5;
+  // spectra here hold at most PMAX <= 65,536 peaks, md_dist_r's checked range)
+  static_assert(PMAX <= 65536, "md_dist_r's exact range");
+  if (tid < n) {
+    const int p = L.soff[tid + 1] - L.soff[tid];
+    L.totals[tid] = p > 0 ? 1.0 / (double)p : 0.0;
+  }
+  __syncthreads();
+  SPX_STAMP2(4, -1);
+
+  auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
+  // the matrix cores for the register kernel's P4; the wide kernel (up to 95 row words,
+  // 128 VGPRs) keeps the AND + popcount pairs: there the sequential MFMA chain measured
+  // slower (600-peak spectra, medoid_shapes: 1.12 -> 1.37 ms)
+  // and only for clusters of more than SPX_MD_MFMA_NMIN spectra: below, one wave holds
+  // the one 32 x 32 tile and its epilogue while the pairs spread over the whole workgroup
+  // (stamps, configs[4]: P4 n 41-50 14.4k -> 11.7k cycles, n 11-25 5.7k -> 8.7k)
+  bool mfma_p4 = false;
+  if constexpr (BLOCK == MD_BLOCK) mfma_p4 = n > SPX_MD_MFMA_NMIN;  // uniform
+  if (mfma_p4) {
+  // P4 on the matrix cores: c_ij = |B_i ∩ B_j| = the Gram of the 0/1 rows, one
+  // 32 x 32 tile per wave -- (0,0) for n <= 32; (0,0), (0,1), (1,1) for n <= 64 --
+  // one v_mfma_f32_32x32x64_f8f6f4 per 64-bin row word (FP4 0/1 operands at unit
+  // scale: the f32 sums of <= 2^24 ones are the integer counts), then
+  // d_ij = 1 - c_ij / min(p_i, p_j) into the packed upper triangle
+  {
+    const int fr = lane & 31, fh = lane >> 5;
+    const int ntile = n > 32 ? 3 : 1;
+    const bool work = wid < ntile;  // wave-uniform
+    const int ta = wid == 2 ? 1 : 0, tb = wid == 0 ? 0 : 1;
+    md_f32x16 acc;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+    if (work) {
+      const int ra = ta * 32 + fr, rb = tb * 32 + fr;
+      const unsigned long long* pa = L.u.a.rows + (ra < n ? ra : 0) * KW;
+      const unsigned long long* pb = L.u.a.rows + (rb < n ? rb : 0) * KW;
+      const unsigned long long ma = ra < n ? ~0ull : 0ull, mb = rb < n ? ~0ull : 0ull;
+      unsigned long long wa = pa[0] & ma, wb = pb[0] & mb;  // one word ahead
+      for (int w = 0; w < KW; ++w) {
+        const int wn = w + 1 < KW ? w + 1 : w;
+        const unsigned long long na = pa[wn] & ma, nb = pb[wn] & mb;
+        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(md_frag4(wa, fh), md_frag4(wb, fh), acc, 4, 4, 0, 0,
+                                                              0, 0);
+        wa = na;
+        wb = nb;
+      }
+    }
+    __syncthreads();  // rows dead: the distance matrix takes their place
+    if (work) {
+      // C/D layout (32x32): col = lane & 31, row = (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5)
+      const int j = tb * 32 + fr;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = ta * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
+        if (i <= j && j < n) {
+          const uint32_t cnt = (uint32_t)acc[q];
+          L.u.d[row_start(i) + j - i] =
+              md_dist_r(cnt, L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
+        }
+      }
+    }
+  }
+  } else {
+    // P4: every pair i <= j of the row-major upper triangle (row i starts at
+    // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
+    // registers until the rows are dead
+    constexpr int PPT = (MD_NMAX * (MD_NMAX + 1) / 2 + BLOCK - 1) / BLOCK;  // pairs per thread (9)
+    const int NP = n * (n + 1) / 2;
+    uint32_t pc[PPT];
+    int pij[PPT];
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const int p = tid + q * BLOCK;
+      pc[q] = 0u;
+      pij[q] = -1;
+      if (p < NP) {
+        const float b2 = 2.0f * n + 1.0f;
+        int i = (int)((b2 - sqrtf(b2 * b2 - 8.0f * (float)p)) * 0.5f);
+        i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+        while (i > 0 && row_start(i) > p) --i;
+        while (i + 1 < n && row_start(i + 1) <= p) ++i;
+        const int j = i + (p - row_start(i));
+        uint32_t cnt = 0;
+        for (int w = 0; w < KW; ++w) cnt += (uint32_t)__popcll(L.u.a.rows[i * KW + w] & L.u.a.rows[j * KW + w]);
+        pc[q] = cnt;
+        pij[q] = i << 8 | j;
+      }
+    }
+    __syncthreads();  // rows dead: the distance matrix takes their place
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      if (pij[q] >= 0) {
+        const int i = pij[q] >> 8, j = pij[q] & 0xff;
+        L.u.d[row_start(i) + j - i] =
+            md_dist_r(pc[q], L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
+      }
+    }
+  }
+  __syncthreads();
+  // D(a, b) of the reference's dense matrix: the upper triangle incl. the
+  // diagonal, zeros below (most_similar_representative.py:91-93)
+
+  SPX_STAMP2(5, 6);
+  // P5: totals, one lane per spectrum (n <= 64): wave 0 sums row i, wave 1 column i, each
+  // with numpy's leaf order -- 8 strided accumulators over j < lim = n - n % 8 (in order),
+  // combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the sequential tail; n < 8 is all
+  // tail.  D's zeros (below the diagonal) are skipped: adding +0.0 to a sum of d >= 0
+  // changes nothing.  (16 lanes per spectrum and 4 rounds of 16 spectra measured slower.)
+  const bool colside = wid == 1;
+  const int i5 = lane;
+  const bool valid5 = i5 < n;
+  double sum = 0.0;
+  if (tid < 2 * kWave) {  // waves 0 and 1
+    const int i = i5;
+    const bool valid = valid5;
+    const int lim = n >= 8 ? n - n % 8 : 0;
+    auto term = [&](int j) -> double {
+      const bool use = valid && (colside ? j <= i : j >= i);
+      return use ? (colside ? L.u.d[row_start(j) + i - j] : L.u.d[row_start(i) + j - i]) : 0.0;
+    };
+    double r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = 0.0;
+    for (int j0 = 0; j0 < lim; j0 += 8) {  // uniform
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = term(j0 + k);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] += v[k];
+    }
+    sum = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int j = lim; j < n; ++j) sum += term(j);  // the sequential tail
+    sum = 0.0 + sum;
+    if (colside && valid) L.u.t.col[i] = sum;
+  }
+  lds_barrier();  // every wave
+  if (wid == 0 && valid5) {
+    const double t = (sum + L.u.t.col[i5]) / (double)n;  // (row + col) / n
+    L.totals[i5] = t;
+    if (totals_out) totals_out[s0 + i5] = t;
+    sum = t;  // wave 0 keeps lane i's total for P6
+  }
+  // P6 straight from wave 0's registers (lane i holds total i): no barrier, no LDS
+  SPX_STAMP2(6, -1);
+  if (wid == 0) {
+    double t = valid5 ? sum : __longlong_as_double(0x7ff0000000000000ll);
+    int idx = tid < n ? tid : 0x7fffffff;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      const double t2 = __shfl_xor(t, o, kWave);
+      const int i2 = __shfl_xor(idx, o, kWave);
+      if (t2 < t || (t2 == t && i2 < idx)) { t = t2; idx = i2; }
+    }
+    if (tid == 0) rep[c] = s0 + idx;
+  }
+  SPX_STAMP2(7, 7);
+}
+
 // The small-cluster body for one cluster c: BLOCK threads, <= UMAX peaks per
 // thread, <= 64 * KWMAX occupied bins.  defer() hands a cluster past those caps on.
 template <int BLOCK, int UMAX, int KWMAX, class Defer>
@@ -473,163 +642,7 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
       }
     }
   }
-  // each spectrum's exact reciprocal for P4's quotients (totals is free until P5;
-  // spectra here hold at most PMAX <= 65,536 peaks, md_dist_r's checked range)
-  static_assert(PMAX <= 65536, "md_dist_r's exact range");
-  if (tid < n) {
-    const int p = L.soff[tid + 1] - L.soff[tid];
-    L.totals[tid] = p > 0 ? 1.0 / (double)p : 0.0;
-  }
-  __syncthreads();
-  SPX_STAMP(4);
-
-  auto row_start = [&](int i) { return i * n - (i * (i - 1)) / 2; };
-  // the matrix cores for the register kernel's P4; the wide kernel (up to 95 row words,
-  // 128 VGPRs) keeps the AND + popcount pairs: there the sequential MFMA chain measured
-  // slower (600-peak spectra, medoid_shapes: 1.12 -> 1.37 ms)
-  // and only for clusters of more than SPX_MD_MFMA_NMIN spectra: below, one wave holds
-  // the one 32 x 32 tile and its epilogue while the pairs spread over the whole workgroup
-  // (stamps, configs[4]: P4 n 41-50 14.4k -> 11.7k cycles, n 11-25 5.7k -> 8.7k)
-  bool mfma_p4 = false;
-  if constexpr (BLOCK == MD_BLOCK) mfma_p4 = n > SPX_MD_MFMA_NMIN;  // uniform
-  if (mfma_p4) {
-  // P4 on the matrix cores: c_ij = |B_i ∩ B_j| = the Gram of the 0/1 rows, one
-  // 32 x 32 tile per wave -- (0,0) for n <= 32; (0,0), (0,1), (1,1) for n <= 64 --
-  // one v_mfma_f32_32x32x64_f8f6f4 per 64-bin row word (FP4 0/1 operands at unit
-  // scale: the f32 sums of <= 2^24 ones are the integer counts), then
-  // d_ij = 1 - c_ij / min(p_i, p_j) into the packed upper triangle
-  {
-    const int fr = lane & 31, fh = lane >> 5;
-    const int ntile = n > 32 ? 3 : 1;
-    const bool work = wid < ntile;  // wave-uniform
-    const int ta = wid == 2 ? 1 : 0, tb = wid == 0 ? 0 : 1;
-    md_f32x16 acc;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-    if (work) {
-      const int ra = ta * 32 + fr, rb = tb * 32 + fr;
-      const unsigned long long* pa = L.u.a.rows + (ra < n ? ra : 0) * KW;
-      const unsigned long long* pb = L.u.a.rows + (rb < n ? rb : 0) * KW;
-      const unsigned long long ma = ra < n ? ~0ull : 0ull, mb = rb < n ? ~0ull : 0ull;
-      unsigned long long wa = pa[0] & ma, wb = pb[0] & mb;  // one word ahead
-      for (int w = 0; w < KW; ++w) {
-        const int wn = w + 1 < KW ? w + 1 : w;
-        const unsigned long long na = pa[wn] & ma, nb = pb[wn] & mb;
-        acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(md_frag4(wa, fh), md_frag4(wb, fh), acc, 4, 4, 0, 0,
-                                                              0, 0);
-        wa = na;
-        wb = nb;
-      }
-    }
-    __syncthreads();  // rows dead: the distance matrix takes their place
-    if (work) {
-      // C/D layout (32x32): col = lane & 31, row = (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5)
-      const int j = tb * 32 + fr;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = ta * 32 + (q & 3) + 8 * (q >> 2) + 4 * fh;
-        if (i <= j && j < n) {
-          const uint32_t cnt = (uint32_t)acc[q];
-          L.u.d[row_start(i) + j - i] =
-              md_dist_r(cnt, L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
-        }
-      }
-    }
-  }
-  } else {
-    // P4: every pair i <= j of the row-major upper triangle (row i starts at
-    // i*n - i*(i-1)/2; recovered by a float sqrt + integer fix-up); counts in
-    // registers until the rows are dead
-    constexpr int PPT = (MD_NMAX * (MD_NMAX + 1) / 2 + BLOCK - 1) / BLOCK;  // pairs per thread (9)
-    const int NP = n * (n + 1) / 2;
-    uint32_t pc[PPT];
-    int pij[PPT];
-#pragma unroll
-    for (int q = 0; q < PPT; ++q) {
-      const int p = tid + q * BLOCK;
-      pc[q] = 0u;
-      pij[q] = -1;
-      if (p < NP) {
-        const float b2 = 2.0f * n + 1.0f;
-        int i = (int)((b2 - sqrtf(b2 * b2 - 8.0f * (float)p)) * 0.5f);
-        i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
-        while (i > 0 && row_start(i) > p) --i;
-        while (i + 1 < n && row_start(i + 1) <= p) ++i;
-        const int j = i + (p - row_start(i));
-        uint32_t cnt = 0;
-        for (int w = 0; w < KW; ++w) cnt += (uint32_t)__popcll(L.u.a.rows[i * KW + w] & L.u.a.rows[j * KW + w]);
-        pc[q] = cnt;
-        pij[q] = i << 8 | j;
-      }
-    }
-    __syncthreads();  // rows dead: the distance matrix takes their place
-#pragma unroll
-    for (int q = 0; q < PPT; ++q) {
-      if (pij[q] >= 0) {
-        const int i = pij[q] >> 8, j = pij[q] & 0xff;
-        L.u.d[row_start(i) + j - i] =
-            md_dist_r(pc[q], L.soff[i + 1] - L.soff[i], L.totals[i], L.soff[j + 1] - L.soff[j], L.totals[j]);
-      }
-    }
-  }
-  __syncthreads();
-  // D(a, b) of the reference's dense matrix: the upper triangle incl. the
-  // diagonal, zeros below (most_similar_representative.py:91-93)
-
-  SPX_STAMP(5);
-  // P5: totals, one lane per spectrum (n <= 64): wave 0 sums row i, wave 1 column i, each
-  // with numpy's leaf order -- 8 strided accumulators over j < lim = n - n % 8 (in order),
-  // combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the sequential tail; n < 8 is all
-  // tail.  D's zeros (below the diagonal) are skipped: adding +0.0 to a sum of d >= 0
-  // changes nothing.  (16 lanes per spectrum and 4 rounds of 16 spectra measured slower.)
-  const bool colside = wid == 1;
-  const int i5 = lane;
-  const bool valid5 = i5 < n;
-  double sum = 0.0;
-  if (tid < 2 * kWave) {  // waves 0 and 1
-    const int i = i5;
-    const bool valid = valid5;
-    const int lim = n >= 8 ? n - n % 8 : 0;
-    auto term = [&](int j) -> double {
-      const bool use = valid && (colside ? j <= i : j >= i);
-      return use ? (colside ? L.u.d[row_start(j) + i - j] : L.u.d[row_start(i) + j - i]) : 0.0;
-    };
-    double r[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) r[k] = 0.0;
-    for (int j0 = 0; j0 < lim; j0 += 8) {  // uniform
-      double v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = term(j0 + k);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) r[k] += v[k];
-    }
-    sum = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (int j = lim; j < n; ++j) sum += term(j);  // the sequential tail
-    sum = 0.0 + sum;
-    if (colside && valid) L.u.t.col[i] = sum;
-  }
-  lds_barrier();  // every wave
-  if (wid == 0 && valid5) {
-    const double t = (sum + L.u.t.col[i5]) / (double)n;  // (row + col) / n
-    L.totals[i5] = t;
-    if (totals_out) totals_out[s0 + i5] = t;
-    sum = t;  // wave 0 keeps lane i's total for P6
-  }
-  // P6 straight from wave 0's registers (lane i holds total i): no barrier, no LDS
-  SPX_STAMP(6);
-  if (wid == 0) {
-    double t = valid5 ? sum : __longlong_as_double(0x7ff0000000000000ll);
-    int idx = tid < n ? tid : 0x7fffffff;
-#pragma unroll
-    for (int o = kWave / 2; o > 0; o >>= 1) {
-      const double t2 = __shfl_xor(t, o, kWave);
-      const int i2 = __shfl_xor(idx, o, kWave);
-      if (t2 < t || (t2 == t && i2 < idx)) { t = t2; idx = i2; }
-    }
-    if (tid == 0) rep[c] = s0 + idx;
-  }
-  SPX_STAMP(7);
+  medoid_tail<BLOCK, UMAX, KWMAX>(L, n, KW, s0, c, rep, totals_out);
 }
 
 // Register kernel: one 256-thread workgroup per cluster.  Clusters past its caps

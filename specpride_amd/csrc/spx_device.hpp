@@ -42,6 +42,19 @@ __device__ unsigned long long* g_spx_stamps;
   do {               \
   } while (0)
 #endif
+// A stamp that the fused pass's diagnostic build (-DSPX_STAMPS -DSPX_STAMPS_FU) records at
+// index `fu` instead of `other` (-1: none), so its eight slots span both methods' phases.
+#ifdef SPX_STAMPS_FU
+#define SPX_STAMP2(other, fu) \
+  do {                        \
+    if ((fu) >= 0) SPX_STAMP((fu) < 0 ? 0 : (fu)); \
+  } while (0)
+#else
+#define SPX_STAMP2(other, fu) \
+  do {                        \
+    if ((other) >= 0) SPX_STAMP((other) < 0 ? 0 : (other)); \
+  } while (0)
+#endif
 
 // ----------------------------------------------------------------- CSR views
 struct CsrView {

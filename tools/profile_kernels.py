@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--which", default="bm,md,ga")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--stamps", action="store_true")
-    ap.add_argument("--stamps-kernel", default="bm", choices=["bm", "md", "ga"])
+    ap.add_argument("--stamps-kernel", default="bm", choices=["bm", "md", "ga", "fu"])
     ap.add_argument("--build-stamps", action="store_true")
     ap.add_argument("--shape", default=None, help="an off-shape batch of tools/run_shape.py (skewed_config3, long_spectra_600)")
     a = ap.parse_args()
@@ -128,6 +128,8 @@ def main():
         assert L.spx_debug_stamps(buf.data_ptr()) == 0
         if a.stamps_kernel == "bm":
             engine.bin_mean(b, out=bm)
+        elif a.stamps_kernel == "fu":  # a -DSPX_STAMPS_FU build: 0 start, 1-3 after A/B/C, 4 bin-mean end,
+            engine.bin_mean_medoid(b, out_bm=fbm, out_md=fmd, check=False)  # 5 rows, 6 after P4, 7 end
         elif a.stamps_kernel == "ga":
             engine.gap_average(b, out=ga)
         else:
