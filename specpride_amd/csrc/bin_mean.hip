@@ -614,23 +614,6 @@ struct MdSide {
   int32_t rlo, rhi;
 };
 
-// f(integral_constant<int, J>) for J = 0, 1, ... while J < n (n <= sizeof...(Js)):
-// a compile-time-unrolled loop with a uniform early exit.  Register arrays are
-// indexed by the constant J, and after the exit nothing is merged back (a
-// prefetch ring read inside f never becomes a phi of a fresh load and an old
-// value, which would compile to a wait for the load right after issuing it).
-template <class F, int... Js>
-__device__ __forceinline__ void unrolled_while(int n, F&& f, std::integer_sequence<int, Js...>) {
-  // each step re-reads n through an empty asm: the compiler cannot evaluate the
-  // 64 uniform guards up front (64 live SGPR pairs, which spill)
-  int nn = __builtin_amdgcn_readfirstlane(n);
-  auto more = [&](int j) __attribute__((always_inline)) {
-    asm volatile("" : "+s"(nn));
-    return j < nn;
-  };
-  (void)((more(Js) ? (f(std::integral_constant<int, Js>{}), true) : false) && ...);
-}
-
 // the register path's step loops: n <= BR_NMAX steps, uniform early exit
 template <class F>
 __device__ __forceinline__ void reg_steps(int n, F&& f) {

@@ -1125,6 +1125,17 @@ struct GapGiant {  // zeroed by the call's memset
   int32_t gany, pad2;           // step 6a: some group has >= min_fraction spectra
 };
 
+// Pass 5 of a giant with more groups than the LDS pre-sum holds: each tile's hashed
+// (group -> sums) table is written as plain records, grouped by chunk of GA_GAGG groups,
+// into the partials arena (instead of three memory-side atomics per entry), and
+// gap_giant_reduce_kernel sums each (giant, chunk)'s records in LDS.  The sums are
+// fixed-point integers, so any order gives the same totals.
+struct GapPartial {
+  uint32_t e, c;            // group, peaks
+  unsigned long long m, i;  // fixed-point m/z and intensity sums
+};
+constexpr int GA_PCH = 2 * kWave - 1;  // chunks of GA_GAGG groups a tile's records can be sorted into (more: atomics)
+
 struct GiantArgs {
   CsrView v;
   GapParams P;
@@ -1136,6 +1147,10 @@ struct GiantArgs {
   double* out_mz;     // step 6 over the flat grid: the consensus outputs
   double* out_int;
   int64_t* out_count;
+  char* part;                      // pass 5's partials arena
+  long long part_cap;              // its bytes
+  unsigned long long* part_used;   // bump pointer (zeroed by the call's memset)
+  long long* tile_off;             // per flat (giant, tile) index: its records' byte offset, -1 = atomics
 };
 
 __device__ __forceinline__ GapState<uint32_t> gap_slice_state(char* base, int wcap, int dcap) {
@@ -1461,6 +1476,18 @@ __device__ __forceinline__ GiantExtent giant_extent(const GapGiant& H, const Gap
   return X;
 }
 
+// A giant's tiles in tile pass `pass` (0: not in it); the tile passes and the pass-5
+// reduction index the (giant, tile) pairs by the same prefix of these counts.
+__device__ __forceinline__ int64_t giant_tiles(const GiantArgs& A, const GapGiant& H, int pass) {
+  if (!H.ok) return 0;
+  if (pass > 1) {
+    if (H.bad || H.status != kOk) return 0;
+    if (giant_extent(H, A.P).nw > A.wcap) return 0;  // the prefix step defers it
+  }
+  const int64_t p0 = A.v.spec_off[A.v.cluster_off[H.c]], p1 = A.v.spec_off[A.v.cluster_off[H.c + 1]];
+  return (p1 - p0 + GA_TILE - 1) / GA_TILE;
+}
+
 // The per-peak passes over every giant's tiles: PASS 1 extrema (and the slices'
 // bitmaps zeroed), 2 bucket bitmap, 3 slot m/z extent, 5 group sums and counts.
 // The (giant, tile) pairs of all giants form one index space, striped over the grid.
@@ -1482,16 +1509,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
     p1 = A.v.spec_off[A.v.cluster_off[H.c + 1]];
   };
   // a giant's tiles in this pass (0: not in it)
-  auto tiles_of = [&](const GapGiant& H) -> int64_t {
-    if (!H.ok) return 0;
-    if (PASS > 1) {
-      if (H.bad || H.status != kOk) return 0;
-      if (giant_extent(H, A.P).nw > A.wcap) return 0;  // the prefix step defers it
-    }
-    int64_t p0, p1;
-    peaks_of(H, p0, p1);
-    return (p1 - p0 + GA_TILE - 1) / GA_TILE;
-  };
+  auto tiles_of = [&](const GapGiant& H) -> int64_t { return giant_tiles(A, H, PASS); };
   if constexpr (kH3) {
     for (int h = tid; h < GA_HCAP; h += GA_BLOCK) {
       hkey[h] = 0u;
@@ -1514,6 +1532,9 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
   // passes 2 and 3 take the tiles in a scattered order (t = u * P mod T): consecutive
   // workgroups then work on different giants instead of 512 neighbouring tiles of one,
   // whose per-tile flushes all hit the same template slots of one slice at once
+  // (round 6, with passes 3 and 5 flushing plain records: the scattered order is still
+  // the fastest for every pass -- skewed configs[3] 1.865 ms; sequential pass 5 1.90,
+  // sequential 3 and 5 1.99, sequential 3 only 1.96)
   constexpr bool kPerm = PASS == 1 || PASS == 2 || PASS == 3 || PASS == 5;
   __shared__ long long tpre[kPerm ? GA_GMAX + 1 : 1];
   __shared__ long long ttmp[kPerm ? GA_NW + 1 : 1];
@@ -1535,21 +1556,80 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
     }
   }
   GapState<uint32_t> S{};
-  // the hashed table after a tile: every occupied entry to the slice, the table emptied
-  auto hflush = [&]() __attribute__((always_inline)) {
-    if constexpr (PASS == 5) {
+  __shared__ int pcnt[PASS == 5 || PASS == 3 ? 2 * kWave : 1];  // passes 3, 5: records per chunk, then cursors
+  __shared__ long long poff;
+  __shared__ int pocc;
+  // the hashed table after tile u: its occupied entries (pass 5: group sums; pass 3: slot
+  // m/z extents) as records sorted by chunk of GA_GAGG groups / slots (the partials arena;
+  // gap_giant_reduce_kernel folds them) or, when the arena is full or the giant has too
+  // many chunks, as global atomics; the table emptied
+  auto hflush = [&](int64_t u) __attribute__((always_inline)) {
+    if constexpr (PASS == 5 || PASS == 3) {
+      const int nch = (E + GA_GAGG - 1) / GA_GAGG;
+      for (int k = tid; k <= GA_PCH; k += GA_BLOCK) pcnt[k] = 0;
       lds_barrier();
+      if (nch <= GA_PCH) {
+        for (int h = tid; h < GA_HCAP; h += GA_BLOCK) {
+          const uint32_t k = hkey[h];
+          if (k) atomicAdd(&pcnt[(k - 1u) / GA_GAGG], 1);
+        }
+      }
+      lds_barrier();
+      if (tid < kWave) {  // chunk starts (exclusive prefix) for the record header and the LDS cursors
+        const int a = pcnt[2 * tid], b = pcnt[2 * tid + 1];
+        const int inc = wave_inclusive_sum(a + b);
+        const int occ = __shfl(inc, kWave - 1, kWave);  // the tile's occupied entries
+        pcnt[2 * tid] = inc - a - b;
+        pcnt[2 * tid + 1] = inc - b;
+        if (tid == 0) {
+          long long off = -1;
+          if (nch <= GA_PCH && occ > 0) {
+            const long long bytes = ((long long)(nch + 1) * 4 + 15) / 16 * 16 + (long long)occ * sizeof(GapPartial);
+            const long long at = (long long)atomicAdd(A.part_used, (unsigned long long)bytes);
+            if (at + bytes <= A.part_cap) off = at;
+          }
+          poff = off;
+          pocc = occ;
+          A.tile_off[u] = off;
+        }
+      }
+      lds_barrier();
+      const long long off = poff;
+      const int occ = pocc;
+      uint32_t* hdr = off >= 0 ? reinterpret_cast<uint32_t*>(A.part + off) : nullptr;
+      GapPartial* rec = off >= 0 ? reinterpret_cast<GapPartial*>(A.part + off + ((long long)(nch + 1) * 4 + 15) / 16 * 16)
+                                 : nullptr;
+      if (off >= 0)
+        for (int k = tid; k <= nch; k += GA_BLOCK) hdr[k] = (uint32_t)(k < nch ? pcnt[k] : occ);
+      lds_barrier();  // the header read its starts before the cursors move
       for (int h = tid; h < GA_HCAP; h += GA_BLOCK) {
         const uint32_t k = hkey[h];
         if (k) {
           const uint32_t e = k - 1u;
-          atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[e]), agg_m[h]);
-          atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[e]), agg_i[h]);
-          atomicAdd(&S.gcnt[e], agg_c[h]);
+          if constexpr (PASS == 5) {
+            if (off >= 0) {
+              const int pos = atomicAdd(&pcnt[e / GA_GAGG], 1);
+              rec[pos] = GapPartial{e, agg_c[h], agg_m[h], agg_i[h]};
+            } else {
+              atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmin[e]), agg_m[h]);
+              atomicAdd(reinterpret_cast<unsigned long long*>(&S.kmax[e]), agg_i[h]);
+              atomicAdd(&S.gcnt[e], agg_c[h]);
+            }
+            agg_m[h] = 0ull;
+            agg_i[h] = 0ull;
+            agg_c[h] = 0u;
+          } else {
+            if (off >= 0) {
+              const int pos = atomicAdd(&pcnt[e / GA_GAGG], 1);
+              rec[pos] = GapPartial{e, 0u, agg_m[h], agg_i[h]};
+            } else {
+              atomicMin(reinterpret_cast<unsigned long long*>(&S.kmin[e]), agg_m[h]);
+              atomicMax(reinterpret_cast<unsigned long long*>(&S.kmax[e]), agg_i[h]);
+            }
+            agg_m[h] = ~0ull;
+            agg_i[h] = 0ull;
+          }
           hkey[h] = 0u;
-          agg_m[h] = 0ull;
-          agg_i[h] = 0ull;
-          agg_c[h] = 0u;
         }
       }
       lds_barrier();
@@ -1601,6 +1681,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
       if constexpr (PASS > 1) {
         const GiantExtent X = giant_extent(H, A.P);
         kb = X.kb;
+        if constexpr (PASS == 3) E = H.D;  // hflush's records are per slot
         if constexpr (PASS == 5) {
           const int64_t N = p1 - p0;
           int ex_m, ex_i;
@@ -1749,24 +1830,15 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           }
         }
       }
-      if constexpr (kH3) {  // the tile's words / slot extents to the slice (only where they change it)
+      if constexpr (PASS == 3) {
+        hflush(u);  // the tile's slot extents: records for gap_giant_reduce_kernel<3>
+      } else if constexpr (kH3) {  // the tile's bitmap words to the slice
         lds_barrier();
         for (int h = tid; h < GA_HCAP; h += GA_BLOCK) {
           const uint32_t k = hkey[h];
           if (k) {
-            if constexpr (PASS == 2) {
-              const unsigned long long bits = agg_m[h];
-              atomicOr(&S.bitmap[k - 1u], bits);
-              agg_m[h] = 0ull;
-            } else {
-              unsigned long long* kmin = reinterpret_cast<unsigned long long*>(&S.kmin[k - 1u]);
-              unsigned long long* kmax = reinterpret_cast<unsigned long long*>(&S.kmax[k - 1u]);
-              const unsigned long long lo = agg_m[h], hi = agg_i[h];
-              atomicMin(kmin, lo);
-              atomicMax(kmax, hi);
-              agg_m[h] = ~0ull;
-              agg_i[h] = 0ull;
-            }
+            atomicOr(&S.bitmap[k - 1u], agg_m[h]);
+            agg_m[h] = 0ull;
             hkey[h] = 0u;
           }
         }
@@ -1820,11 +1892,115 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
         }
       });
       if constexpr (PASS == 5) {
-        if (hashed) hflush();  // uniform: the giant's mode
+        if (hashed) hflush(u);  // uniform: the giant's mode
       }
     }
   }
   flush();
+}
+
+// Passes 3b / 5b: the partial records of the tile passes (gap_giant_tiles_kernel's
+// hflush), one workgroup per (giant, chunk of GA_GAGG slots / groups): every tile's
+// records of that chunk folded in LDS -- pass 3 the slots' min / max m/z keys, pass 5 the
+// groups' fixed-point sums and counts -- then into the slice's words (the tiles that fell
+// back to global atomics folded theirs already).  Integer min / max / sums: the same
+// words as the atomics gave.
+template <int PASS>
+__global__ __launch_bounds__(GA_BLOCK) void gap_giant_reduce_kernel(GiantArgs A) {
+  static_assert(PASS == 3 || PASS == 5, "passes 3 (slot extents) and 5 (group sums)");
+  __shared__ unsigned long long sm[GA_GAGG], si[GA_GAGG];
+  __shared__ uint32_t sc[GA_GAGG];
+  __shared__ long long tpre[GA_GMAX + 1], cpre[GA_GMAX + 1];
+  __shared__ long long ttmp[GA_NW + 1];
+  __shared__ long long rs_off[GA_BLOCK];  // per tile of the current batch: its records' byte offset
+  __shared__ int rs_a[GA_BLOCK], rs_b[GA_BLOCK];  // and this chunk's record range
+  const int tid = threadIdx.x;
+  const int ng = min(*A.n_giant, A.gmax);
+  long long tc = 0, cc = 0;
+  if (PASS == 3 && blockIdx.x == 0 && tid == 0) *A.part_used = 0ull;  // the arena is pass 5's next
+  if (tid < ng) {
+    const GapGiant& H = A.giants[tid];
+    tc = giant_tiles(A, H, PASS);
+    const int NE = PASS == 5 ? H.E : H.D;
+    const long long nch = (NE + GA_GAGG - 1) / GA_GAGG;
+    // the giants whose tiles wrote records (pass 5: the hashed ones, past the LDS pre-sum)
+    cc = (tc > 0 && (PASS == 3 || NE > GA_GAGG) && nch <= GA_PCH) ? nch : 0;
+  }
+  long long tot;
+  const long long te = block_exclusive_scan<GA_BLOCK, long long>(tc, ttmp, tot);
+  if (tid < ng) tpre[tid] = te;
+  const long long ce = block_exclusive_scan<GA_BLOCK, long long>(cc, ttmp, tot);
+  if (tid < ng) cpre[tid] = ce;
+  if (tid == 0) cpre[ng] = tot;
+  __syncthreads();
+  for (long long w = blockIdx.x; w < cpre[ng]; w += gridDim.x) {  // uniform
+    int lo = 0, hi = ng;  // the giant with cpre[g] <= w < cpre[g + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (cpre[mid] <= w) lo = mid; else hi = mid;
+    }
+    while (lo + 1 < ng && cpre[lo + 1] <= w) ++lo;
+    const int g = lo;
+    const GapGiant& H = A.giants[g];
+    const int k = (int)(w - cpre[g]);
+    const int NE = PASS == 5 ? H.E : H.D;
+    const int nch = (NE + GA_GAGG - 1) / GA_GAGG;
+    const int e0 = k * GA_GAGG, ne = min(NE - e0, GA_GAGG);
+    for (int e = tid; e < ne; e += GA_BLOCK) { sm[e] = PASS == 5 ? 0ull : ~0ull; si[e] = 0ull; sc[e] = 0u; }
+    __syncthreads();
+    const long long tiles = giant_tiles(A, H, PASS);
+    const long long hbytes = ((long long)(nch + 1) * 4 + 15) / 16 * 16;
+    // GA_BLOCK tiles at a time: thread t reads tile t's offset and this chunk's record
+    // range (one dependent chain for all of them), then every wave folds whole runs
+    for (long long t0 = 0; t0 < tiles; t0 += GA_BLOCK) {  // uniform
+      const long long t = t0 + tid;
+      long long off = -1;
+      int a = 0, b = 0;
+      if (t < tiles) {
+        off = A.tile_off[tpre[g] + t];
+        if (off >= 0) {
+          const uint32_t* hdr = reinterpret_cast<const uint32_t*>(A.part + off);
+          a = (int)hdr[k];
+          b = (int)hdr[k + 1];
+        }
+      }
+      rs_off[tid] = off + hbytes;
+      rs_a[tid] = a;
+      rs_b[tid] = off >= 0 ? b : a;
+      __syncthreads();
+      const int nt = (int)min<long long>(GA_BLOCK, tiles - t0);
+      for (int q = wave_id(); q < nt; q += GA_NW) {  // wave-uniform
+        const GapPartial* rec = reinterpret_cast<const GapPartial*>(A.part + rs_off[q]);
+        for (int r = rs_a[q] + lane_id(); r < rs_b[q]; r += kWave) {
+          const GapPartial R = rec[r];
+          const int e = (int)R.e - e0;
+          if constexpr (PASS == 5) {
+            atomicAdd(&sm[e], R.m);
+            atomicAdd(&si[e], R.i);
+            atomicAdd(&sc[e], R.c);
+          } else {
+            atomicMin(&sm[e], R.m);
+            atomicMax(&si[e], R.i);
+          }
+        }
+      }
+      __syncthreads();  // the run table is refilled
+    }
+    const GapState<uint32_t> S = gap_slice_state(A.arena + H.off, A.wcap, H.dcap);
+    for (int e = tid; e < ne; e += GA_BLOCK) {
+      if constexpr (PASS == 5) {
+        if (sc[e]) {
+          S.kmin[e0 + e] += sm[e];
+          S.kmax[e0 + e] += si[e];
+          S.gcnt[e0 + e] += sc[e];
+        }
+      } else if (sm[e] != ~0ull) {
+        S.kmin[e0 + e] = min((unsigned long long)S.kmin[e0 + e], sm[e]);
+        S.kmax[e0 + e] = max((unsigned long long)S.kmax[e0 + e], si[e]);
+      }
+    }
+    __syncthreads();  // sm/si/sc are zeroed for the next chunk
+  }
 }
 
 // The per-giant steps, a workgroup per giant: STEP 0 the bitmap prefix (and the

@@ -650,13 +650,13 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
 __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
                                                               double* totals_out, StripedList wide) {
   __shared__ MedoidRegSmem<MD_BLOCK, MR_UMAX, MD_KWMAX> L;
-  medoid_small_body<MD_BLOCK, MR_UMAX, MD_KWMAX>(v, P, rep, totals_out, L, (int64_t)blockIdx.x,
-                                                [&](int64_t c, int64_t, int) {
+  auto defer = [&](int64_t c, int64_t, int) {
     // every leftover via the wide kernel, which passes n > 64 straight on (one
     // list target here keeps the kernel's register budget)
     rep[c] = -4;
     striped_push(wide, (int32_t)c);
-  });
+  };
+  medoid_small_body<MD_BLOCK, MR_UMAX, MD_KWMAX>(v, P, rep, totals_out, L, (int64_t)blockIdx.x, defer);
 }
 
 // Wide kernel: the register kernel's leftovers, grid-stride; what it cannot hold

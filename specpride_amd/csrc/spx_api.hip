@@ -195,6 +195,22 @@ int64_t gap_giant_arena(const spx_csr* csr, const spx_gap_params* params, const 
   return std::min<int64_t>(int64_t(1) << 30, per * std::max<int64_t>(giants, 1));
 }
 
+// Pass 5's partial records (gap_giant_tiles_kernel<5>, gap_giant_reduce_kernel): a
+// per-(giant, tile) offset for every tile a batch's giants can have, and an arena of at
+// most 256 MiB for the records (a tile whose records do not fit flushes by atomics).
+int64_t gap_giant_tile_slots(const spx_csr* csr, const spx_batch_info* info) {
+  if (info->max_cluster_peaks <= spx::GA_GIANT_N) return 0;
+  return csr->n_peaks / spx::GA_TILE + spx::GA_GMAX + 1;
+}
+int64_t gap_partials_cap(const spx_csr* csr, const spx_batch_info* info) {
+  if (info->max_cluster_peaks <= spx::GA_GIANT_N) return 0;
+  return std::min<int64_t>(int64_t(256) << 20, csr->n_peaks * 6 + (int64_t(1) << 20));
+}
+size_t gap_partials_bytes(const spx_csr* csr, const spx_batch_info* info) {
+  return align256(sizeof(long long) * (size_t)std::max<int64_t>(gap_giant_tile_slots(csr, info), 1)) +
+         align256((size_t)std::max<int64_t>(gap_partials_cap(csr, info), 1));
+}
+
 int64_t gap_fallback_grid(int64_t C, const spx_gap_params* params, const spx_batch_info* info) {
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   return fallback_grid_sized(C, spx::gap_slice_bytes(gap_wcap(params, info), (int)std::min<int64_t>(dcap, INT32_MAX)));
@@ -547,8 +563,9 @@ size_t spx_gap_average_workspace_size(const spx_csr* csr, const spx_gap_params* 
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   const size_t Cm = (size_t)std::max<int64_t>(C, 1);
-  return align256(sizeof(int32_t)) * 3 + align256(sizeof(unsigned long long)) +
+  return align256(sizeof(int32_t)) * 3 + align256(sizeof(unsigned long long)) * 2 +
          align256(sizeof(spx::GapGiant) * spx::GA_GMAX) + align256(spx::kListCountBytes) +
+         gap_partials_bytes(csr, info) +
          align256(sizeof(int32_t) * Cm) + (size_t)gap_giant_arena(csr, params, info) +
          align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
          (size_t)gap_fallback_grid(C, params, info) *
@@ -573,6 +590,7 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   int32_t* unresolved = w.take<int32_t>(1);
   int32_t* n_giant = w.take<int32_t>(1);
   unsigned long long* arena_used = w.take<unsigned long long>(1);
+  unsigned long long* part_used = w.take<unsigned long long>(1);  // pass 5's partials bump pointer
   spx::GapGiant* giants = w.take<spx::GapGiant>(spx::GA_GMAX);  // the global kernel's giants
   spx::StripedList wide;  // the LDS kernel's leftovers for the wide kernel
   wide.counts = w.take<int32_t>((size_t)spx::kListStripes * spx::kListLine);
@@ -582,6 +600,11 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   wide.items = w.take<int32_t>((size_t)wide.cap * spx::kListStripes);
   const int64_t arena_bytes = gap_giant_arena(csr, params, info);
   char* arena = w.take<char>((size_t)arena_bytes);
+  // pass 5's partial records and the per-(giant, tile) offsets (none when no giant is possible)
+  const int64_t ntile_off = gap_giant_tile_slots(csr, info);
+  long long* tile_off = w.take<long long>((size_t)std::max<int64_t>(ntile_off, 1));
+  const int64_t part_cap = gap_partials_cap(csr, info);
+  char* part = w.take<char>((size_t)std::max<int64_t>(part_cap, 1));
   char* scratch = w.base + w.used;
   spx::GapParams P;
   P.mz_accuracy = params->mz_accuracy;
@@ -622,18 +645,21 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   if (int rc = check_launch("gap_average_global_kernel")) return rc;
   if (arena_bytes == 0) return SPX_SUCCESS;  // no cluster of this batch can be a giant
   // the giant clusters' pipeline
-  const spx::GiantArgs A{V, P2, giants, n_giant, gmax, arena, wcap, O.mz, O.inten, O.count};
+  const spx::GiantArgs A{V, P2, giants, n_giant, gmax, arena, wcap, O.mz, O.inten, O.count,
+                         part, (long long)part_cap, part_used, tile_off};
   const dim3 tiles(spx::GA_GIANT_GRID), per(gmax), blk(spx::GA_BLOCK);
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<1>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<2>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_step_kernel<0>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
                      unresolved);
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<3>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_reduce_kernel<3>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<0>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<1>, per, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<2>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<3>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<5>, tiles, blk, 0, s, A);
+  hipLaunchKernelGGL(spx::gap_giant_reduce_kernel<5>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<4>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<5>, tiles, blk, 0, s, A);
   hipLaunchKernelGGL(spx::gap_giant_groups_kernel<6>, per, blk, 0, s, A);

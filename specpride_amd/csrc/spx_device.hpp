@@ -6,6 +6,7 @@
 // precursor means): the library is compiled with -ffp-contract=off and these
 // helpers never use fast-math intrinsics.
 #pragma once
+#include <utility>
 
 #include <hip/hip_runtime.h>
 
@@ -177,6 +178,23 @@ __device__ __forceinline__ T wave_inclusive_sum(T x) {
     }
     return x;
   }
+}
+
+// f(integral_constant<int, J>) for J = 0, 1, ... while J < n (n <= sizeof...(Js)):
+// a compile-time-unrolled loop with a uniform early exit.  Register arrays are
+// indexed by the constant J, and after the exit nothing is merged back (a
+// prefetch ring read inside f never becomes a phi of a fresh load and an old
+// value, which would compile to a wait for the load right after issuing it).
+template <class F, int... Js>
+__device__ __forceinline__ void unrolled_while(int n, F&& f, std::integer_sequence<int, Js...>) {
+  // each step re-reads n through an empty asm: the compiler cannot evaluate the
+  // 64 uniform guards up front (64 live SGPR pairs, which spill)
+  int nn = __builtin_amdgcn_readfirstlane(n);
+  auto more = [&](int j) __attribute__((always_inline)) {
+    asm volatile("" : "+s"(nn));
+    return j < nn;
+  };
+  (void)((more(Js) ? (f(std::integral_constant<int, Js>{}), true) : false) && ...);
 }
 
 // ------------------------------------------------------ striped cluster lists
