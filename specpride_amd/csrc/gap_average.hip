@@ -1122,7 +1122,11 @@ struct GapGiant {  // zeroed by the call's memset
   long long off;                                // its arena slice
   int32_t c, dcap, ok, bad, status, D, E, pad;  // pad: step 4a's "a bucket spans mz_accuracy" flag
   unsigned long long gmax_key;  // step 6a: order key of the largest kept group intensity
-  int32_t gany, pad2;           // step 6a: some group has >= min_fraction spectra
+  int32_t gany, gnan;           // step 6a: some group has >= min_fraction spectra; one of them a NaN intensity
+  // non-finite values (round 6: such a giant takes the tiled passes too; average_spectrum_clustering.py:59-98
+  // as gap_body_nf restates it): any NaN/inf m/z or intensity; the -inf, +inf and NaN m/z counts; the true
+  // groups' count M (the -inf group, the finite gaps' groups, the +inf boundary) and the -inf group's b0
+  int32_t nf, n_ninf, n_pinf, n_nan, M, b0;
 };
 
 // Pass 5 of a giant with more groups than the LDS pre-sum holds: each tile's hashed
@@ -1482,6 +1486,7 @@ __device__ __forceinline__ int64_t giant_tiles(const GiantArgs& A, const GapGian
   if (!H.ok) return 0;
   if (pass > 1) {
     if (H.bad || H.status != kOk) return 0;
+    if (H.hi_key == 0ull) return 0;  // no finite m/z (step 0 sends it to gap_body_nf)
     if (giant_extent(H, A.P).nw > A.wcap) return 0;  // the prefix step defers it
   }
   const int64_t p0 = A.v.spec_off[A.v.cluster_off[H.c]], p1 = A.v.spec_off[A.v.cluster_off[H.c + 1]];
@@ -1526,8 +1531,8 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
         bm[w] = 0ull;
     }
   }
-  int g = 0, cur = -1, E = 0, sc_m = 0, sc_i = 0;
-  bool agg = false, hashed = false;
+  int g = 0, cur = -1, E = 0, sc_m = 0, sc_i = 0, Mg = 0;
+  bool agg = false, hashed = false, nfg = false;
   int64_t gbase = 0, gtiles = ng > 0 ? tiles_of(A.giants[0]) : 0, p0 = 0, p1 = 0, kb = 0;
   // passes 2 and 3 take the tiles in a scattered order (t = u * P mod T): consecutive
   // workgroups then work on different giants instead of 512 neighbouring tiles of one,
@@ -1689,6 +1694,8 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           frexp(X.imax * (double)N, &ex_i);
           sc_m = 61 - ex_m;
           sc_i = 61 - ex_i;
+          nfg = H.nf != 0;
+          Mg = H.M;
           // few groups: this workgroup's sums and counts in LDS first, one global add
           // per group at the end (integer adds: the same totals)
           E = H.E;
@@ -1706,14 +1713,29 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
     }
     const int64_t t0 = p0 + (u - gbase) * GA_TILE, t1 = min(p1, t0 + GA_TILE);
     if constexpr (PASS == 1) {
+      // the FINITE m/z extent and max |finite intensity| (gap_body_nf's pass 1); a
+      // non-finite m/z is counted by class, and any non-finite value flags the giant
       double lo = __longlong_as_double(0x7ff0000000000000ll), hi = -lo, imax = 0.0;
-      int bad = 0;
+      int bad = 0, cn = 0, cp = 0, cq = 0;
       gap_peaks<true>(A.v, t0, t1, [&](int64_t, double m, double it) {
-        bad |= !isfinite(m) || !isfinite(it);
-        lo = fmin(lo, m);
-        hi = fmax(hi, m);
-        imax = fmax(imax, fabs(it));
+        if (isfinite(m)) {
+          lo = fmin(lo, m);
+          hi = fmax(hi, m);
+        } else {
+          cq += isnan(m);
+          cp += m == __longlong_as_double(0x7ff0000000000000ll);
+          cn += m == -__longlong_as_double(0x7ff0000000000000ll);
+        }
+        if (isfinite(it)) imax = fmax(imax, fabs(it));
+        else bad = 1;
       });
+      bad |= cn | cp | cq;
+      if (cn | cp | cq) {  // rare: per thread, straight to the giant's counters
+        GapGiant& Hc = A.giants[g];
+        if (cn) atomicAdd(&Hc.n_ninf, cn);
+        if (cp) atomicAdd(&Hc.n_pinf, cp);
+        if (cq) atomicAdd(&Hc.n_nan, cq);
+      }
       lo = wave_min_dpp(lo);
       hi = wave_max_dpp(hi);
       imax = wave_max_dpp(imax);
@@ -1726,12 +1748,12 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           imax = fmax(imax, red[2 * GA_NW + w]);
         }
         GapGiant& Hw = A.giants[g];
-        if (anybad) atomicOr(&Hw.bad, 1);
+        if (anybad) atomicOr(&Hw.nf, 1);
         if (lo <= hi) {
           atomicMax(&Hw.lo_inv, ~(unsigned long long)f64_order_key(lo));
           atomicMax(&Hw.hi_key, (unsigned long long)f64_order_key(hi));
-          atomicMax(&Hw.imax_key, (unsigned long long)f64_order_key(imax));
         }
+        atomicMax(&Hw.imax_key, (unsigned long long)f64_order_key(imax));
       }
       lds_barrier();  // red and votes are reused by the next tile
     } else if (PASS == 2 || PASS == 3) {
@@ -1745,13 +1767,15 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           const int64_t k = k0 + (int64_t)q * GA_BLOCK;
           m[q] = A.v.mz[k < t1 ? k : t0];
         }
+        // a non-finite m/z takes no bucket (its index 0 is never used)
         int64_t b[GA_BATCH];
 #pragma unroll
-        for (int q = 0; q < GA_BATCH; ++q) b[q] = floor_div_exact(m[q], A.P.bucket_w, A.P.inv_bucket_w) - kb;
+        for (int q = 0; q < GA_BATCH; ++q)
+          b[q] = isfinite(m[q]) ? floor_div_exact(m[q], A.P.bucket_w, A.P.inv_bucket_w) - kb : 0;
         if constexpr (PASS == 2 && kH3) {
 #pragma unroll
           for (int q = 0; q < GA_BATCH; ++q) {
-            if (k0 + (int64_t)q * GA_BLOCK >= t1) continue;
+            if (k0 + (int64_t)q * GA_BLOCK >= t1 || !isfinite(m[q])) continue;
             const uint32_t wi = (uint32_t)(b[q] >> 6);
             const unsigned long long bit = 1ull << (b[q] & 63);
             const uint32_t want = wi + 1u;
@@ -1786,7 +1810,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           for (int q = 0; q < GA_BATCH; ++q) slot[q] = bitmap_rank(S.bitmap, S.wprefix, b[q]);
 #pragma unroll
           for (int q = 0; q < GA_BATCH; ++q) {
-            if (k0 + (int64_t)q * GA_BLOCK >= t1) continue;
+            if (k0 + (int64_t)q * GA_BLOCK >= t1 || !isfinite(m[q])) continue;
             const unsigned long long key = f64_order_key(m[q]);
             const uint32_t want = (uint32_t)slot[q] + 1u;
             uint32_t h = ((uint32_t)slot[q] * 2654435761u) >> (32 - 11);  // log2(GA_HCAP) = 11
@@ -1846,7 +1870,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
       }
     } else {
       gap_peaks<PASS == 5>(A.v, t0, t1, [&](int64_t, double m, double it) {
-        const int64_t b = floor_div_exact(m, A.P.bucket_w, A.P.inv_bucket_w) - kb;
+        const int64_t b = isfinite(m) ? floor_div_exact(m, A.P.bucket_w, A.P.inv_bucket_w) - kb : 0;
         // bits and extrema only grow / shrink, so a stale read that says "no
         // change" is still right: the atomic is issued only when it can matter
         if constexpr (PASS == 2) {
@@ -1860,9 +1884,21 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
           if (key < *kmin) atomicMin(kmin, key);
           if (key > *kmax) atomicMax(kmax, key);
         } else {
-          const uint32_t eg = S.cnt[bitmap_rank(S.bitmap, S.wprefix, b)];
-          const unsigned long long qm = (unsigned long long)__double2ll_rn(ldexp(m, sc_m));
-          const unsigned long long qi = (unsigned long long)__double2ll_rn(ldexp(it, sc_i));
+          uint32_t eg;
+          unsigned long long qm = 0ull, qi = 0ull;
+          if (!nfg || isfinite(m)) {
+            eg = S.cnt[bitmap_rank(S.bitmap, S.wprefix, b)];
+            qm = (unsigned long long)__double2ll_rn(ldexp(m, sc_m));
+          } else {  // -inf: true group 0; +inf, NaN: the last true group (gap_body_nf)
+            eg = (uint32_t)min(m < 0.0 ? 0 : Mg, E - 1);
+          }
+          if (!nfg || isfinite(it)) qi = (unsigned long long)__double2ll_rn(ldexp(it, sc_i));
+          if (nfg) {  // the classes of the group's non-finite m/z and intensities
+            uint32_t fl = 0u;
+            if (!isfinite(m)) fl = isnan(m) ? NF_MZ_NAN : (m > 0.0 ? NF_MZ_PINF : NF_MZ_NINF);
+            if (!isfinite(it)) fl |= (isnan(it) ? NF_MZ_NAN : (it > 0.0 ? NF_MZ_PINF : NF_MZ_NINF)) << 3;
+            if (fl) atomicOr(&S.flags[eg], fl);
+          }
           if (agg) {
             atomicAdd(&agg_m[eg], qm);
             atomicAdd(&agg_i[eg], qi);
@@ -2025,6 +2061,11 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_step_kernel(GiantArgs A, P
     int32_t st = H.bad ? kNonFinite : H.status;
     if constexpr (STEP == 0) {
       if (st != kOk) continue;
+      if (H.hi_key == 0ull) {  // uniform: every m/z non-finite -- one workgroup in step 6 (gap_body_nf)
+        __syncthreads();
+        if (tid == 0) H.bad = 1;
+        continue;
+      }
       const GiantExtent X = giant_extent(H, A.P);
       int D = 0;
       if (X.nw > S.wcap) {
@@ -2106,6 +2147,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_groups_kernel(GiantArgs A)
   __shared__ int pre[GA_GMAX + 1];
   __shared__ int tmp[GA_NW + 1];
   __shared__ int votes[2 * GA_NW];
+  __shared__ uint32_t nf_prev, nf_wave[GA_NW];  // steps 6a-d of a giant with non-finite values
   const int tid = threadIdx.x;
   const double acc = A.P.mz_accuracy;
   auto key = [&](const uint64_t* a, int d) { return f64_from_order_key(a[d]); };
@@ -2148,10 +2190,16 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_groups_kernel(GiantArgs A)
           carry += __shfl(inc, kWave - 1, kWave);
         }
         if (tid == 0) {
-          const int m_gaps = carry;
+          // the true groups' boundaries: after the -inf peaks, the finite gaps, before the
+          // +inf peaks (gap_body_nf; 0 and 0 for a finite giant)
+          const int b0 = H.n_ninf > 0 ? 1 : 0, be = H.n_pinf > 0 ? 1 : 0;
+          const int M = b0 + carry + be;
+          H.M = M;
+          H.b0 = b0;
           if (H.pad) H.status = kDeferred;  // a bucket spans mz_accuracy
-          else if (m_gaps == 0) H.status = kNoGap;
-          else H.E = m_gaps >= 2 ? m_gaps : 2;
+          else if (M == 0) H.status = kNoGap;
+          else if ((M >= 2 ? M : 2) > H.dcap) H.status = kDeferred;  // the group words hold dcap
+          else H.E = M >= 2 ? M : 2;
         }
       }
     }
@@ -2172,7 +2220,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_groups_kernel(GiantArgs A)
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int e = db + q;
-          if (e < H.E) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; }
+          if (e < H.E) { S.kmin[e] = 0ull; S.kmax[e] = 0ull; S.flags[e] = 0u; }
         }
         continue;
       }
@@ -2188,32 +2236,85 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_groups_kernel(GiantArgs A)
         const double min_len = A.P.min_fraction * (double)n;
         const int E = H.E;
         auto isum = [&](int e) -> double { return ldexp((double)(int64_t)S.kmax[e], -sc_i); };
+        // a giant with non-finite values (round 6): each group's values are what the
+        // reference's cumsum differences give (nf_value, gap_body_nf's step 6), from the
+        // classes of the groups before it -- the chunks before this one and this chunk's
+        // groups before the thread's first
+        const bool nfg = H.nf != 0;  // uniform
+        uint32_t pf = 0u;
+        if (nfg) {
+          if (tid == 0) nf_prev = 0u;
+          __syncthreads();
+          uint32_t a = 0u;
+          for (int e = tid; e < k * GA_GCH && e < E; e += GA_BLOCK) a |= S.flags[e];
+          if (a) atomicOr(&nf_prev, a);
+          uint32_t own = 0u;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) own |= db + q < E ? S.flags[db + q] : 0u;
+          uint32_t x = own;  // the wave's inclusive OR scan
+#pragma unroll
+          for (int o = 1; o < kWave; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, kWave);
+            if (lane_id() >= o) x |= y;
+          }
+          uint32_t ex_or = __shfl_up(x, 1, kWave);
+          if (lane_id() == 0) ex_or = 0u;
+          if (lane_id() == kWave - 1) nf_wave[wave_id()] = x;
+          __syncthreads();
+          pf = nf_prev | ex_or;
+          for (int w = 0; w < wave_id(); ++w) pf |= nf_wave[w];
+        }
+        auto values = [&](int e, uint32_t pre, double& vm, double& vi) {
+          const double fm = ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e];
+          const double fi = isum(e) / (double)n;
+          if (!nfg) {
+            vm = fm;
+            vi = fi;
+          } else {
+            const uint32_t gf = S.flags[e];
+            vm = nf_value(pre, gf, fm);
+            vi = nf_value(pre >> 3, gf >> 3, fi);
+          }
+        };
         if constexpr (PART == 4) {  // (6a) the largest kept group intensity, any kept group
           double gm = -__longlong_as_double(0x7ff0000000000000ll);
-          int anyg = 0;
+          int anyg = 0, gn = 0;
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const int e = db + q;
             if (e < E && (double)S.gcnt[e] >= min_len) {
-              gm = fmax(gm, isum(e) / (double)n);
+              double vm, vi;
+              values(e, pf, vm, vi);
+              if (isnan(vi)) gn = 1;  // np.max propagates NaN: nothing is kept
+              else gm = fmax(gm, vi);
               anyg = 1;
             }
+            if (nfg && e < E) pf |= S.flags[e];
           }
           gm = wave_max_dpp(gm);
           const unsigned long long any_w = __ballot(anyg);
+          const unsigned long long nan_w = __ballot(gn);
           if (lane_id() == 0 && any_w) {
             atomicMax(&H.gmax_key, f64_order_key(gm));
             atomicOr(&H.gany, 1);
           }
+          if (lane_id() == 0 && nan_w) atomicOr(&H.gnan, 1);
           continue;
         }
         if (!H.gany) continue;  // uniform: kEmpty (the per-giant step reports it)
-        const double thr = f64_from_order_key(H.gmax_key) / A.P.dyn_range;
+        // a kept NaN intensity makes the threshold NaN: nothing passes `>=`
+        const double thr = H.gnan ? nan_d() : f64_from_order_key(H.gmax_key) / A.P.dyn_range;
         int keep[8], mine = 0;
+        double kvm[8], kvi[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int e = db + q;
-          keep[q] = e < E && (double)S.gcnt[e] >= min_len && isum(e) / (double)n >= thr;
+          keep[q] = 0;
+          if (e < E) {
+            values(e, pf, kvm[q], kvi[q]);
+            keep[q] = (double)S.gcnt[e] >= min_len && kvi[q] >= thr;
+            if (nfg) pf |= S.flags[e];
+          }
           mine += keep[q];
         }
         int tot;
@@ -2224,11 +2325,10 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_groups_kernel(GiantArgs A)
           int o = ch[k] + ex;
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
-            const int e = db + q;
             if (keep[q]) {
               SPX_GUARD(o < N, "giant out c=%ld o=%d N=%ld\n", (long)c, o, (long)N)
-              A.out_mz[p0 + o] = ldexp((double)(int64_t)S.kmin[e], -sc_m) / (double)S.gcnt[e];
-              A.out_int[p0 + o] = isum(e) / (double)n;
+              A.out_mz[p0 + o] = kvm[q];
+              A.out_int[p0 + o] = kvi[q];
               ++o;
             }
           }
@@ -2250,7 +2350,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_groups_kernel(GiantArgs A)
         if (block_any<GA_BLOCK, false>(split, votes, 1) && tid == 0) atomicOr(&H.pad, 1);
         if (tid == 0) ch[k] = tot;
       } else {  // (c)
-        int gg = ch[k] + ex;
+        int gg = H.b0 + ch[k] + ex;
         const int E = H.E;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {

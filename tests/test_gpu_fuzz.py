@@ -221,8 +221,10 @@ def test_precursor_picks_large_clusters(gpu):
 
 def test_gap_average_giant_pipeline(gpu):
     """Clusters past GA_GIANT_N (16,384) peaks go from the global kernel to the
-    tiled giant pipeline.  24 clusters here: 21 giants, one with a NaN intensity and
-    one with NaN / +-inf m/z (both go to gap_body_nf), giants on a coarse m/z grid
+    tiled giant pipeline.  24 clusters here: 21 giants -- with a NaN intensity, NaN / +inf
+    m/z, -inf m/z, +-inf m/z with a -inf intensity, an +inf intensity with a NaN m/z (since
+    round 6 all of them through the tiled passes, the reference's NaN arithmetic in the
+    flat emit), every m/z NaN (one workgroup, gap_body_nf) -- giants on a coarse m/z grid
     (exact ties, several peaks per bucket), a 2-spectrum giant, and small clusters
     between them.  Against the C oracle (the reference's NaN arithmetic): group
     structure exact, values within GAP_RTOL, under the default and non-default
@@ -236,6 +238,13 @@ def test_gap_average_giant_pipeline(gpu):
     mz[so[co[7]] + 3] = np.nan   # cluster 7: NaN and +inf m/z (the merged last group)
     mz[so[co[7] + 5] + 9] = np.inf
     mz[so[co[13] + 9] + 1] = -np.inf  # cluster 13: -inf m/z (group 0; every later m/z NaN)
+    mz[so[co[15] + 2] + 5] = -np.inf  # cluster 15: -inf AND +inf m/z, and a -inf intensity
+    mz[so[co[15] + 7] + 11] = np.inf
+    it[so[co[15] + 4] + 20] = -np.inf
+    it[so[co[16] + 1] + 30] = np.inf  # cluster 16: +inf intensity in a middle group, NaN m/z
+    mz[so[co[16] + 3] + 2] = np.nan
+    for s_ in range(co[17], co[18]):  # cluster 17: every m/z NaN (no finite m/z: one workgroup)
+        mz[so[s_]:so[s_ + 1]] = np.nan
     top = so[co[10]] + int(np.argmax(mz[so[co[10]]:so[co[11]]]))
     it[top] = np.inf  # cluster 10: +inf intensity in the last group
     for c in (5, 9, 12):  # coarse grid, spectra kept sorted
@@ -263,7 +272,10 @@ def test_gap_average_giant_pipeline(gpu):
     batch = engine.DeviceBatch.from_host(csr)
     for kw in (dict(), dict(mz_accuracy=0.02, dyn_range=100.0, min_fraction=0.3)):
         got = engine.gap_average(batch, **kw).to_host()
-        assert not got["status"].any()
+        # cluster 17 has no finite m/z: no diff reaches mz_accuracy, the reference's
+        # ind_list[0] raises IndexError (average_spectrum_clustering.py:69) -> SPX_NO_GAP
+        assert got["status"][17] == engine.STATUS_NO_GAP
+        assert not np.delete(got["status"], 17).any()
         assert got["out_off"][5] == got["out_off"][4]  # the NaN intensity: max NaN -> nothing kept
         o = got["out_off"]
         assert o[14] > o[13] and np.isnan(got["out_mz"][o[13]:o[14]]).all()  # after -inf: cm differences NaN
