@@ -67,6 +67,8 @@ def parse():
                     help="strong (default): ONE configs[4] batch split over the ranks by size-balanced LPT "
                          "buckets; weak: every rank its own --clusters batch")
     ap.add_argument("--tier3-clusters", type=int, default=20000, help="tier-3 MGF size in clusters (0: skip)")
+    ap.add_argument("--rank0-weight", type=float, default=None,
+                    help="strong scaling: rank 0's relative speed in the LPT plan (default rank0_weight(N))")
     return ap.parse_args()
 
 
@@ -455,6 +457,17 @@ def check_assembled(a, want, ids, total_p):
     return res
 
 
+def rank0_weight(world: int) -> float:
+    """Rank 0's relative speed in the strong-scaling LPT plan.  Besides its share, rank 0
+    rebuilds the other ranks' gathered consensus peaks from the wire format (spx_wire_unpack,
+    25 B of HBM traffic per peak) while RCCL writes them into its HBM (9 B per peak); on one
+    GPU that load, run beside rank 0's step, added 0.38 / 0.55 / 0.66 ms to a 5.6 / 2.8 /
+    1.4 ms step at N = 2 / 4 / 8 (tools/rank0_probe.py, profiles/r06_rank0_probe.txt), against
+    ~0.13-0.25 ms of packing and compaction on the other ranks: equal finishing times need
+    rank 0 at ~0.98 / ~0.88 / ~0.73 of the others' share."""
+    return max(0.5, 1.0 - 0.04 * (world - 1))
+
+
 def headline(args, rank, world, local, out, be):
     import torch
 
@@ -471,7 +484,8 @@ def headline(args, rank, world, local, out, be):
         if world > 1:
             global_co = t["cluster_off"].cpu().numpy()
             so = t["spec_off"].cpu().numpy()
-            parts, loads = shard.strong_partition(global_co, so, world, "both")
+            w0 = args.rank0_weight if args.rank0_weight is not None else rank0_weight(world)
+            parts, loads = shard.strong_partition(global_co, so, world, "both", rank0_weight=w0)
             if rank == 0:  # world-1 results of a sample of every rank's clusters, for the check
                 ids = sample_ids(parts)
                 want = be.sample_results(t, ids, global_co, so)
@@ -559,7 +573,8 @@ def headline(args, rank, world, local, out, be):
                    "clusters": total_clusters, "clusters_this_rank": batch.n_clusters,
                    "spectra_this_rank": batch.n_spectra, "peaks_this_rank": batch.n_peaks,
                    "parallelism": (f"cluster-sharded x{world}, size-balanced LPT buckets of one batch "
-                                   "(cost = peaks + n*peaks/64)" if strong and world > 1
+                                   "(cost = peaks + n*peaks/64; rank 0, which also rebuilds the gathered peaks, "
+                                   "weighted by rank0_weight)" if strong and world > 1
                                    else f"cluster-sharded x{world}"),
                    "launcher": ("bench.py --gpus N (own worker processes)" if os.environ.get("SPX_BENCH_SPAWNED")
                                 else ("external (torchrun)" if world > 1 else "single process")),
@@ -573,6 +588,7 @@ def headline(args, rank, world, local, out, be):
                                         "(csrc/wire.hip)" if gat.wire else "f64 peaks")
         out["config"]["rank0_inbound_bytes_per_step"] = gat.wire_bytes_per_step() if rank == 0 else None
     if loads is not None:
+        out["config"]["rank0_weight"] = w0
         out["config"]["rank_cost_share"] = [round(float(x / loads.sum()), 5) for x in loads]
         out["config"]["cost_max_over_min"] = round(float(loads.max() / max(loads.min(), 1.0)), 5)
         out["config"]["rank_clusters"] = [int(len(p)) for p in parts]

@@ -48,18 +48,36 @@ def cluster_costs(csr: SpectraCSR, method: str) -> np.ndarray:
     return costs_from_sizes(csr.cluster_sizes(), csr.cluster_peaks(), method)
 
 
-def plan_costs(cost, world: int) -> list:
-    """LPT greedy assignment: rank -> ascending array of cluster ids."""
+def plan_costs(cost, world: int, rank0_weight: float = 1.0) -> list:
+    """LPT greedy assignment: rank -> ascending array of cluster ids.  Each cluster, longest
+    first, goes to the rank that would finish it first.  ``rank0_weight`` < 1 makes rank 0
+    a slower machine (it finishes a load L at L / rank0_weight): bench.py's multi-GPU rank 0
+    also rebuilds the other ranks' gathered peaks, so it takes a smaller share."""
     if world < 1:
         raise ValueError("world must be >= 1")
+    if not 0.0 < rank0_weight <= 1.0:
+        raise ValueError("rank0_weight must be in (0, 1]")
     cost = np.asarray(cost, np.float64)
     order = np.argsort(-cost, kind="stable")
-    heap = [(0.0, r) for r in range(world)]
     owner = np.empty(len(cost), np.int64)
-    for c in order:
-        load, r = heapq.heappop(heap)
-        owner[c] = r
-        heapq.heappush(heap, (load + float(cost[c]), r))
+    if rank0_weight == 1.0 or world == 1:
+        heap = [(0.0, r) for r in range(world)]
+        for c in order:
+            load, r = heapq.heappop(heap)
+            owner[c] = r
+            heapq.heappush(heap, (load + float(cost[c]), r))
+    else:
+        heap = [(0.0, r) for r in range(1, world)]
+        load0 = 0.0
+        for c in order:
+            x = float(cost[c])
+            if (load0 + x) / rank0_weight <= heap[0][0] + x:
+                owner[c] = 0
+                load0 += x
+            else:
+                load, r = heapq.heappop(heap)
+                owner[c] = r
+                heapq.heappush(heap, (load + x, r))
     return [np.flatnonzero(owner == r) for r in range(world)]
 
 
@@ -353,7 +371,7 @@ class StepGatherer:
         return dict(out_off=out_off, out_mz=out_mz, out_int=out_int, count=count, rep=rep)
 
 
-def strong_partition(cluster_off, spec_off, world: int, method: str = "both"):
+def strong_partition(cluster_off, spec_off, world: int, method: str = "both", rank0_weight: float = 1.0):
     """bench.py's strong-scaling split of ONE batch (the same on every rank: each
     rank computes it from the offsets of the batch it generated identically):
     size-balanced LPT buckets (:func:`plan_costs`) over the per-cluster cost of
@@ -364,7 +382,7 @@ def strong_partition(cluster_off, spec_off, world: int, method: str = "both"):
     sizes = np.diff(co)
     peaks = so[co[1:]] - so[co[:-1]]
     cost = costs_from_sizes(sizes, peaks, method)
-    parts = plan_costs(cost, world)
+    parts = plan_costs(cost, world, rank0_weight)
     loads = np.array([float(cost[p].sum()) for p in parts])
     return parts, loads
 

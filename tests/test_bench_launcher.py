@@ -37,6 +37,7 @@ def test_bench_gpus_n_spawns_ranks(n):
     assert cfg["launcher"].startswith("bench.py --gpus N")
     assert cfg["clusters"] == 61 and sum(cfg["rank_clusters"]) == 61
     assert abs(sum(cfg["rank_cost_share"]) - 1.0) < 1e-3
+    assert cfg["rank0_weight"] == 1.0 - 0.04 * (n - 1) and cfg["rank_cost_share"][0] < cfg["rank_cost_share"][1]
     a = cfg["assembled_last_step"]
     assert a["ok"] and a["reps_resolved"] and a["sample_equal_world1"] and a["clusters"] == 61
     assert a["consensus_peaks"] == a["planned_peaks"] == cfg["gathered_peaks_per_step"]

@@ -102,6 +102,20 @@ def test_plan_is_balanced_partition():
     assert [len(p) for p in shard.plan(csr, 1)] == [csr.n_clusters]
 
 
+@pytest.mark.parametrize("w0", [1.0, 0.72, 0.5])
+def test_plan_costs_rank0_weight(w0):
+    """Rank 0 as a slower machine (bench.py's strong split: it also rebuilds the gathered
+    peaks): still a partition, rank 0's load ~w0 x the others', and finishing times
+    load/speed within one cluster's cost of each other."""
+    cost = shard.cluster_costs(make_clusters_np(800, seed=5), "both")
+    parts = shard.plan_costs(cost, 8, rank0_weight=w0)
+    np.testing.assert_array_equal(np.sort(np.concatenate(parts)), np.arange(len(cost)))
+    loads = np.array([cost[p].sum() for p in parts])
+    fin = loads / np.array([w0] + [1.0] * 7)
+    assert fin.max() - fin.min() <= cost.max() / w0
+    assert abs(loads[0] / loads[1:].mean() - w0) < 0.05
+
+
 # ------------------------------------------------ bench.py's per-step gatherer
 class _FakeConsensus:
     """A consensus result in the capacity layout (cluster c's kept peaks at its
