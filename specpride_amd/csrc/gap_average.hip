@@ -32,12 +32,18 @@
 #include "spx_device.hpp"
 
 // The stamps build leaves the gap-average kernels unstamped unless asked
-// (-DSPX_STAMPS_GA): with stamps, the LDS kernel trips an "illegal VGPR to SGPR
-// copy" in this compiler (ROCm 7.2)
+// (-DSPX_STAMPS_GA): with stamp 0, the LDS kernel trips an "illegal VGPR to SGPR
+// copy" in this compiler (ROCm 7.2), so build with -DSPX_GA_STAMP_MASK=0xFE
 #if defined(SPX_STAMPS) && !defined(SPX_STAMPS_GA)
 #define SPX_GA_STAMP(k) do { } while (0)
 #else
-#define SPX_GA_STAMP(k) SPX_STAMP(k)
+#ifndef SPX_GA_STAMP_MASK
+#define SPX_GA_STAMP_MASK 0xFF  // diagnostic builds: the stamps recorded
+#endif
+#define SPX_GA_STAMP(k)                                   \
+  do {                                                    \
+    if constexpr (((SPX_GA_STAMP_MASK) >> (k)) & 1) SPX_STAMP(k); \
+  } while (0)
 #endif
 
 namespace spx {
@@ -58,6 +64,16 @@ constexpr int GA_NW = GA_BLOCK / kWave;
 constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10,240 per cluster: n <= 51 at ~200 peaks)
 #ifndef SPX_GA_WMAXN
 #define SPX_GA_WMAXN 65536  // the wide kernel hands clusters of more peaks than this to the giant pipeline (0: none)
+#endif
+#ifndef SPX_GA_INTAKE
+#define SPX_GA_INTAKE 1  // giants registered up front, their pipeline on a second stream
+#endif
+#ifndef SPX_GA_OWN_N
+#define SPX_GA_OWN_N 65536  // the intake takes every cluster of more peaks than this (16,384: skewed configs[3]
+                            // 15 ms instead of 1.75 -- past the 256 records the global kernel takes them)
+#endif
+#ifndef SPX_GA_OWN_LO
+#define SPX_GA_OWN_LO 32768  // ... and those of more than this while its table has room (0: none)
 #endif
 #ifndef SPX_GA_WUM
 #define SPX_GA_WUM 20
@@ -1012,7 +1028,8 @@ __device__ __forceinline__ void gap_finish(const CsrView& v, const GapParams& P,
 __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v, GapParams P, PeaksOut out,
                                                                    double* prec_out, int32_t* charge_out,
                                                                    double* rt_out, int32_t* status,
-                                                                   StripedList deferred) {
+                                                                   StripedList deferred, int64_t own_n,
+                                                                   int64_t own_lo) {
   __shared__ GapSmem L;
   const int64_t c = blockIdx.x;
   SPX_GA_STAMP(0);
@@ -1024,8 +1041,13 @@ __global__ __launch_bounds__(GA_BLOCK, 4) void gap_average_lds_kernel(CsrView v,
   // here it would only be deferred after its bitmap pass (600-peak spectra from n ~ 18)
   const int32_t st = gap_body<GA_UM, true>(v, P, S, c, out, L.tmp, L.red, L.votes, &pl, L.prank);
   if (st == kDeferred || st == kNonFinite) {  // non-finite: the global kernel's gap_body_nf
+    // a cluster of more than own_n peaks belongs to the giant intake (gap_giant_intake_kernel,
+    // on the call's second stream): its status is the giant pipeline's to write; one of more
+    // than own_lo MAY be the intake's (the wide kernel checks), so its status is left alone
+    const int64_t pN = (own_n > 0 && pn >= 2) ? v.spec_off[ps0 + pn] - v.spec_off[ps0] : 0;
+    if (own_n > 0 && pN > own_n) return;  // uniform
     if (threadIdx.x == 0) {
-      status[c] = kDeferred;
+      if (!(own_lo > 0 && pN > own_lo)) status[c] = kDeferred;
       striped_push(deferred, (int32_t)c);
     }
     return;
@@ -1042,7 +1064,8 @@ __global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v
                                                                     double* prec_out, int32_t* charge_out,
                                                                     double* rt_out, int32_t* status,
                                                                     StripedList list, int32_t* deferred,
-                                                                    int32_t* n_deferred) {
+                                                                    int32_t* n_deferred, int64_t own_n,
+                                                                    const uint8_t* owned) {
   __shared__ GapSmemT<GA_WDCAP> L;
   __shared__ int32_t lbase[kListStripes + 1];
   const int32_t nl = striped_prefix(list, lbase);
@@ -1050,7 +1073,10 @@ __global__ __launch_bounds__(GA_BLOCK, 1) void gap_average_wide_kernel(CsrView v
   for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
     const int64_t c = striped_at(list, lbase, i);
     const int64_t ps0 = v.cluster_off[c], pn = v.cluster_off[c + 1] - ps0;
-    if (SPX_GA_WMAXN > 0 && pn >= 2 && v.spec_off[ps0 + pn] - v.spec_off[ps0] > (int64_t)SPX_GA_WMAXN) {  // uniform
+    const int64_t pN = pn >= 2 ? v.spec_off[ps0 + pn] - v.spec_off[ps0] : 0;
+    if (own_n > 0 && pN > own_n) continue;  // uniform: the giant intake's
+    if (owned && owned[c]) continue;        // uniform: taken by the intake's second tier
+    if (SPX_GA_WMAXN > 0 && pN > (int64_t)SPX_GA_WMAXN) {  // uniform
       // too many peaks for one CU (the hybrid path re-reads its tail every pass): to the
       // global kernel, which hands it to the giant pipeline spread over the grid
       if (threadIdx.x == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
@@ -1104,6 +1130,13 @@ __host__ __device__ inline GapSliceLayout gap_slice_layout(int wcap, int dcap) {
 constexpr int64_t GA_GIANT_N = 16384;
 constexpr int GA_GMAX = 256;                      // giant records per call
 constexpr int64_t GA_TILE = 2 * GA_BATCH * GA_BLOCK;  // peaks per tile
+// The global kernel's giants (more than 16,384 peaks, deferred by the wide kernel; with
+// the intake, the skewed law's mid-size clusters of a few hundred spectra) are few: their
+// pipeline takes smaller tiles, so its per-tile passes spread over more workgroups
+#ifndef SPX_GA_TILE_LATE
+#define SPX_GA_TILE_LATE 2048
+#endif
+constexpr int64_t GA_TILE_LATE = SPX_GA_TILE_LATE;
 #ifndef SPX_GA_GGRID
 #define SPX_GA_GGRID 512  // skewed configs[3] gap-average: 1024 4.21 ms, 512 3.77-3.79, 256 3.78-3.80, 4096 6.05
 #endif
@@ -1155,6 +1188,7 @@ struct GiantArgs {
   long long part_cap;              // its bytes
   unsigned long long* part_used;   // bump pointer (zeroed by the call's memset)
   long long* tile_off;             // per flat (giant, tile) index: its records' byte offset, -1 = atomics
+  int64_t tile;                    // peaks per tile (GA_TILE; the global kernel's few giants: GA_TILE_LATE)
 };
 
 __device__ __forceinline__ GapState<uint32_t> gap_slice_state(char* base, int wcap, int dcap) {
@@ -1490,7 +1524,7 @@ __device__ __forceinline__ int64_t giant_tiles(const GiantArgs& A, const GapGian
     if (giant_extent(H, A.P).nw > A.wcap) return 0;  // the prefix step defers it
   }
   const int64_t p0 = A.v.spec_off[A.v.cluster_off[H.c]], p1 = A.v.spec_off[A.v.cluster_off[H.c + 1]];
-  return (p1 - p0 + GA_TILE - 1) / GA_TILE;
+  return (p1 - p0 + A.tile - 1) / A.tile;
 }
 
 // The per-peak passes over every giant's tiles: PASS 1 extrema (and the slices'
@@ -1711,7 +1745,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_tiles_kernel(GiantArgs A) 
         }
       }
     }
-    const int64_t t0 = p0 + (u - gbase) * GA_TILE, t1 = min(p1, t0 + GA_TILE);
+    const int64_t t0 = p0 + (u - gbase) * A.tile, t1 = min(p1, t0 + A.tile);
     if constexpr (PASS == 1) {
       // the FINITE m/z extent and max |finite intensity| (gap_body_nf's pass 1); a
       // non-finite m/z is counted by class, and any non-finite value flags the giant
@@ -2368,6 +2402,51 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_giant_groups_kernel(GiantArgs A)
   }
 }
 
+// A giant's record and arena slice (the global kernel's hand-off and the intake's): 1 if
+// taken, 0 if the record table or the arena is full (the cluster then stays where it is).
+__device__ __forceinline__ int giant_register(int64_t c, int64_t N, GapGiant* giants, int32_t* n_giant, int gmax,
+                                              unsigned long long* arena_used, long long arena_bytes, int wcap) {
+  const int g = atomicAdd(n_giant, 1);
+  if (g >= gmax) return 0;
+  const int dg = (int)(N < (int64_t)wcap * 64 ? N : (int64_t)wcap * 64);  // D <= both
+  const long long need = (long long)gap_slice_layout(wcap, dg).total;
+  const long long off = (long long)atomicAdd(arena_used, (unsigned long long)need);
+  if (off + need > arena_bytes) return 0;
+  GapGiant& H = giants[g];
+  H.c = (int32_t)c;
+  H.dcap = dg;
+  H.off = off;
+  H.ok = 1;
+  return 1;
+}
+
+// The giant intake (round 6): clusters of at least 2 spectra registered as giants up
+// front, so their pipeline runs on the call's second stream BESIDE the LDS and wide
+// kernels instead of after them.  TIER 0 takes every cluster of more than own_n peaks --
+// what the LDS and wide kernels only pass on (one the table or the arena cannot take goes
+// on the global kernel's list, which the main stream reads after the intake).  TIER 1,
+// launched after it, takes clusters of (own_lo, own_n] peaks while the table has room --
+// the skewed law's clusters of a few hundred spectra, whose 0.01-Da buckets often outgrow
+// the wide kernel's LDS, which would then hand them on after reading them -- and marks
+// them in `owned`, which the wide kernel reads (after the intake) to leave them alone.
+template <int TIER>
+__global__ __launch_bounds__(256) void gap_giant_intake_kernel(CsrView v, int64_t own_n, int64_t own_lo,
+                                                               GapGiant* giants, int32_t* n_giant, int gmax,
+                                                               unsigned long long* arena_used, long long arena_bytes,
+                                                               int wcap, int32_t* deferred, int32_t* n_deferred,
+                                                               uint8_t* owned) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < v.n_clusters;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+    if (s1 - s0 < 2) continue;
+    const int64_t N = v.spec_off[s1] - v.spec_off[s0];
+    if (TIER == 0 ? N <= own_n : (N <= own_lo || N > own_n)) continue;
+    if (TIER == 1 && *n_giant >= gmax) continue;  // (a stale read only costs a failed registration)
+    if (giant_register(c, N, giants, n_giant, gmax, arena_used, arena_bytes, wcap)) owned[c] = 1;
+    else if (TIER == 0) deferred[atomicAdd(n_deferred, 1)] = (int32_t)c;
+  }
+}
+
 __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v, GapParams P, PeaksOut out,
                                                                       double* prec_out, int32_t* charge_out,
                                                                       double* rt_out, int32_t* status,
@@ -2391,24 +2470,7 @@ __global__ __launch_bounds__(GA_BLOCK) void gap_average_global_kernel(CsrView v,
     const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
     const int64_t N = v.spec_off[s1] - v.spec_off[s0];
     if (s1 - s0 >= 2 && N > GA_GIANT_N) {  // uniform: hand it to the giant pipeline if it fits
-      if (threadIdx.x == 0) {
-        int h = 0;
-        const int g = atomicAdd(n_giant, 1);
-        if (g < gmax) {
-          const int dg = (int)(N < (int64_t)wcap * 64 ? N : (int64_t)wcap * 64);  // D <= both
-          const long long need = (long long)gap_slice_layout(wcap, dg).total;
-          const long long off = (long long)atomicAdd(arena_used, (unsigned long long)need);
-          if (off + need <= arena_bytes) {
-            GapGiant& H = giants[g];
-            H.c = (int32_t)c;
-            H.dcap = dg;
-            H.off = off;
-            H.ok = 1;
-            h = 1;
-          }
-        }
-        handed = h;
-      }
+      if (threadIdx.x == 0) handed = giant_register(c, N, giants, n_giant, gmax, arena_used, arena_bytes, wcap);
       __syncthreads();
       const int h = handed;
       __syncthreads();

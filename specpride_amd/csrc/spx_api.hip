@@ -135,6 +135,44 @@ struct ProfScope {
   }
 };
 
+// A second stream per device, for a call's work that can run BESIDE the kernels on the
+// caller's stream (gap-average's giant pipeline next to its LDS and wide kernels).  The
+// call forks it from the caller's stream with an event and joins it back before returning,
+// so to the caller the call is one stream's worth of ordered work (hipGraph capture
+// included).  The mutex covers one call's fork ... join enqueue, so the shared events pair up.
+#ifndef SPX_SIDE_PRIO
+#define SPX_SIDE_PRIO 1
+#endif
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, mid = nullptr, join = nullptr;
+};
+std::mutex g_side_mu;
+SideStream g_side[64];
+
+// the current device's side stream (created on first use), or nullptr on a HIP error;
+// call with g_side_mu held
+SideStream* side_stream() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SideStream& S = g_side[dev];
+  if (!S.s) {
+#if SPX_SIDE_PRIO
+    // the side stream's work is the call's long pole: its workgroups go first
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithPriority(&S.s, hipStreamNonBlocking, hi) != hipSuccess) return nullptr;
+#else
+    if (hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+#endif
+    if (hipEventCreateWithFlags(&S.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.mid, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.join, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+  }
+  return &S;
+}
+
 // carving helper: takes `bytes` (256-aligned) from the workspace
 struct Carver {
   char* base;
@@ -198,16 +236,16 @@ int64_t gap_giant_arena(const spx_csr* csr, const spx_gap_params* params, const 
 // Pass 5's partial records (gap_giant_tiles_kernel<5>, gap_giant_reduce_kernel): a
 // per-(giant, tile) offset for every tile a batch's giants can have, and an arena of at
 // most 256 MiB for the records (a tile whose records do not fit flushes by atomics).
-int64_t gap_giant_tile_slots(const spx_csr* csr, const spx_batch_info* info) {
+int64_t gap_giant_tile_slots(const spx_csr* csr, const spx_batch_info* info, int64_t tile) {
   if (info->max_cluster_peaks <= spx::GA_GIANT_N) return 0;
-  return csr->n_peaks / spx::GA_TILE + spx::GA_GMAX + 1;
+  return csr->n_peaks / tile + spx::GA_GMAX + 1;
 }
 int64_t gap_partials_cap(const spx_csr* csr, const spx_batch_info* info) {
   if (info->max_cluster_peaks <= spx::GA_GIANT_N) return 0;
   return std::min<int64_t>(int64_t(256) << 20, csr->n_peaks * 6 + (int64_t(1) << 20));
 }
-size_t gap_partials_bytes(const spx_csr* csr, const spx_batch_info* info) {
-  return align256(sizeof(long long) * (size_t)std::max<int64_t>(gap_giant_tile_slots(csr, info), 1)) +
+size_t gap_partials_bytes(const spx_csr* csr, const spx_batch_info* info, int64_t tile) {
+  return align256(sizeof(long long) * (size_t)std::max<int64_t>(gap_giant_tile_slots(csr, info, tile), 1)) +
          align256((size_t)std::max<int64_t>(gap_partials_cap(csr, info), 1));
 }
 
@@ -563,9 +601,11 @@ size_t spx_gap_average_workspace_size(const spx_csr* csr, const spx_gap_params* 
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   const size_t Cm = (size_t)std::max<int64_t>(C, 1);
-  return align256(sizeof(int32_t)) * 3 + align256(sizeof(unsigned long long)) * 2 +
-         align256(sizeof(spx::GapGiant) * spx::GA_GMAX) + align256(spx::kListCountBytes) +
-         gap_partials_bytes(csr, info) +
+  // (two giant tables, counters and partial arenas: the intake's pipeline and the global kernel's)
+  return align256(sizeof(int32_t)) * 4 + align256(sizeof(unsigned long long)) * 3 +
+         align256(sizeof(spx::GapGiant) * spx::GA_GMAX) * 2 + align256(spx::kListCountBytes) +
+         gap_partials_bytes(csr, info, spx::GA_TILE) + gap_partials_bytes(csr, info, spx::GA_TILE_LATE) +
+         align256(Cm) +
          align256(sizeof(int32_t) * Cm) + (size_t)gap_giant_arena(csr, params, info) +
          align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
          (size_t)gap_fallback_grid(C, params, info) *
@@ -591,7 +631,10 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   int32_t* n_giant = w.take<int32_t>(1);
   unsigned long long* arena_used = w.take<unsigned long long>(1);
   unsigned long long* part_used = w.take<unsigned long long>(1);  // pass 5's partials bump pointer
+  int32_t* n_giant_in = w.take<int32_t>(1);                        // the same for the intake's giants
+  unsigned long long* part_used_in = w.take<unsigned long long>(1);
   spx::GapGiant* giants = w.take<spx::GapGiant>(spx::GA_GMAX);  // the global kernel's giants
+  spx::GapGiant* giants_in = w.take<spx::GapGiant>(spx::GA_GMAX);  // the intake's
   spx::StripedList wide;  // the LDS kernel's leftovers for the wide kernel
   wide.counts = w.take<int32_t>((size_t)spx::kListStripes * spx::kListLine);
   const size_t zeroed = (size_t)(w.base + w.used - reinterpret_cast<char*>(n_def));
@@ -601,10 +644,13 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   const int64_t arena_bytes = gap_giant_arena(csr, params, info);
   char* arena = w.take<char>((size_t)arena_bytes);
   // pass 5's partial records and the per-(giant, tile) offsets (none when no giant is possible)
-  const int64_t ntile_off = gap_giant_tile_slots(csr, info);
+  const int64_t ntile_off = gap_giant_tile_slots(csr, info, spx::GA_TILE_LATE);  // the global kernel's giants
   long long* tile_off = w.take<long long>((size_t)std::max<int64_t>(ntile_off, 1));
   const int64_t part_cap = gap_partials_cap(csr, info);
   char* part = w.take<char>((size_t)std::max<int64_t>(part_cap, 1));
+  uint8_t* owned = w.take<uint8_t>((size_t)C);  // the intake's second tier, per cluster
+  long long* tile_off_in = w.take<long long>((size_t)std::max<int64_t>(gap_giant_tile_slots(csr, info, spx::GA_TILE), 1));
+  char* part_in = w.take<char>((size_t)std::max<int64_t>(part_cap, 1));
   char* scratch = w.base + w.used;
   spx::GapParams P;
   P.mz_accuracy = params->mz_accuracy;
@@ -620,53 +666,99 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   const int wcap = gap_wcap(params, info);
   const int dcap = (int)std::min<int64_t>(std::max<int64_t>(1, info->max_cluster_peaks), INT32_MAX);
 
-  // the counters, the giants' records and the striped list's counters
-  if (hipMemsetAsync(n_def, 0, zeroed, s) != hipSuccess)
-    return check_launch("spx_gap_average memset");
-  ProfScope prof_lds(3, s);
-  hipLaunchKernelGGL(spx::gap_average_lds_kernel, dim3((unsigned)C), dim3(spx::GA_BLOCK), 0, s, V, P, O, pepmass_out,
-                     charge_out, rt_out, status, wide);
-  prof_lds.end();
-  if (int rc = check_launch("gap_average_lds_kernel")) return rc;
-  ProfScope prof_wide(4, s);
-  hipLaunchKernelGGL(spx::gap_average_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 256))),
-                     dim3(spx::GA_BLOCK), 0, s, V, P, O, pepmass_out, charge_out, rt_out, status, wide, def, n_def);
-  prof_wide.end();
-  if (int rc = check_launch("gap_average_wide_kernel")) return rc;
   spx::GapParams P2 = P;  // half-width buckets: no gap can hide inside one
   P2.bucket_w = params->mz_accuracy * 0.5;
   P2.inv_bucket_w = 1.0 / P2.bucket_w;
-  const int64_t ggrid = gap_fallback_grid(C, params, info);
   const int gmax = spx::GA_GMAX;
+  const dim3 tiles(spx::GA_GIANT_GRID), per(gmax), blk(spx::GA_BLOCK);
+  // the giant clusters' pipeline over one giant table, on stream `q`
+  auto giant_pipeline = [&](const spx::GiantArgs& A, hipStream_t q) {
+    hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<1>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<2>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_step_kernel<0>, per, blk, 0, q, A, O, pepmass_out, charge_out, rt_out, status,
+                       unresolved);
+    hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<3>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_reduce_kernel<3>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_groups_kernel<0>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_groups_kernel<1>, per, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_groups_kernel<2>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_groups_kernel<3>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<5>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_reduce_kernel<5>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_groups_kernel<4>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_groups_kernel<5>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_groups_kernel<6>, per, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_groups_kernel<7>, tiles, blk, 0, q, A);
+    hipLaunchKernelGGL(spx::gap_giant_step_kernel<6>, per, blk, 0, q, A, O, pepmass_out, charge_out, rt_out, status,
+                       unresolved);
+    return check_launch("gap_giant pipeline");
+  };
+
+  // the counters, the giants' records and the striped list's counters
+  if (hipMemsetAsync(n_def, 0, zeroed, s) != hipSuccess)
+    return check_launch("spx_gap_average memset");
+  // Clusters past SPX_GA_WMAXN peaks (the skewed law's giants) are known by size alone:
+  // with any in the batch, the intake registers them and their pipeline runs on the side
+  // stream while the LDS and wide kernels take the rest on the caller's (own_n tells those
+  // two to leave such clusters alone).  The global kernel waits for the intake (its list
+  // takes what the intake's table could not) and hands ITS giants (data-dependent: more
+  // than 16,384 peaks and deferred by the wide kernel) to the second table's pipeline.
+  const bool intake = SPX_GA_INTAKE && arena_bytes > 0 && info->max_cluster_peaks > (int64_t)SPX_GA_OWN_N;
+  const int64_t own_n = intake ? (int64_t)SPX_GA_OWN_N : 0;
+  const int64_t own_lo = intake ? (int64_t)SPX_GA_OWN_LO : 0;
+  static_assert(SPX_GA_OWN_N > spx::GA_GIANT_N && (SPX_GA_OWN_LO == 0 || SPX_GA_OWN_LO > spx::GA_GIANT_N),
+                "the intake takes giants only");
+  std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
+  SideStream* side = nullptr;
+  if (intake) {
+    side_lock.lock();
+    side = side_stream();
+    if (!side) return check_launch("spx_gap_average side stream");
+    if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
+      return check_launch("spx_gap_average fork");
+  }
+  // the LDS kernel first: the side stream's 17 launches would otherwise delay its start
+  ProfScope prof_lds(3, s);
+  hipLaunchKernelGGL(spx::gap_average_lds_kernel, dim3((unsigned)C), dim3(spx::GA_BLOCK), 0, s, V, P, O, pepmass_out,
+                     charge_out, rt_out, status, wide, own_n, own_lo);
+  prof_lds.end();
+  if (int rc = check_launch("gap_average_lds_kernel")) return rc;
+  if (intake) {
+    if (hipMemsetAsync(owned, 0, (size_t)C, side->s) != hipSuccess) return check_launch("spx_gap_average memset");
+    const dim3 gin((unsigned)std::min<int64_t>((C + 255) / 256, 1024));
+    hipLaunchKernelGGL(spx::gap_giant_intake_kernel<0>, gin, dim3(256), 0, side->s, V, own_n, own_lo, giants_in,
+                       n_giant_in, gmax, arena_used, (long long)arena_bytes, wcap, def, n_def, owned);
+    if (own_lo > 0)
+      hipLaunchKernelGGL(spx::gap_giant_intake_kernel<1>, gin, dim3(256), 0, side->s, V, own_n, own_lo, giants_in,
+                         n_giant_in, gmax, arena_used, (long long)arena_bytes, wcap, def, n_def, owned);
+    if (int rc = check_launch("gap_giant_intake_kernel")) return rc;
+    if (hipEventRecord(side->mid, side->s) != hipSuccess) return check_launch("spx_gap_average intake event");
+    const spx::GiantArgs Ain{V, P2, giants_in, n_giant_in, gmax, arena, wcap, O.mz, O.inten, O.count,
+                             part_in, (long long)part_cap, part_used_in, tile_off_in, spx::GA_TILE};
+    if (int rc = giant_pipeline(Ain, side->s)) return rc;
+    if (hipEventRecord(side->join, side->s) != hipSuccess) return check_launch("spx_gap_average join");
+  }
+  // the wide kernel reads `owned` and appends to the global kernel's list after the intake
+  if (intake && hipStreamWaitEvent(s, side->mid, 0) != hipSuccess) return check_launch("spx_gap_average wait");
+  ProfScope prof_wide(4, s);
+  hipLaunchKernelGGL(spx::gap_average_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 256))),
+                     dim3(spx::GA_BLOCK), 0, s, V, P, O, pepmass_out, charge_out, rt_out, status, wide, def, n_def,
+                     own_n, intake ? owned : nullptr);
+  prof_wide.end();
+  if (int rc = check_launch("gap_average_wide_kernel")) return rc;
+  const int64_t ggrid = gap_fallback_grid(C, params, info);
   const int64_t slice = spx::gap_slice_bytes(wcap, dcap);
   hipLaunchKernelGGL(spx::gap_average_global_kernel, dim3((unsigned)ggrid), dim3(spx::GA_BLOCK), 0, s, V, P2, O,
                      pepmass_out, charge_out, rt_out, status, def, n_def, scratch, slice, wcap, dcap, unresolved,
                      giants, n_giant, gmax, arena_used, (long long)arena_bytes);
   if (int rc = check_launch("gap_average_global_kernel")) return rc;
-  if (arena_bytes == 0) return SPX_SUCCESS;  // no cluster of this batch can be a giant
-  // the giant clusters' pipeline
-  const spx::GiantArgs A{V, P2, giants, n_giant, gmax, arena, wcap, O.mz, O.inten, O.count,
-                         part, (long long)part_cap, part_used, tile_off};
-  const dim3 tiles(spx::GA_GIANT_GRID), per(gmax), blk(spx::GA_BLOCK);
-  hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<1>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<2>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_step_kernel<0>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
-                     unresolved);
-  hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<3>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_reduce_kernel<3>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<0>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<1>, per, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<2>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<3>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_tiles_kernel<5>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_reduce_kernel<5>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<4>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<5>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<6>, per, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_groups_kernel<7>, tiles, blk, 0, s, A);
-  hipLaunchKernelGGL(spx::gap_giant_step_kernel<6>, per, blk, 0, s, A, O, pepmass_out, charge_out, rt_out, status,
-                     unresolved);
-  return check_launch("gap_giant pipeline");
+  if (arena_bytes > 0) {  // (arena_bytes == 0: no cluster of this batch can be a giant)
+    const spx::GiantArgs A{V, P2, giants, n_giant, gmax, arena, wcap, O.mz, O.inten, O.count,
+                           part, (long long)part_cap, part_used, tile_off, spx::GA_TILE_LATE};
+    if (int rc = giant_pipeline(A, s)) return rc;
+  }
+  if (intake && hipStreamWaitEvent(s, side->join, 0) != hipSuccess) return check_launch("spx_gap_average join");
+  return SPX_SUCCESS;
 }
 
 // ------------------------------------------------------------------- medoid

@@ -302,3 +302,24 @@ def test_gap_average_giant_overflow(gpu):
     batch = engine.DeviceBatch.from_host(csr)
     got = engine.gap_average(batch).to_host()
     assert_gap_close(got, c_oracle.gap_average(csr), 1000.0)
+
+
+def test_gap_average_giant_intake_overflow(gpu):
+    """The giant intake (round 6): clusters past SPX_GA_WMAXN (65,536) peaks are
+    registered up front and their pipeline runs on the call's second stream beside the
+    LDS and wide kernels.  260 such clusters here (230 spectra of ~300 peaks) plus small
+    ones between them: the intake's table takes 256, the other 4 go to the global kernel,
+    which hands them to its own table's pipeline on the caller's stream.  Every cluster
+    matches the C oracle, and a second call on a reused output gives the same bits."""
+    sizes = np.array([230, 230, 3] * 130)
+    csr = make_clusters_np(len(sizes), seed=97, sizes=sizes, n_template=300)
+    N = np.diff(csr.spec_off[csr.cluster_off])
+    assert (N > 65536).sum() == 260
+    batch = engine.DeviceBatch.from_host(csr)
+    res = engine.gap_average(batch)
+    got = res.to_host()
+    assert not got["status"].any()
+    assert_gap_close(got, c_oracle.gap_average(csr), 1000.0)
+    again = engine.gap_average(batch, out=res).to_host()
+    for k in ("out_off", "out_mz", "out_int", "status", "prec", "rt"):
+        np.testing.assert_array_equal(again[k], got[k])

@@ -148,8 +148,9 @@ def main():
             ok = (s[:, k1] > 0) & (s[:, k0] > 0)
             if ok.any():
                 ph[f"p{k0}->p{k1}"] = round(float(np.mean(s[ok, k1] - s[ok, k0])), 1)
-        ok = (s[:, last] > 0) & (s[:, 0] > 0)
-        ph["lifetime"] = round(float(np.mean(s[ok, last] - s[ok, 0])), 1)
+        first = present[0]  # the gap-average build records no stamp 0 (-DSPX_GA_STAMP_MASK=0xFE)
+        ok = (s[:, last] > 0) & (s[:, first] > 0)
+        ph["lifetime"] = round(float(np.mean(s[ok, last] - s[ok, first])), 1)
         bands = {}
         for lo, hi in ((2, 10), (11, 25), (26, 40), (41, 50)):
             m = ok & (sizes >= lo) & (sizes <= hi)
@@ -158,7 +159,7 @@ def main():
             if m.any():
                 bands[f"n{lo}-{hi}"] = {f"p{k0}->p{k1}": round(float(np.mean(s[m, k1] - s[m, k0])), 1)
                                         for k0, k1 in zip(present[:-1], present[1:])}
-        span = (s[ok, last].max() - s[ok, 0].min())
+        span = (s[ok, last].max() - s[ok, first].min())
         res["stamps"] = {"phases_cycles": ph, "by_size": bands, "span_cycles": span,
                          "cycles_per_cluster_per_cu": round(span * 256 / ok.sum(), 1)}
     print(json.dumps(res), flush=True)
