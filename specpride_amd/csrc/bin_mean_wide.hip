@@ -83,7 +83,7 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
     return kEmpty;
   }
   const int64_t p0 = v.spec_off[s0], p1 = v.spec_off[s1];
-  if (n64 > BM_NMAX || P.n_words > BM_WMAX || p1 - p0 >= (int64_t(1) << 28)) return kDeferred;
+  if (n64 > BM_NMAX || P.n_words > BM_WMAX || p1 - p0 >= (int64_t(1) << 28)) return kDeferred;  // bin_mean_past_wide
   const int n = (int)n64;
   const int np = (int)(p1 - p0);
   for (int j = tid; j <= n; j += BW_BLOCK) L.soff[j] = (int32_t)(v.spec_off[s0 + j] - p0);
@@ -216,6 +216,25 @@ __device__ __forceinline__ int32_t bin_mean_wide_body(const CsrView& v, const Bi
   return kOk;
 }
 
+// Whether the wide kernel hands cluster c on by its size alone (bin_mean_wide_body's first
+// test): more than BM_NMAX spectra, a bin space past BM_WMAX words, 2^28 peaks or more.
+__device__ __forceinline__ bool bin_mean_past_wide(const CsrView& v, const BinMeanParams& P, int64_t c) {
+  const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
+  if (s1 == s0) return false;
+  return s1 - s0 > BM_NMAX || P.n_words > BM_WMAX || v.spec_off[s1] - v.spec_off[s0] >= (int64_t(1) << 28);
+}
+
+// The bin-mean intake (round 6): every cluster the wide kernel would hand on by its size
+// (the skewed law's clusters of more than 128 spectra) listed up front, so that the kept-bin
+// fold of those clusters runs on the call's second stream BESIDE the register and wide
+// kernels instead of after them; the wide kernel (owned = 1) then leaves them alone.
+__global__ __launch_bounds__(256) void bin_mean_intake_kernel(CsrView v, BinMeanParams P, int32_t* list,
+                                                              int32_t* n_list) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < v.n_clusters;
+       c += (int64_t)gridDim.x * blockDim.x)
+    if (bin_mean_past_wide(v, P, c)) list[atomicAdd(n_list, 1)] = (int32_t)c;
+}
+
 // The register kernel's leftovers, grid-stride over the list.
 __global__ __launch_bounds__(BW_BLOCK, SPX_BW_MINW) void bin_mean_wide_kernel(CsrView v, BinMeanParams P,
                                                                               PeaksOut out, double* prec_out,
@@ -223,12 +242,13 @@ __global__ __launch_bounds__(BW_BLOCK, SPX_BW_MINW) void bin_mean_wide_kernel(Cs
                                                                               StripedList list,
                                                                               int32_t* deferred,
                                                                               int32_t* n_deferred, int32_t* glist,
-                                                                              int32_t* n_glist) {
+                                                                              int32_t* n_glist, int owned) {
   __shared__ BinWideSmem L;
   __shared__ int32_t lbase[kListStripes + 1];
   const int32_t nl = striped_prefix(list, lbase);
   for (int32_t i = blockIdx.x; i < nl; i += gridDim.x) {
     const int64_t c = striped_at(list, lbase, i);
+    if (owned && bin_mean_past_wide(v, P, c)) continue;  // uniform: the intake's (bin_mean_intake_kernel)
     const int32_t st = bin_mean_wide_body(v, P, L, c, out, prec_out, charge_out);
     if (threadIdx.x == 0) {
       if (st == kUnsortedW) {

@@ -348,6 +348,11 @@ int kept_fold_enabled() {
 
 struct BinMeanWs {
   int32_t *counters, *def, *glist, *split_list, *task_cl, *tile_cl;
+  // the intake's kept-bin fold (clusters past the wide kernel by size, on the side stream):
+  // its own list, records and task / tile / unit lists (empty when no cluster can be one)
+  int32_t *def_in, *q_task_cl_in, *q_tile_cl_in, *q_unit_cl_in;
+  spx::QMeta* qmeta_in;
+  int32_t q_task_cap_in, q_tile_cap_in, q_unit_cap_in;
   spx::StripedList rest;  // the register kernel's leftovers (striped appends)
   int32_t *seg_in, *q_task_cl, *q_tile_cl, *q_unit_cl;
   unsigned long long* bump;
@@ -360,11 +365,21 @@ struct BinMeanWs {
   int32_t range_cap, q_task_cap, q_tile_cap, q_unit_cap;
 };
 
+#ifndef SPX_BM_INTAKE
+#define SPX_BM_INTAKE 1  // clusters past the wide kernel by size: their kept-bin fold on the side stream
+#endif
+// A batch whose largest cluster has more than BM_NMAX spectra may hold clusters the
+// intake takes (bin_mean_past_wide's other tests -- 2^28 peaks, a bin space past BM_WMAX
+// words -- the chain after the wide kernel keeps, as before).
+bool bin_mean_intake_possible(const spx_batch_info* info) {
+  return SPX_BM_INTAKE && info->max_cluster_spectra > spx::BM_NMAX;
+}
+
 // The workspace layout (the size query and the launch use the same carving).
-BinMeanWs carve_bin_mean(Carver& w, const spx_csr* csr, const spx_bin_params* params) {
+BinMeanWs carve_bin_mean(Carver& w, const spx_csr* csr, const spx_bin_params* params, const spx_batch_info* info) {
   const size_t C = (size_t)std::max<int64_t>(csr->n_clusters, 1);
   BinMeanWs W;
-  W.counters = w.take<int32_t>(16);
+  W.counters = w.take<int32_t>(32);
   W.bump = w.take<unsigned long long>(1);
   // right after the counters and the bump pointer: one memset clears all three
   W.rest.counts = w.take<int32_t>((size_t)spx::kListStripes * spx::kListLine);
@@ -396,6 +411,16 @@ BinMeanWs carve_bin_mean(Carver& w, const spx_csr* csr, const spx_bin_params* pa
   W.tile_cl = w.take<int32_t>((size_t)W.n_tile_cap);
   W.arena_bytes = seg_arena_bytes(csr, params);
   W.arena = w.take<char>((size_t)W.arena_bytes);
+  const bool in = bin_mean_intake_possible(info);
+  const size_t Cin = in ? C : 1;
+  W.def_in = w.take<int32_t>(Cin);
+  W.qmeta_in = w.take<spx::QMeta>(Cin);
+  W.q_task_cap_in = in ? W.q_task_cap : 1;
+  W.q_task_cl_in = w.take<int32_t>((size_t)W.q_task_cap_in);
+  W.q_tile_cap_in = in ? W.q_tile_cap : 1;
+  W.q_tile_cl_in = w.take<int32_t>((size_t)W.q_tile_cap_in);
+  W.q_unit_cap_in = in ? W.q_unit_cap : 2;
+  W.q_unit_cl_in = w.take<int32_t>((size_t)W.q_unit_cap_in);
   W.scratch = w.base + w.used;
   return W;
 }
@@ -408,7 +433,7 @@ size_t spx_bin_mean_workspace_size(const spx_csr* csr, const spx_bin_params* par
   const int64_t C = csr->n_clusters;
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
   Carver w{nullptr, 0, 0};
-  carve_bin_mean(w, csr, params);
+  carve_bin_mean(w, csr, params, info);
   return w.used + (size_t)bin_mean_fallback_grid(C, params, dcap) * (size_t)spx::bin_mean_slice_bytes(bin_words(params), dcap);
 }
 
@@ -452,7 +477,7 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
   if (C == 0) return SPX_SUCCESS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   Carver w{static_cast<char*>(workspace), 0, workspace_bytes};
-  const BinMeanWs W = carve_bin_mean(w, csr, params);
+  const BinMeanWs W = carve_bin_mean(w, csr, params, info);
   // counters: [0] deferred past the wide kernel (kept-bin fold), [1] (unused), [2] planned split clusters, [3] split ranges, [4] the global
   // kernel's list, [5] segmented-fold block tasks, [6] its slot tiles, [7] the
   // split path's list (clusters the segmented fold's arena could not hold)
@@ -480,6 +505,44 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
   const int64_t dcap = std::max<int64_t>(1, info->max_cluster_peaks);
 
   const dim3 gcl((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 2048)));
+  const dim3 bsg(spx::SG_BLOCK);
+  const dim3 gqt((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.q_task_cap, 8192)));
+  // the kept-bin fold (bin_mean_q.hip) over one list of clusters, on stream q
+  auto kept_fold = [&](int32_t* list, int32_t* n_list, spx::QMeta* meta, int32_t* task_cl, int32_t task_cap,
+                       int32_t* n_tasks_q, int32_t* tile_cl, int32_t tile_cap, int32_t* n_tiles_q, int32_t* unit_cl,
+                       int32_t unit_cap, int32_t* n_units_q, hipStream_t q) {
+    hipLaunchKernelGGL(spx::bin_mean_q_setup_kernel, gcl, bsg, 0, q, V, P, O, prec_out, charge_out, status, list,
+                       n_list, meta, W.arena, W.bump, W.arena_bytes, task_cl, n_tasks_q, task_cap, tile_cl, n_tiles_q,
+                       tile_cap, kept_fold_enabled());
+    if (int rc = check_launch("bin_mean_q_setup_kernel")) return rc;
+    hipLaunchKernelGGL(spx::bin_mean_q_tally_kernel, gqt, bsg, 0, q, V, P, meta, W.arena, task_cl, n_tasks_q,
+                       task_cap);
+    if (int rc = check_launch("bin_mean_q_tally_kernel")) return rc;
+    hipLaunchKernelGGL(spx::bin_mean_q_count_kernel, dim3((unsigned)std::max(1, std::min(tile_cap, 8192))), bsg, 0,
+                       q, meta, W.arena, tile_cl, n_tiles_q, tile_cap);
+    if (int rc = check_launch("bin_mean_q_count_kernel")) return rc;
+    hipLaunchKernelGGL(spx::bin_mean_q_plan_kernel, gcl, bsg, 0, q, n_list, meta, W.arena, W.bump, W.arena_bytes,
+                       unit_cl, n_units_q, unit_cap);
+    if (int rc = check_launch("bin_mean_q_plan_kernel")) return rc;
+    hipLaunchKernelGGL(spx::bin_mean_q_place_kernel, gqt, bsg, 0, q, V, P, meta, W.arena, task_cl, n_tasks_q,
+                       task_cap);
+    if (int rc = check_launch("bin_mean_q_place_kernel")) return rc;
+    hipLaunchKernelGGL(spx::bin_mean_q_fold_kernel, dim3((unsigned)std::max(1, std::min(unit_cap, 2048))),
+                       dim3(spx::QF_BLOCK), 0, q, meta, W.arena, unit_cl, n_units_q, unit_cap);
+    if (int rc = check_launch("bin_mean_q_fold_kernel")) return rc;
+    hipLaunchKernelGGL(spx::bin_mean_q_emit_kernel, gcl, bsg, 0, q, V, O, prec_out, charge_out, status, n_list, meta,
+                       W.arena, W.seg_in, W.counters + 8, W.glist, W.counters + 4);
+    return check_launch("bin_mean_q_emit_kernel");
+  };
+  // The intake (spx_bin_mean's whole chain only, with the quorum): the clusters past the wide
+  // kernel by size go to a list of their own at once, and their kept-bin fold runs on the
+  // side stream while the register and wide kernels take the rest on `s`; the wide kernel
+  // leaves them alone, its own leftovers take a second kept-bin fold on `s`, and the chain
+  // after it (segmented fold, split path, global kernel) waits for both.
+  const bool intake = stage == kBmAll && !head && P.apply_quorum && kept_fold_enabled() &&
+                      bin_mean_intake_possible(info);
+  std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
+  SideStream* side = nullptr;
   auto global_pass = [&]() {
     hipLaunchKernelGGL(spx::bin_mean_global_kernel, dim3((unsigned)bin_mean_fallback_grid(C, params, dcap)),
                        dim3(spx::BM_BLOCK), 0, s, V, P, O, prec_out, charge_out, status, W.glist, n_glist, W.scratch,
@@ -492,6 +555,13 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
   if (stage == kBmAll || stage == kBmFront || stage == kBmHead) {
     if (hipMemsetAsync(W.counters, 0, 512 + spx::kListCountBytes, s) != hipSuccess)
       return check_launch("spx_bin_mean memset");
+    if (intake) {
+      side_lock.lock();
+      side = side_stream();
+      if (!side) return check_launch("spx_bin_mean side stream");
+      if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
+        return check_launch("spx_bin_mean fork");
+    }
     if (head) {
       if (int rc = head->launch(head->ctx, V, P, O, prec_out, charge_out, status, W.rest, s)) return rc;
     } else {
@@ -501,11 +571,21 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
       prof.end();
       if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
     }
+    if (intake) {  // (after the register kernel's launch: the side stream's 8 launches would delay it)
+      int32_t* c_in = W.counters + 16;  // [16] the intake's list, [17..20] its tasks, tiles, units (2)
+      hipLaunchKernelGGL(spx::bin_mean_intake_kernel, dim3((unsigned)std::min<int64_t>((C + 255) / 256, 1024)),
+                         dim3(256), 0, side->s, V, P, W.def_in, c_in);
+      if (int rc = check_launch("bin_mean_intake_kernel")) return rc;
+      if (int rc = kept_fold(W.def_in, c_in, W.qmeta_in, W.q_task_cl_in, W.q_task_cap_in, c_in + 1, W.q_tile_cl_in,
+                             W.q_tile_cap_in, c_in + 2, W.q_unit_cl_in, W.q_unit_cap_in, c_in + 3, side->s))
+        return rc;
+      if (hipEventRecord(side->join, side->s) != hipSuccess) return check_launch("spx_bin_mean join");
+    }
   }
   if (stage == kBmHead) return SPX_SUCCESS;  // the head's leftovers stay on W.rest for kBmTail
   if (stage != kBmChain) {
     hipLaunchKernelGGL(spx::bin_mean_wide_kernel, gcl, dim3(spx::BW_BLOCK), 0, s, V, P, O, prec_out, charge_out,
-                       status, W.rest, W.def, n_def, W.glist, n_glist);
+                       status, W.rest, W.def, n_def, W.glist, n_glist, intake ? 1 : 0);
     if (int rc = check_launch("bin_mean_wide_kernel")) return rc;
   }
   if (stage == kBmFront) return global_pass();  // clusters past the wide kernel keep status SPX_UNRESOLVED
@@ -513,31 +593,12 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
     // the global kernel's list was consumed by stage 1: the chain's own start at 0
     if (hipMemsetAsync(n_glist, 0, sizeof(int32_t), s) != hipSuccess) return check_launch("spx_bin_mean memset");
   }
-  const dim3 bsg(spx::SG_BLOCK);
   // kept-bin fold of the clusters past the wide kernel (the quorum applies)
-  const dim3 gqt((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.q_task_cap, 8192)));
-  hipLaunchKernelGGL(spx::bin_mean_q_setup_kernel, gcl, bsg, 0, s, V, P, O, prec_out, charge_out, status, W.def,
-                     n_def, W.qmeta, W.arena, W.bump, W.arena_bytes, W.q_task_cl, n_qtasks, W.q_task_cap, W.q_tile_cl,
-                     n_qtiles, W.q_tile_cap, kept_fold_enabled());
-  if (int rc = check_launch("bin_mean_q_setup_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_q_tally_kernel, gqt, bsg, 0, s, V, P, W.qmeta, W.arena, W.q_task_cl, n_qtasks,
-                     W.q_task_cap);
-  if (int rc = check_launch("bin_mean_q_tally_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_q_count_kernel, dim3((unsigned)std::max(1, std::min(W.q_tile_cap, 8192))), bsg, 0,
-                     s, W.qmeta, W.arena, W.q_tile_cl, n_qtiles, W.q_tile_cap);
-  if (int rc = check_launch("bin_mean_q_count_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_q_plan_kernel, gcl, bsg, 0, s, n_def, W.qmeta, W.arena, W.bump, W.arena_bytes,
-                     W.q_unit_cl, n_qunits, W.q_unit_cap);
-  if (int rc = check_launch("bin_mean_q_plan_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_q_place_kernel, gqt, bsg, 0, s, V, P, W.qmeta, W.arena, W.q_task_cl, n_qtasks,
-                     W.q_task_cap);
-  if (int rc = check_launch("bin_mean_q_place_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_q_fold_kernel, dim3((unsigned)std::max(1, std::min(W.q_unit_cap, 2048))),
-                     dim3(spx::QF_BLOCK), 0, s, W.qmeta, W.arena, W.q_unit_cl, n_qunits, W.q_unit_cap);
-  if (int rc = check_launch("bin_mean_q_fold_kernel")) return rc;
-  hipLaunchKernelGGL(spx::bin_mean_q_emit_kernel, gcl, bsg, 0, s, V, O, prec_out, charge_out, status, n_def, W.qmeta,
-                     W.arena, W.seg_in, n_seg_in, W.glist, n_glist);
-  if (int rc = check_launch("bin_mean_q_emit_kernel")) return rc;
+  if (int rc = kept_fold(W.def, n_def, W.qmeta, W.q_task_cl, W.q_task_cap, n_qtasks, W.q_tile_cl, W.q_tile_cap,
+                         n_qtiles, W.q_unit_cl, W.q_unit_cap, n_qunits, s))
+    return rc;
+  // the segmented fold reads what both kept-bin folds passed on
+  if (intake && hipStreamWaitEvent(s, side->join, 0) != hipSuccess) return check_launch("spx_bin_mean join");
   // segmented fold of what the kept-bin fold passes on (no quorum, no room)
   const dim3 gtask((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.n_task_cap, 8192)));
   const dim3 gtile((unsigned)std::max<int64_t>(1, std::min<int64_t>(W.n_tile_cap, 8192)));

@@ -589,7 +589,8 @@ def test_bin_mean_split_path(gpu):
 
 def test_bin_mean_kept_fold(gpu):
     """The kept-bin fold (bin_mean_q.hip) on the clusters the wide kernel defers:
-    n = 129 .. 2,500 (blocks of 64 spectra, the last one partial), 700-peak spectra
+    n = 129 .. 2,500 (blocks of 64 spectra, the last one partial; the intake's list, folded on
+    the side stream), 100 spectra of 20k distinct bins (the wide kernel's list), 700-peak spectra
     (blocks of < 64 spectra), more than Q_KCAP = 2,048 kept bins (-> the segmented
     fold), a NaN intensity in a kept bin (that bin dropped), every spectrum empty,
     nothing in range, peaks on the window's ends, a mixed-charge one, an unsorted
@@ -598,6 +599,9 @@ def test_bin_mean_kept_fold(gpu):
     rng = np.random.default_rng(17)
     parts = [make_clusters_np(1, seed=60 + k, sizes=np.array([n])) for k, n in enumerate((129, 192, 257, 700, 2500))]
     parts.append(make_clusters_np(2, seed=70, sizes=np.array([140, 200]), n_template=700))
+    # 100 spectra of ~2,000 peaks: 20,636 distinct bins, past the wide kernel's 4,096 -- a kept-bin fold
+    # of the wide kernel's own leftovers, beside the intake's (clusters past 128 spectra) since round 6
+    parts.append(make_clusters_np(1, seed=75, sizes=np.array([100]), n_template=2000))
 
     def spec(mz, it=None):
         mz = np.asarray(mz, np.float64)
