@@ -96,15 +96,39 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_setup_kernel(
     const int64_t s0 = v.cluster_off[c], s1 = v.cluster_off[c + 1];
     const int n = (int)(s1 - s0);
     const int32_t z0 = v.charge[s0];
-    int mixed = 0;
-    for (int64_t r0 = s0 + 1 + tid; r0 < s1; r0 += 8 * SG_BLOCK) {
-      int32_t z[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) z[u] = v.charge[min(r0 + u * SG_BLOCK, s1 - 1)];  // (clamped: a repeat)
-#pragma unroll
-      for (int u = 0; u < 8; ++u) mixed |= z[u] != z0;
-    }
+    // the charges, the longest spectrum and the bin window (first / last peak of each
+    // spectrum) in ONE pass, QS_U spectra per thread per round with their loads issued
+    // together: a 5,000-spectrum cluster is 3 rounds of two dependent loads (the charges
+    // used to take a pass of their own before it, and the window pass 4 spectra a round)
+    constexpr int QS_U = 8;
+    int mixed = 0, maxlen = 0, lok = 0x7fffffff, hik = -1;
     if (tid == 0) { red[0] = 0; red[1] = 0x7fffffff; red[2] = -1; }
+    for (int64_t r0 = s0 + tid; r0 < s1; r0 += QS_U * SG_BLOCK) {
+      int64_t a[QS_U], e[QS_U];
+      int32_t z[QS_U];
+#pragma unroll
+      for (int u = 0; u < QS_U; ++u) {
+        const int64_t sp = min(r0 + u * SG_BLOCK, s1 - 1);  // (clamped: a repeat)
+        a[u] = v.spec_off[sp];
+        e[u] = v.spec_off[sp + 1];
+        z[u] = v.charge[sp];
+      }
+      double mf[QS_U], ml[QS_U];
+#pragma unroll
+      for (int u = 0; u < QS_U; ++u) {
+        mf[u] = e[u] > a[u] ? v.mz[a[u]] : 0.0;
+        ml[u] = e[u] > a[u] ? v.mz[e[u] - 1] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < QS_U; ++u) {
+        mixed |= z[u] != z0;
+        if (r0 + u * SG_BLOCK < s1 && e[u] > a[u]) {
+          maxlen = max(maxlen, (int)min<int64_t>(e[u] - a[u], 0x7fffffff));
+          lok = min(lok, q_window_key(mf[u], P));
+          hik = max(hik, q_window_key(ml[u], P));
+        }
+      }
+    }
     const bool mix = block_any<SG_BLOCK, false>(mixed, votes, 0);
     QMeta M = {};
     M.c = c;
@@ -121,33 +145,6 @@ __global__ __launch_bounds__(SG_BLOCK) void bin_mean_q_setup_kernel(
       }
       __syncthreads();
       continue;
-    }
-    // longest spectrum and the bin window (first / last peak of each spectrum),
-    // QS_U spectra per thread per round with their loads issued together
-    constexpr int QS_U = 4;
-    int maxlen = 0, lok = 0x7fffffff, hik = -1;
-    for (int64_t r0 = s0 + tid; r0 < s1; r0 += QS_U * SG_BLOCK) {
-      int64_t a[QS_U], e[QS_U];
-#pragma unroll
-      for (int u = 0; u < QS_U; ++u) {
-        const int64_t sp = min(r0 + u * SG_BLOCK, s1 - 1);
-        a[u] = v.spec_off[sp];
-        e[u] = v.spec_off[sp + 1];
-      }
-      double mf[QS_U], ml[QS_U];
-#pragma unroll
-      for (int u = 0; u < QS_U; ++u) {
-        mf[u] = e[u] > a[u] ? v.mz[a[u]] : 0.0;
-        ml[u] = e[u] > a[u] ? v.mz[e[u] - 1] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < QS_U; ++u) {
-        if (r0 + u * SG_BLOCK < s1 && e[u] > a[u]) {
-          maxlen = max(maxlen, (int)min<int64_t>(e[u] - a[u], 0x7fffffff));
-          lok = min(lok, q_window_key(mf[u], P));
-          hik = max(hik, q_window_key(ml[u], P));
-        }
-      }
     }
     atomicMax(&red[0], maxlen);
     atomicMin(&red[1], lok);

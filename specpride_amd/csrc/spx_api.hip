@@ -368,6 +368,9 @@ struct BinMeanWs {
 #ifndef SPX_BM_INTAKE
 #define SPX_BM_INTAKE 1  // clusters past the wide kernel by size: their kept-bin fold on the side stream
 #endif
+#ifndef SPX_BM_SETUP_FIRST
+#define SPX_BM_SETUP_FIRST 1
+#endif
 // A batch whose largest cluster has more than BM_NMAX spectra may hold clusters the
 // intake takes (bin_mean_past_wide's other tests -- 2^28 peaks, a bin space past BM_WMAX
 // words -- the chain after the wide kernel keeps, as before).
@@ -510,11 +513,14 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
   // the kept-bin fold (bin_mean_q.hip) over one list of clusters, on stream q
   auto kept_fold = [&](int32_t* list, int32_t* n_list, spx::QMeta* meta, int32_t* task_cl, int32_t task_cap,
                        int32_t* n_tasks_q, int32_t* tile_cl, int32_t tile_cap, int32_t* n_tiles_q, int32_t* unit_cl,
-                       int32_t unit_cap, int32_t* n_units_q, hipStream_t q) {
-    hipLaunchKernelGGL(spx::bin_mean_q_setup_kernel, gcl, bsg, 0, q, V, P, O, prec_out, charge_out, status, list,
-                       n_list, meta, W.arena, W.bump, W.arena_bytes, task_cl, n_tasks_q, task_cap, tile_cl, n_tiles_q,
-                       tile_cap, kept_fold_enabled());
-    if (int rc = check_launch("bin_mean_q_setup_kernel")) return rc;
+                       int32_t unit_cap, int32_t* n_units_q, hipStream_t q, int part) {  // part 1: setup only, 2: the rest
+    if (part != 2) {
+      hipLaunchKernelGGL(spx::bin_mean_q_setup_kernel, gcl, bsg, 0, q, V, P, O, prec_out, charge_out, status, list,
+                         n_list, meta, W.arena, W.bump, W.arena_bytes, task_cl, n_tasks_q, task_cap, tile_cl,
+                         n_tiles_q, tile_cap, kept_fold_enabled());
+      if (int rc = check_launch("bin_mean_q_setup_kernel")) return rc;
+      if (part == 1) return (int)SPX_SUCCESS;
+    }
     hipLaunchKernelGGL(spx::bin_mean_q_tally_kernel, gqt, bsg, 0, q, V, P, meta, W.arena, task_cl, n_tasks_q,
                        task_cap);
     if (int rc = check_launch("bin_mean_q_tally_kernel")) return rc;
@@ -562,6 +568,23 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
       if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
         return check_launch("spx_bin_mean fork");
     }
+    int32_t* c_in = W.counters + 16;  // [16] the intake's list, [17..20] its tasks, tiles, units (2)
+    auto intake_fold = [&](int part) {
+      return kept_fold(W.def_in, c_in, W.qmeta_in, W.q_task_cl_in, W.q_task_cap_in, c_in + 1, W.q_tile_cl_in,
+                       W.q_tile_cap_in, c_in + 2, W.q_unit_cl_in, W.q_unit_cap_in, c_in + 3, side->s, part);
+    };
+    if (intake) {
+      hipLaunchKernelGGL(spx::bin_mean_intake_kernel, dim3((unsigned)std::min<int64_t>((C + 255) / 256, 1024)),
+                         dim3(256), 0, side->s, V, P, W.def_in, c_in);
+      if (int rc = check_launch("bin_mean_intake_kernel")) return rc;
+#if SPX_BM_SETUP_FIRST
+      // the kept-bin fold's set-up (a few long latency chains: the big clusters' offsets,
+      // charges and window) alone on the GPU, before the register kernel fills it
+      if (int rc = intake_fold(1)) return rc;
+      if (hipEventRecord(side->mid, side->s) != hipSuccess || hipStreamWaitEvent(s, side->mid, 0) != hipSuccess)
+        return check_launch("spx_bin_mean set-up event");
+#endif
+    }
     if (head) {
       if (int rc = head->launch(head->ctx, V, P, O, prec_out, charge_out, status, W.rest, s)) return rc;
     } else {
@@ -571,14 +594,8 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
       prof.end();
       if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
     }
-    if (intake) {  // (after the register kernel's launch: the side stream's 8 launches would delay it)
-      int32_t* c_in = W.counters + 16;  // [16] the intake's list, [17..20] its tasks, tiles, units (2)
-      hipLaunchKernelGGL(spx::bin_mean_intake_kernel, dim3((unsigned)std::min<int64_t>((C + 255) / 256, 1024)),
-                         dim3(256), 0, side->s, V, P, W.def_in, c_in);
-      if (int rc = check_launch("bin_mean_intake_kernel")) return rc;
-      if (int rc = kept_fold(W.def_in, c_in, W.qmeta_in, W.q_task_cl_in, W.q_task_cap_in, c_in + 1, W.q_tile_cl_in,
-                             W.q_tile_cap_in, c_in + 2, W.q_unit_cl_in, W.q_unit_cap_in, c_in + 3, side->s))
-        return rc;
+    if (intake) {  // (after the register kernel's launch: the side stream's launches would delay it)
+      if (int rc = intake_fold(SPX_BM_SETUP_FIRST ? 2 : 0)) return rc;
       if (hipEventRecord(side->join, side->s) != hipSuccess) return check_launch("spx_bin_mean join");
     }
   }
@@ -595,7 +612,7 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
   }
   // kept-bin fold of the clusters past the wide kernel (the quorum applies)
   if (int rc = kept_fold(W.def, n_def, W.qmeta, W.q_task_cl, W.q_task_cap, n_qtasks, W.q_tile_cl, W.q_tile_cap,
-                         n_qtiles, W.q_unit_cl, W.q_unit_cap, n_qunits, s))
+                         n_qtiles, W.q_unit_cl, W.q_unit_cap, n_qunits, s, 0))
     return rc;
   // the segmented fold reads what both kept-bin folds passed on
   if (intake && hipStreamWaitEvent(s, side->join, 0) != hipSuccess) return check_launch("spx_bin_mean join");
