@@ -13,6 +13,7 @@ fallback -- without the HIP library it raises (see :mod:`specpride_amd._lib`).
 from __future__ import annotations
 
 import ctypes
+import threading
 from dataclasses import dataclass
 from typing import Optional
 
@@ -46,8 +47,9 @@ def _stream_handle(stream=None) -> Optional[int]:
 PACKED_MAX_BYTES = 64 << 20
 
 
-class _Pinned:
-    """A grow-only pinned host staging buffer (one per direction).  Every copy
+class _Pinned(threading.local):
+    """A grow-only pinned host staging buffer (one per direction and host thread:
+    two threads reading results back at once must not share it).  Every copy
     through it is waited for before the call returns, so it is free again."""
 
     def __init__(self):
