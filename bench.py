@@ -84,6 +84,9 @@ class HipBackend:
     def __init__(self, local: int):
         import torch
 
+        if rehearsal():  # every rank on GPU 0, gloo between them (host-staged P2P)
+            local = 0
+            self.dist_backend = "gloo"
         torch.cuda.set_device(local)
         self.dev = torch.device("cuda", local)
         self.stream = torch.cuda.current_stream()
@@ -169,6 +172,17 @@ class HipBackend:
                     member=np.where(rep >= 0, rep - first, rep))
 
 
+def rehearsal() -> bool:
+    """SPX_BENCH_REHEARSE=1: the multi-GPU step rehearsed on ONE GPU (a profiling and test aid;
+    the pool gives this repo one GPU per box, and RCCL takes one rank per device): every rank
+    runs the HIP engine on GPU 0 and the ranks talk over gloo, the gather's payloads staged
+    through host copies (shard.StepGatherer(stage_host=True)).  Everything but RCCL itself --
+    the split, the per-rank fused steps, the device-side wire pack / unpack, rank 0's
+    reassembly and its bit-for-bit check -- runs as on the node; the timing is not the
+    node's and the line says so."""
+    return os.environ.get("SPX_BENCH_REHEARSE") == "1"
+
+
 def make_backend(local: int):
     """HipBackend, unless SPX_BENCH_BACKEND=module:Class names a test stand-in (the CPU
     suite's launcher test; never set on the GPU box)."""
@@ -208,7 +222,7 @@ def max_over_ranks(x: float, world: int, be) -> float:
 
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=be.dev)
+    t = torch.tensor([x], dtype=torch.float64, device="cpu" if be.dist_backend == "gloo" else be.dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -226,7 +240,7 @@ def launch_ranks(args) -> int:
     import threading
 
     n = args.gpus
-    if not os.environ.get("SPX_BENCH_BACKEND"):
+    if not os.environ.get("SPX_BENCH_BACKEND") and not rehearsal():
         import torch  # device_count() does not initialise HIP on this image
 
         have = torch.cuda.device_count()
@@ -511,7 +525,8 @@ def headline(args, rank, world, local, out, be):
         bufs.append(be.alloc(batch))
         gat = shard.StepGatherer(batch.n_clusters, rank, world, be.dev,
                                  wire_max_count=max(1, be.max_cluster_spectra(batch)),
-                                 wire_ops=getattr(be, "wire_ops", None))
+                                 wire_ops=getattr(be, "wire_ops", None),
+                                 stage_host=be.kind == "hip" and be.dist_backend == "gloo")
         total_c, total_p = gat.plan(kept)
 
     inflight = [None] * len(bufs)  # per buffer: the event of the gather reading it
@@ -576,6 +591,8 @@ def headline(args, rank, world, local, out, be):
                                    "(cost = peaks + n*peaks/64; rank 0, which also rebuilds the gathered peaks, "
                                    "weighted by rank0_weight)" if strong and world > 1
                                    else f"cluster-sharded x{world}"),
+                   "rehearsal": ("SPX_BENCH_REHEARSE=1: every rank on GPU 0, gloo with host-staged P2P -- "
+                                 "not the node's timing" if rehearsal() and world > 1 else None),
                    "launcher": ("bench.py --gpus N (own worker processes)" if os.environ.get("SPX_BENCH_SPAWNED")
                                 else ("external (torchrun)" if world > 1 else "single process")),
                    "gather": ("per-step RCCL gather of reps + compacted consensus peaks to rank 0, "
@@ -969,6 +986,10 @@ def tier3(args, out):
 
 def main():
     args = parse()
+    if rehearsal() and os.environ.get("SPX_BENCH_TRACE_AFTER"):  # where each rank is, if a rehearsal stalls
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["SPX_BENCH_TRACE_AFTER"]), exit=False)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         os.environ["SPX_BENCH_SPAWNED"] = "1"
         sys.exit(launch_ranks(args))

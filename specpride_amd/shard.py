@@ -192,12 +192,17 @@ class StepGatherer:
     the peaks travel as f64 and the P2P ops are the same."""
 
     def __init__(self, n_clusters: int, rank: int, world: int, device, group=None, wire_max_count=None,
-                 wire_ops=None):
+                 wire_ops=None, stage_host: bool = False):
         import torch
 
         from . import engine
 
         self.rank, self.world, self.n, self.group = rank, world, int(n_clusters), group
+        # stage_host (bench.py's one-GPU rehearsal of the multi-GPU step under gloo, whose
+        # point-to-point ops take host tensors): the same device-side pack / unpack, the
+        # payloads staged through host copies around the P2P ops
+        self.stage_host = bool(stage_host)
+        self._host_bufs = {}
         self.dev = torch.device(device)
         self.cuda = self.dev.type == "cuda"
         self.stream = torch.cuda.Stream(device=self.dev) if self.cuda else None
@@ -220,7 +225,8 @@ class StepGatherer:
         import torch
         import torch.distributed as dist
 
-        sizes = torch.tensor([self.n, int(kept_peaks), self.wire_max], dtype=torch.int64, device=self.dev)
+        sizes = torch.tensor([self.n, int(kept_peaks), self.wire_max], dtype=torch.int64,
+                             device="cpu" if self.stage_host else self.dev)
         allsz = [torch.empty_like(sizes) for _ in range(self.world)]
         dist.all_gather(allsz, sizes, group=self.group)
         got = [tuple(int(v) for v in t.cpu()) for t in allsz]
@@ -311,8 +317,13 @@ class StepGatherer:
                     payload = payload[:2] + (torch.zeros(2, dtype=torch.float32, device=self.dev),
                                              torch.zeros(self.wire, dtype=torch.uint8, device=self.dev))
                 ops = [dist.P2POp(dist.isend, one(x), 0, group=self.group) for x in payload]
+            if self.stage_host and ops:
+                ops = self._stage(ops)
             for q in (dist.batch_isend_irecv(ops) if ops else []):
                 q.wait()
+            if self.stage_host and self.rank == 0:
+                for dev_t, host_t in self._recv_pairs:
+                    dev_t.copy_(host_t)
             if self.rank == 0 and self.wire:
                 for r in range(1, self.world):  # rank 0's rebuild of the f64 peaks, on the gather stream
                     p_r = self.recv_sizes[r][1]
@@ -325,6 +336,29 @@ class StepGatherer:
             ev = torch.cuda.Event()
             ev.record(self.stream)
         return ev
+
+    def _stage(self, ops):
+        """stage_host: the P2P ops on host copies -- a sender's payloads copied out once its
+        gather stream has produced them, rank 0's receives into host buffers that launch()
+        copies into the device buffers afterwards (self._recv_pairs)."""
+        import torch
+        import torch.distributed as dist
+
+        if self.stream is not None:
+            self.stream.synchronize()
+        staged, self._recv_pairs = [], []
+        for k, op in enumerate(ops):
+            t = op.tensor
+            if op.op is dist.isend:
+                staged.append(dist.P2POp(dist.isend, t.cpu(), op.peer, group=self.group))
+            else:
+                h = self._host_bufs.get(k)
+                if h is None or h.shape != t.shape or h.dtype != t.dtype:
+                    h = torch.empty(t.shape, dtype=t.dtype)
+                    self._host_bufs[k] = h
+                staged.append(dist.P2POp(dist.irecv, h, op.peer, group=self.group))
+                self._recv_pairs.append((t, h))
+        return staged
 
     def assemble(self, parts: list, cluster_off: np.ndarray, own_bm, own_member) -> dict:
         """Rank 0, after a step's gather has completed: the whole batch's results in

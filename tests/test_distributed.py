@@ -145,13 +145,13 @@ def _step_result(rank, step, n_clusters):
     return _FakeConsensus(count, cap_off, mz, inten), rep
 
 
-def _gatherer_worker(rank, world, port, q):
+def _gatherer_worker(rank, world, port, q, stage_host=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         n = 5 + 3 * rank
         bm, _ = _step_result(rank, 0, n)
-        gat = shard.StepGatherer(n, rank, world, "cpu")
+        gat = shard.StepGatherer(n, rank, world, "cpu", stage_host=stage_host)
         totals = gat.plan(int(bm.count.sum()))
         ok = True
         for step in range(3):
@@ -169,15 +169,15 @@ def _gatherer_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_step_gatherer_gloo(world):
+@pytest.mark.parametrize("world,stage_host", [(2, False), (3, False), (2, True)])
+def test_step_gatherer_gloo(world, stage_host):
     """bench.py's multi-GPU step gather (shard.StepGatherer: sizes exchanged once,
     then per step counts + representatives + compacted peaks point-to-point to
     rank 0) under gloo: rank 0 holds every peer's step results, step after step."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gatherer_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gatherer_worker, args=(r, world, port, q, stage_host)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict((r, (ok, tot)) for r, ok, tot in (q.get(timeout=120) for _ in range(world)))
