@@ -65,16 +65,12 @@ constexpr int GA_UM = SPX_GA_UM;  // m/z values per thread held in registers (10
 #ifndef SPX_GA_WMAXN
 #define SPX_GA_WMAXN 65536  // the wide kernel hands clusters of more peaks than this to the giant pipeline (0: none)
 #endif
-#ifndef SPX_GA_INTAKE
-#define SPX_GA_INTAKE 1  // giants registered up front, their pipeline on a second stream
-#endif
-#ifndef SPX_GA_OWN_N
-#define SPX_GA_OWN_N 65536  // the intake takes every cluster of more peaks than this (16,384: skewed configs[3]
-                            // 15 ms instead of 1.75 -- past the 256 records the global kernel takes them)
-#endif
-#ifndef SPX_GA_OWN_LO
-#define SPX_GA_OWN_LO 32768  // ... and those of more than this while its table has room (0: none)
-#endif
+// the giant intake (spx_gap_average, round 6): every cluster of more than GA_OWN_N peaks
+// is registered up front and its pipeline runs on the call's second stream; those of more
+// than GA_OWN_LO while its table has room (16,384 for all giants measured 15 ms on skewed
+// configs[3] instead of 1.63: past the 256 records the global kernel takes them)
+constexpr int64_t GA_OWN_N = 65536;
+constexpr int64_t GA_OWN_LO = 32768;
 #ifndef SPX_GA_WUM
 #define SPX_GA_WUM 20
 #endif
@@ -1133,10 +1129,7 @@ constexpr int64_t GA_TILE = 2 * GA_BATCH * GA_BLOCK;  // peaks per tile
 // The global kernel's giants (more than 16,384 peaks, deferred by the wide kernel; with
 // the intake, the skewed law's mid-size clusters of a few hundred spectra) are few: their
 // pipeline takes smaller tiles, so its per-tile passes spread over more workgroups
-#ifndef SPX_GA_TILE_LATE
-#define SPX_GA_TILE_LATE 2048
-#endif
-constexpr int64_t GA_TILE_LATE = SPX_GA_TILE_LATE;
+constexpr int64_t GA_TILE_LATE = 2048;
 #ifndef SPX_GA_GGRID
 #define SPX_GA_GGRID 512  // skewed configs[3] gap-average: 1024 4.21 ms, 512 3.77-3.79, 256 3.78-3.80, 4096 6.05
 #endif

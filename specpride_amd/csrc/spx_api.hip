@@ -140,9 +140,6 @@ struct ProfScope {
 // call forks it from the caller's stream with an event and joins it back before returning,
 // so to the caller the call is one stream's worth of ordered work (hipGraph capture
 // included).  The mutex covers one call's fork ... join enqueue, so the shared events pair up.
-#ifndef SPX_SIDE_PRIO
-#define SPX_SIDE_PRIO 1
-#endif
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, mid = nullptr, join = nullptr;
@@ -157,14 +154,8 @@ SideStream* side_stream() {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   SideStream& S = g_side[dev];
   if (!S.s) {
-#if SPX_SIDE_PRIO
-    // the side stream's work is the call's long pole: its workgroups go first
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return nullptr;
-    if (hipStreamCreateWithPriority(&S.s, hipStreamNonBlocking, hi) != hipSuccess) return nullptr;
-#else
+    // (a high-priority stream measured the same: profiles/r06_ga_intake.txt)
     if (hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-#endif
     if (hipEventCreateWithFlags(&S.fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.mid, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.join, hipEventDisableTiming) != hipSuccess)
@@ -365,17 +356,11 @@ struct BinMeanWs {
   int32_t range_cap, q_task_cap, q_tile_cap, q_unit_cap;
 };
 
-#ifndef SPX_BM_INTAKE
-#define SPX_BM_INTAKE 1  // clusters past the wide kernel by size: their kept-bin fold on the side stream
-#endif
-#ifndef SPX_BM_SETUP_FIRST
-#define SPX_BM_SETUP_FIRST 1
-#endif
 // A batch whose largest cluster has more than BM_NMAX spectra may hold clusters the
 // intake takes (bin_mean_past_wide's other tests -- 2^28 peaks, a bin space past BM_WMAX
 // words -- the chain after the wide kernel keeps, as before).
 bool bin_mean_intake_possible(const spx_batch_info* info) {
-  return SPX_BM_INTAKE && info->max_cluster_spectra > spx::BM_NMAX;
+  return info->max_cluster_spectra > spx::BM_NMAX;
 }
 
 // The workspace layout (the size query and the launch use the same carving).
@@ -577,13 +562,11 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
       hipLaunchKernelGGL(spx::bin_mean_intake_kernel, dim3((unsigned)std::min<int64_t>((C + 255) / 256, 1024)),
                          dim3(256), 0, side->s, V, P, W.def_in, c_in);
       if (int rc = check_launch("bin_mean_intake_kernel")) return rc;
-#if SPX_BM_SETUP_FIRST
       // the kept-bin fold's set-up (a few long latency chains: the big clusters' offsets,
       // charges and window) alone on the GPU, before the register kernel fills it
       if (int rc = intake_fold(1)) return rc;
       if (hipEventRecord(side->mid, side->s) != hipSuccess || hipStreamWaitEvent(s, side->mid, 0) != hipSuccess)
         return check_launch("spx_bin_mean set-up event");
-#endif
     }
     if (head) {
       if (int rc = head->launch(head->ctx, V, P, O, prec_out, charge_out, status, W.rest, s)) return rc;
@@ -595,7 +578,7 @@ int bin_mean_impl(const spx_csr* csr, const spx_bin_params* params, const spx_ba
       if (int rc = check_launch("bin_mean_reg_kernel")) return rc;
     }
     if (intake) {  // (after the register kernel's launch: the side stream's launches would delay it)
-      if (int rc = intake_fold(SPX_BM_SETUP_FIRST ? 2 : 0)) return rc;
+      if (int rc = intake_fold(2)) return rc;
       if (hipEventRecord(side->join, side->s) != hipSuccess) return check_launch("spx_bin_mean join");
     }
   }
@@ -781,10 +764,10 @@ int spx_gap_average(const spx_csr* csr, const spx_gap_params* params, const spx_
   // two to leave such clusters alone).  The global kernel waits for the intake (its list
   // takes what the intake's table could not) and hands ITS giants (data-dependent: more
   // than 16,384 peaks and deferred by the wide kernel) to the second table's pipeline.
-  const bool intake = SPX_GA_INTAKE && arena_bytes > 0 && info->max_cluster_peaks > (int64_t)SPX_GA_OWN_N;
-  const int64_t own_n = intake ? (int64_t)SPX_GA_OWN_N : 0;
-  const int64_t own_lo = intake ? (int64_t)SPX_GA_OWN_LO : 0;
-  static_assert(SPX_GA_OWN_N > spx::GA_GIANT_N && (SPX_GA_OWN_LO == 0 || SPX_GA_OWN_LO > spx::GA_GIANT_N),
+  const bool intake = arena_bytes > 0 && info->max_cluster_peaks > spx::GA_OWN_N;
+  const int64_t own_n = intake ? spx::GA_OWN_N : 0;
+  const int64_t own_lo = intake ? spx::GA_OWN_LO : 0;
+  static_assert(spx::GA_OWN_N > spx::GA_GIANT_N && (spx::GA_OWN_LO == 0 || spx::GA_OWN_LO > spx::GA_GIANT_N),
                 "the intake takes giants only");
   std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
   SideStream* side = nullptr;
