@@ -647,10 +647,30 @@ __device__ __forceinline__ void medoid_small_body(const CsrView& v, const Medoid
 
 // Register kernel: one 256-thread workgroup per cluster.  Clusters past its caps
 // go to the wide kernel's list.
+// Whether a cluster goes to the large path by its size alone (spx_api.hip's
+// medoid_large_by_size): more than MD_NMAX spectra, or more peaks than the wide kernel holds.
+__device__ __forceinline__ bool md_large_by_size(const CsrView& v, int64_t s0, int n) {
+  return n > MD_NMAX || v.spec_off[s0 + n] - v.spec_off[s0] > MW_PMAX;
+}
+
+// The medoid intake (spx_medoid, round 6): every cluster large by size deferred up front
+// into a list of its own, so its large path runs on the call's second stream BESIDE the
+// register and wide kernels; the register kernel (own = 1) leaves those clusters alone.
+__global__ __launch_bounds__(256) void medoid_intake_kernel(CsrView v, int64_t* rep, int32_t* deferred,
+                                                            int32_t* n_deferred, MedoidMeta* meta) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < v.n_clusters;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s0 = v.cluster_off[c];
+    const int n = (int)(v.cluster_off[c + 1] - s0);
+    if (md_large_by_size(v, s0, n)) md_defer(c, s0, n, deferred, n_deferred, meta, rep);
+  }
+}
+
 __global__ __launch_bounds__(MD_BLOCK, SPX_MD_MINW) void medoid_reg_kernel(CsrView v, MedoidParams P, int64_t* rep,
-                                                              double* totals_out, StripedList wide) {
+                                                              double* totals_out, StripedList wide, int own) {
   __shared__ MedoidRegSmem<MD_BLOCK, MR_UMAX, MD_KWMAX> L;
-  auto defer = [&](int64_t c, int64_t, int) {
+  auto defer = [&](int64_t c, int64_t s0, int n) {
+    if (own && md_large_by_size(v, s0, n)) return;  // the intake's (its rep is the large path's to write)
     // every leftover via the wide kernel, which passes n > 64 straight on (one
     // list target here keeps the kernel's register budget)
     rep[c] = -4;

@@ -852,7 +852,10 @@ size_t spx_medoid_workspace_size(const int64_t* hco, const int64_t* hso, int64_t
   size_t fixed = align256(sizeof(int32_t)) + align256(sizeof(unsigned long long)) + align256(spx::kListCountBytes) +
                  align256(sizeof(int32_t) * Cm) +
                  align256(sizeof(int32_t) * (size_t)spx::striped_cap((int64_t)Cm) * spx::kListStripes) +
-                 align256(sizeof(spx::MedoidMeta) * Cm) + 5 * align256(sizeof(int64_t) * (Cm + 1));
+                 align256(sizeof(spx::MedoidMeta) * Cm) + 5 * align256(sizeof(int64_t) * (Cm + 1)) +
+                 // the intake's list, records and tile spaces (medoid_impl, part 0)
+                 align256(sizeof(int32_t) * Cm) + align256(sizeof(spx::MedoidMeta) * Cm) +
+                 5 * align256(sizeof(int64_t) * (Cm + 1));
   size_t arena = 0, margin = 0;
   // small clusters with more peaks than the wide kernel has bin words for: the only
   // ones a run can defer into the arena (their arena bytes)
@@ -934,6 +937,11 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
   int64_t* chunk_base = w.take<int64_t>((size_t)C + 1);
   int64_t* xpose_base = w.take<int64_t>((size_t)C + 1);
   int64_t* pk_base = w.take<int64_t>((size_t)C + 1);
+  // the intake's (n_def[1] is its count: zeroed with n_def)
+  int32_t* def_in = w.take<int32_t>((size_t)C);
+  spx::MedoidMeta* meta_in = w.take<spx::MedoidMeta>((size_t)C);
+  int64_t* bases_in[5];
+  for (auto& b : bases_in) b = w.take<int64_t>((size_t)C + 1);
   if (w.used >= workspace_bytes) return fail(SPX_ENOSPACE, "spx_medoid: workspace too small");
   char* arena = w.base + w.used;
   const int64_t arena_bytes = (int64_t)(workspace_bytes - w.used);
@@ -953,50 +961,78 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
     head->P = P;
     return SPX_SUCCESS;
   }
+  // The large path over one list of deferred clusters (`nd`, `mt`, the five tile-space
+  // bases), on stream q.
+  auto large_path = [&](int32_t* nd, spx::MedoidMeta* mt, int64_t* const* bs, hipStream_t q) {
+    int64_t *tile_b = bs[0], *unit_b = bs[1], *chunk_b = bs[2], *xpose_b = bs[3], *pk_b = bs[4];
+    hipLaunchKernelGGL(spx::medoid_units_kernel, dim3(1), blk, 0, q, V, mt, nd, pk_b);
+    if (int rc = check_launch("medoid_units_kernel")) return rc;
+    // the peak passes: a flat grid over MD_PU-peak units of every deferred cluster
+    const dim3 gridu(2048);
+    hipLaunchKernelGGL(spx::medoid_range_kernel, gridu, blk, 0, q, V, P, nd, mt, pk_b, arena, bump, arena_bytes);
+    if (int rc = check_launch("medoid_range_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_l1_kernel, gridu, blk, 0, q, V, P, nd, mt, pk_b, arena);
+    if (int rc = check_launch("medoid_l1_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_plan1_kernel, dim3(g), blk, 0, q, nd, mt, arena, bump, arena_bytes, rep);
+    if (int rc = check_launch("medoid_plan1_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_l2_kernel, gridu, blk, 0, q, V, P, nd, mt, pk_b, arena);
+    if (int rc = check_launch("medoid_l2_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_plan2_kernel, dim3(g), blk, 0, q, nd, mt, arena, bump, arena_bytes, rep);
+    if (int rc = check_launch("medoid_plan2_kernel")) return rc;
+    // row_base reuses pk_base (the peak passes are done with it)
+    int64_t* row_b = pk_b;
+    hipLaunchKernelGGL(spx::medoid_scan_kernel, dim3(1), blk, 0, q, mt, nd, tile_b, unit_b, chunk_b, xpose_b, row_b);
+    if (int rc = check_launch("medoid_scan_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_fill_kernel, grid2, blk, 0, q, V, P, mt, nd, row_b, arena);
+    if (int rc = check_launch("medoid_fill_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_transpose_kernel, dim3(4096), blk, 0, q, mt, nd, xpose_b, arena);
+    if (int rc = check_launch("medoid_transpose_kernel")) return rc;
+    ProfScope prof_gram(2, q);
+    hipLaunchKernelGGL(spx::medoid_gram_reg_kernel, dim3(SPX_GR_GRID), blk, 0, q, mt, nd, tile_b, arena);
+    prof_gram.end();
+    if (int rc = check_launch("medoid_gram_reg_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_leaves_kernel, dim3(4096), blk, 0, q, V, mt, nd, unit_b, arena);
+    if (int rc = check_launch("medoid_leaves_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_combine_kernel, dim3(1024), blk, 0, q, mt, nd, chunk_b, arena, totals);
+    if (int rc = check_launch("medoid_combine_kernel")) return rc;
+    hipLaunchKernelGGL(spx::medoid_argmin_kernel, dim3(g), blk, 0, q, mt, nd, arena, rep);
+    return check_launch("medoid_argmin_kernel");
+  };
+  // The intake (spx_medoid's whole call with the large path): the clusters large by size
+  // are deferred up front and their large path runs on the side stream while the register
+  // and wide kernels take the others on `s`; the register kernel leaves them alone, the wide
+  // kernel's own deferrals take a second large path on `s`, which then waits for the first.
+  const bool intake = part == 0 && params->large_path;
+  std::unique_lock<std::mutex> side_lock(g_side_mu, std::defer_lock);
+  SideStream* side = nullptr;
+  if (intake) {
+    side_lock.lock();
+    side = side_stream();
+    if (!side) return check_launch("spx_medoid side stream");
+    if (hipEventRecord(side->fork, s) != hipSuccess || hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess)
+      return check_launch("spx_medoid fork");
+  }
   if (part == 0) {
     ProfScope prof_reg(1, s);
-    hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, wide);
+    hipLaunchKernelGGL(spx::medoid_reg_kernel, dim3((unsigned)C), blk, 0, s, V, P, rep, totals, wide, intake ? 1 : 0);
     prof_reg.end();
     if (int rc = check_launch("medoid_reg_kernel")) return rc;
+  }
+  if (intake) {  // (after the register kernel's launch: the side stream's launches would delay it)
+    hipLaunchKernelGGL(spx::medoid_intake_kernel, dim3((unsigned)std::min<int64_t>((C + 255) / 256, 1024)), dim3(256),
+                       0, side->s, V, rep, def_in, n_def + 1, meta_in);
+    if (int rc = check_launch("medoid_intake_kernel")) return rc;
+    if (int rc = large_path(n_def + 1, meta_in, bases_in, side->s)) return rc;
+    if (hipEventRecord(side->join, side->s) != hipSuccess) return check_launch("spx_medoid join");
   }
   hipLaunchKernelGGL(spx::medoid_wide_kernel, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(C, 1024))),
                      dim3(spx::MW_BLOCK), 0, s, V, P, rep, totals, wide, def, n_def, meta);
   if (int rc = check_launch("medoid_wide_kernel")) return rc;
   if (!params->large_path) return SPX_SUCCESS;  // deferred clusters keep rep = SPX_REP_DEFERRED
-  hipLaunchKernelGGL(spx::medoid_units_kernel, dim3(1), blk, 0, s, V, meta, n_def, pk_base);
-  if (int rc = check_launch("medoid_units_kernel")) return rc;
-  // the peak passes: a flat grid over MD_PU-peak units of every deferred cluster
-  const dim3 gridu(2048);
-  hipLaunchKernelGGL(spx::medoid_range_kernel, gridu, blk, 0, s, V, P, n_def, meta, pk_base, arena, bump,
-                     arena_bytes);
-  if (int rc = check_launch("medoid_range_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_l1_kernel, gridu, blk, 0, s, V, P, n_def, meta, pk_base, arena);
-  if (int rc = check_launch("medoid_l1_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_plan1_kernel, dim3(g), blk, 0, s, n_def, meta, arena, bump, arena_bytes, rep);
-  if (int rc = check_launch("medoid_plan1_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_l2_kernel, gridu, blk, 0, s, V, P, n_def, meta, pk_base, arena);
-  if (int rc = check_launch("medoid_l2_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_plan2_kernel, dim3(g), blk, 0, s, n_def, meta, arena, bump, arena_bytes, rep);
-  if (int rc = check_launch("medoid_plan2_kernel")) return rc;
-  // row_base reuses pk_base (the peak passes are done with it)
-  int64_t* row_base = pk_base;
-  hipLaunchKernelGGL(spx::medoid_scan_kernel, dim3(1), blk, 0, s, meta, n_def, tile_base, unit_base, chunk_base,
-                     xpose_base, row_base);
-  if (int rc = check_launch("medoid_scan_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_fill_kernel, grid2, blk, 0, s, V, P, meta, n_def, row_base, arena);
-  if (int rc = check_launch("medoid_fill_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_transpose_kernel, dim3(4096), blk, 0, s, meta, n_def, xpose_base, arena);
-  if (int rc = check_launch("medoid_transpose_kernel")) return rc;
-  ProfScope prof_gram(2, s);
-  hipLaunchKernelGGL(spx::medoid_gram_reg_kernel, dim3(SPX_GR_GRID), blk, 0, s, meta, n_def, tile_base, arena);
-  prof_gram.end();
-  if (int rc = check_launch("medoid_gram_reg_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_leaves_kernel, dim3(4096), blk, 0, s, V, meta, n_def, unit_base, arena);
-  if (int rc = check_launch("medoid_leaves_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_combine_kernel, dim3(1024), blk, 0, s, meta, n_def, chunk_base, arena, totals);
-  if (int rc = check_launch("medoid_combine_kernel")) return rc;
-  hipLaunchKernelGGL(spx::medoid_argmin_kernel, dim3(g), blk, 0, s, meta, n_def, arena, rep);
-  return check_launch("medoid_argmin_kernel");
+  int64_t* const bases[5] = {tile_base, unit_base, chunk_base, xpose_base, pk_base};
+  if (int rc = large_path(n_def, meta, bases, s)) return rc;
+  if (intake && hipStreamWaitEvent(s, side->join, 0) != hipSuccess) return check_launch("spx_medoid join");
+  return SPX_SUCCESS;
 }
 
 struct FusedCtx {
