@@ -102,9 +102,11 @@ constexpr const char* kProfNames[] = {"bin_mean_reg_kernel", "medoid_reg_kernel"
 constexpr int kProfN = sizeof(kProfNames) / sizeof(kProfNames[0]);
 struct ProfAcc {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  std::vector<int64_t> calls;  // per pending pair: the call it belongs to
   double ms = 0.0;
-  int64_t launches = 0;
+  int64_t launches = 0, last_call = -1;
 };
+std::atomic<int64_t> g_prof_calls{0};
 std::atomic<bool> g_prof_on{false};
 std::mutex g_prof_mu;
 ProfAcc g_prof[kProfN];
@@ -119,8 +121,12 @@ struct ProfScope {
   int idx = -1;
   hipEvent_t a = nullptr, b = nullptr;
   hipStream_t s = nullptr;
-  ProfScope(int i, hipStream_t st) : s(st) {
+  int64_t call = -1;
+  // `call` >= 0: scopes of one call sharing it count as ONE launch (spx_medoid's two large
+  // paths, one per stream: the Gram time of the call is their sum)
+  ProfScope(int i, hipStream_t st, int64_t call_id = -1) : s(st), call(call_id) {
     if (!g_prof_on.load(std::memory_order_relaxed)) return;
+    if (call < 0) call = g_prof_calls.fetch_add(1);
     if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
     if (hipEventRecord(a, s) != hipSuccess) return;
     idx = i;
@@ -130,6 +136,7 @@ struct ProfScope {
     if (hipEventRecord(b, s) == hipSuccess) {
       std::lock_guard<std::mutex> lock(g_prof_mu);
       g_prof[idx].pending.emplace_back(a, b);
+      g_prof[idx].calls.push_back(call);
     }
     idx = -1;
   }
@@ -278,16 +285,19 @@ int spx_profile_read(const char* kernel, double* total_ms, int64_t* launches) {
   if (i < 0 || !total_ms || !launches) return fail(SPX_EINVAL, "spx_profile_read: unknown kernel or null output");
   std::lock_guard<std::mutex> lock(g_prof_mu);
   ProfAcc& p = g_prof[i];
-  for (auto& ab : p.pending) {
+  for (size_t k = 0; k < p.pending.size(); ++k) {
+    auto& ab = p.pending[k];
     float ms = 0.0f;
     if (hipEventSynchronize(ab.second) == hipSuccess && hipEventElapsedTime(&ms, ab.first, ab.second) == hipSuccess) {
       p.ms += ms;
-      ++p.launches;
+      if (p.calls[k] != p.last_call) ++p.launches;  // a call's scopes are recorded back to back
+      p.last_call = p.calls[k];
     }
     (void)hipEventDestroy(ab.first);
     (void)hipEventDestroy(ab.second);
   }
   p.pending.clear();
+  p.calls.clear();
   *total_ms = p.ms;
   *launches = p.launches;
   return SPX_SUCCESS;
@@ -963,6 +973,7 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
   }
   // The large path over one list of deferred clusters (`nd`, `mt`, the five tile-space
   // bases), on stream q.
+  const int64_t prof_call = g_prof_calls.fetch_add(1);  // both large paths' Gram time: one launch of the call
   auto large_path = [&](int32_t* nd, spx::MedoidMeta* mt, int64_t* const* bs, hipStream_t q) {
     int64_t *tile_b = bs[0], *unit_b = bs[1], *chunk_b = bs[2], *xpose_b = bs[3], *pk_b = bs[4];
     hipLaunchKernelGGL(spx::medoid_units_kernel, dim3(1), blk, 0, q, V, mt, nd, pk_b);
@@ -987,7 +998,7 @@ int medoid_impl(const spx_csr* csr, const spx_medoid_params* params, int64_t* re
     if (int rc = check_launch("medoid_fill_kernel")) return rc;
     hipLaunchKernelGGL(spx::medoid_transpose_kernel, dim3(4096), blk, 0, q, mt, nd, xpose_b, arena);
     if (int rc = check_launch("medoid_transpose_kernel")) return rc;
-    ProfScope prof_gram(2, q);
+    ProfScope prof_gram(2, q, prof_call);
     hipLaunchKernelGGL(spx::medoid_gram_reg_kernel, dim3(SPX_GR_GRID), blk, 0, q, mt, nd, tile_b, arena);
     prof_gram.end();
     if (int rc = check_launch("medoid_gram_reg_kernel")) return rc;
