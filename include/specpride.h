@@ -142,7 +142,8 @@ typedef struct spx_gap_params {
  * NaN): such a cluster is OK, possibly with NaN/inf values or no peaks, never an
  * error status (average_spectrum_clustering.py:59-98).
  * With clusters past 65,536 peaks in the batch, the giants' pipeline runs on a second
- * stream the library owns (one per device), forked from `stream` by an event and
+ * stream the library owns (one per device; spx_bin_mean's kept-bin fold of clusters past
+ * 128 spectra and spx_medoid's large path use it the same way), forked from `stream` by an event and
  * joined back to it before the call returns: the call stays ordered on `stream`,
  * hipGraph capture of `stream` included. */
 size_t spx_gap_average_workspace_size(const spx_csr *csr, const spx_gap_params *params,
